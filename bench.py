@@ -1,0 +1,234 @@
+"""NNGP fused B/F + log-likelihood sweep benchmark (BASELINE.json headline).
+
+One step = one sweep over this rank's shard of locations: the gfx950 kernel
+builds every location's (m+1)x(m+1) joint covariance block, factors it, writes
+B (rows, m) and F (rows,), and reduces the log-likelihood partials; with more
+than one rank the partials are all-gathered over RCCL and summed in rank order.
+
+Workload (BASELINE.json configs[2], the headline): N = 1,000,000 locations per
+GPU (weak scaling: N_total = 1e6 x world), m = 15, exponential covariance
+(sigma2 = 1, phi = 30, tau2 = 0), synthetic uniform [0,1]^2 coordinates and
+N(0,1) values from numpy default_rng(0).  Inputs and neighbour
+sets are resident in HBM before timing; the one-off neighbour build is timed
+separately (``neighbor_build_s``).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from pynngp_amd import Covariance, ShardedLogLik, _lib  # noqa: E402
+from pynngp_amd.sweep import combine_partials  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (MI355X_MICROARCH.md chip table)
+FP64_PEAK = 78.6e12  # FLOP/s, MI355X fp64 vector spec
+METRIC = "NNGP log-lik sweeps/sec (N=1M, m=15) at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def bytes_per_location(m):
+    # 4m idx + 16 own coord + 16m nbr coords + 8 own value + 8m nbr values + (8m + 8) B, F writes
+    return 36 * m + 32
+
+
+def flops_per_location(m):
+    # Cholesky m^3/3 + solves 2m^2 + covariance fill 4.5 m(m+1) + 4m
+    return m ** 3 / 3 + 2 * m ** 2 + 4.5 * m * (m + 1) + 4 * m
+
+
+def synth(n_total, seed=0):
+    rng = np.random.default_rng(seed)
+    coords = rng.uniform(0.0, 1.0, (n_total, 2))
+    values = rng.standard_normal(n_total)
+    return coords, values
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(coords, values, nbr_host, kind, theta, budget_s, F_gpu):
+    """C oracle (oracle/nngp_oracle.c, OpenMP) on a bounded sample of the same workload."""
+    from oracle import nngp_oracle as O
+
+    threads = O.load_c_oracle().oracle_num_threads()
+    rows_done, t_cpu = 0, 0.0
+    chunk = 50_000
+    max_dF = 0.0
+    r0 = 0
+    n = nbr_host.shape[0]
+    while t_cpu < budget_s and r0 < n:
+        r1 = min(n, r0 + chunk)
+        t = time.perf_counter()
+        _, Fo, _ = O.c_bf_sweep(coords, nbr_host[r0:r1], kind, theta, values, i0=r0)
+        t_cpu += time.perf_counter() - t
+        max_dF = max(max_dF, float(np.max(np.abs(F_gpu[r0:r1] - Fo) / Fo)))
+        rows_done += r1 - r0
+        r0 = r1
+        chunk = min(400_000, chunk * 2)
+    return {
+        "value": rows_done / t_cpu,
+        "unit": "locations/s",
+        "cores": int(threads),
+        "kind": "port",
+        "sample": f"rows 0..{rows_done} of the same field, one fused B/F+loglik pass, C oracle (OpenMP, "
+                  f"{threads} threads, {cpu_model()}) in {t_cpu:.2f} s",
+        "parity_max_rel_dF": max_dF,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=1_000_000, help="locations per GPU")
+    ap.add_argument("--m", type=int, default=15)
+    ap.add_argument("--kind", default="exponential", choices=["exponential", "matern32"])
+    ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
+    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--pmc-traffic", type=float, default=None,
+                    help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    sigma2, phi, tau2 = (float(x) for x in args.theta.split(","))
+    cov = Covariance(args.kind, sigma2, phi, tau2)
+    n_total = args.n * world
+    coords, values = synth(n_total, seed=0)
+    c = torch.from_numpy(coords).to(dev)
+    v = torch.from_numpy(values).to(dev)
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo)
+    torch.cuda.synchronize()
+    knn_s = time.perf_counter() - t0
+    want_bf = not args.loglik_only
+    rows = sweep.hi - sweep.lo
+
+    for _ in range(args.warmup):
+        sweep.partials(cov, v, want_bf)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        local = sweep.local_partials(cov, v, want_bf)
+        ev[k][1].record(stream)
+        combine_partials(local, world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    p = sweep.partials(cov, v, want_bf).cpu().numpy()
+    ll = -0.5 * (n_total * np.log(2 * np.pi) + p[0] + p[1])
+
+    if rank == 0:
+        bpl = bytes_per_location(args.m) if want_bf else bytes_per_location(args.m) - 8 * args.m - 8
+        achieved = bpl * rows / (kern_ms * 1e-3)
+        fpl = flops_per_location(args.m)
+        traffic = args.pmc_traffic
+        out = {
+            "metric": METRIC,
+            "value": n_total * args.steps / elapsed,
+            "unit": "locations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "sweeps_per_s": args.steps / elapsed,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: uniform [0,1]^2 coords + N(0,1) values, numpy default_rng(0)",
+            "config": {
+                "workload": "BASELINE config 3: fused B/F + log-lik sweep, N=1,000,000 locations per GPU, m=15, "
+                            "exponential covariance" if (args.n == 1_000_000 and args.m == 15
+                                                         and args.kind == "exponential") else
+                            f"fused B/F + log-lik sweep, N={args.n} per GPU, m={args.m}, {args.kind}",
+                "n_per_gpu": args.n,
+                "n_total": n_total,
+                "m": args.m,
+                "kind": args.kind,
+                "theta": [sigma2, phi, tau2],
+                "algo": args.algo,
+                "write_BF": want_bf,
+                "global_batch": n_total,
+                "parallelism": f"dp{world} (contiguous location shards, all-gather of 4 partials per sweep)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved / 1e9,
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK,
+                "traffic": traffic,
+                "algorithmic_bytes_per_location": bpl,
+                "kernel_ms": kern_ms,
+                "kernel_rows": rows,
+            },
+            "roofline_fp64": {
+                "achieved": fpl * rows / (kern_ms * 1e-3) / 1e12,
+                "peak": FP64_PEAK / 1e12,
+                "unit": "TFLOP/s",
+                "frac": fpl * rows / (kern_ms * 1e-3) / FP64_PEAK,
+                "algorithmic_flops_per_location": fpl,
+            },
+            "neighbor_build_s": knn_s,
+            "loglik": ll,
+            "bad_rows": [int(p[2]), int(p[3])],
+            "lib": os.path.relpath(_lib.LIB_PATH, ROOT),
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            F_gpu = sweep.F.cpu().numpy() if want_bf else None
+            if F_gpu is None:
+                _, F_t, _ = _lib.bf_sweep(c, sweep.nbr, 0, cov.kind, *cov.theta)
+                F_gpu = F_t.cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(coords, values, sweep.nbr.cpu().numpy(), args.kind,
+                                               (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

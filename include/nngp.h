@@ -1,0 +1,110 @@
+/*
+ * nngp.h -- C ABI of libnngp_hip.so, the MI355X (gfx950) NNGP hot path.
+ *
+ * The reference (bwpriest/pyNNGP) exposes this path only as Python methods of
+ * class NNGP; there is no FFI in it.  Each entry point below names the reference
+ * interface it replaces (file:line under /root/reference).  The Python binding
+ * (pynngp_amd/_lib.py, ctypes) and the torch custom ops (pynngp_amd/ops.py) are
+ * thin layers over exactly these symbols; INTEGRATION.md shows the binding a
+ * pyNNGP maintainer would add.
+ *
+ * Conventions
+ *   - Every pointer argument except the host-side `partials_host` of
+ *     nngp_loglik_from_partials is a DEVICE pointer (hipMalloc / torch CUDA
+ *     tensor memory); the caller owns every buffer.
+ *   - `stream` is a hipStream_t (NULL = default stream).  All work is
+ *     stream-ordered; no call synchronises the host, allocates, or frees.
+ *   - Coordinates are fp64 (n_points, 2) row-major; neighbour sets are int32
+ *     (rows, m) row-major, padded with -1 (row i holds min(i, m) indices).
+ *   - Return 0 on success or a negative NNGP_E* code (nngp_last_error() gives
+ *     the message).  Numerical failures are data, not return codes, because the
+ *     work is asynchronous: see `partials` of nngp_bf_sweep.
+ */
+#ifndef NNGP_H
+#define NNGP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NNGP_OK 0
+#define NNGP_EINVAL (-1)    /* bad argument (shape, range, null pointer, small workspace) */
+#define NNGP_EHIP (-3)      /* a HIP runtime call or kernel launch failed */
+#define NNGP_EUNSUP (-4)    /* unsupported configuration (e.g. m > 63) */
+
+#define NNGP_COV_EXPONENTIAL 0 /* sigma2 * exp(-phi d)                  */
+#define NNGP_COV_MATERN32 1    /* sigma2 * (1 + phi d) * exp(-phi d)      */
+
+#define NNGP_ALGO_AUTO 0 /* lane kernel for m <= 16, wave kernel above */
+#define NNGP_ALGO_LANE 1 /* one lane per location (m <= 16)           */
+#define NNGP_ALGO_WAVE 2 /* one wavefront per location (m <= 63)      */
+
+#define NNGP_MAX_M 63
+
+/* Library version string, e.g. "pynngp_amd 0.1.0 gfx950". */
+const char *nngp_version(void);
+
+/* Message for the last error returned on the calling thread. */
+const char *nngp_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Neighbour sets.
+ * Replaces NNGP._make_s_neighbor_sets, pyNNGP/nngp.py:49-62 (a sklearn KDTree
+ * rebuilt on s[0:i] for every i; ordering key sklearn euclidean_rdist64,
+ * sklearn/metrics/_dist_metrics.pxd:26-40).
+ * For every query row i in [q0, q1): the k = min(m, i) nearest points among
+ * coords[0:i], ascending fp64 rdist = (0 + t0*t0) + t1*t1 (no FMA), exact
+ * ties by lower index, written to nbr[(i - q0) * m + s], s < k; -1 beyond.
+ * Requires n_points <= INT32_MAX, 0 <= m <= 64, 0 <= q0 <= q1 <= n_points.
+ * ------------------------------------------------------------------------- */
+size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m);
+int nngp_knn_prior(const double *coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t *nbr,
+                   void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Unrestricted k-nearest neighbours of query points among a reference set.
+ * Replaces the sklearn searches behind NNGP._init_ws (pyNNGP/nngp.py:45-47,
+ * KNeighborsRegressor(n_neighbors=5).fit(t, y).predict(s)) and
+ * NNGP._make_t_neighbor_sets (nngp.py:64-71, KDTree(s).query(t, m)).
+ * nbr[q * k + s] = index into ref of the s-th nearest point to query[q]
+ * ((rdist, index) order, self included when a query point is in ref), -1 for
+ * s >= n_ref.  Workspace: nngp_knn_workspace_bytes(n_ref, k).
+ * ------------------------------------------------------------------------- */
+int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_t n_query, int32_t k, int32_t *nbr,
+                   void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused B/F + log-likelihood sweep over locations i0 .. i0 + n_rows - 1.
+ * Replaces the per-location stubs of class NNGP:
+ *   _CNs  nngp.py:78-82   C_{N(s_i)}       (covariance among the neighbours, + tau2 I)
+ *   _Ccross nngp.py:84-86 C_{s_i, N(s_i)}  (location vs neighbours)
+ *   _Cs   nngp.py:92-96   C_{s_i, s_i}     (sigma2 + tau2)
+ *   _Bsi  nngp.py:73-76   B_i = C_{s_i,N} C_N^{-1}       -> B (n_rows, m), 0 in -1 slots
+ *   _Fsi  nngp.py:88-90   F_i = C_ii - B_i C_{N,s_i}     -> F (n_rows,)
+ * and the log-likelihood sweep consumed by oneSample (nngp.py:98-101, absent):
+ *   partials[0] = sum_i log F_i
+ *   partials[1] = sum_i (v_i - B_i v_N(i))^2 / F_i        (0 when values == NULL)
+ *   partials[2] = first location index whose Cholesky pivot or F_i is not > 0, else -1
+ *   partials[3] = first location index with a neighbour index >= n_points, else -1
+ *   log-lik = -1/2 (n_rows log 2 pi + partials[0] + partials[1]).
+ * Rows flagged in partials[2] get B = F = NaN.  The sum order is fixed, so the
+ * partials are bit-reproducible run to run.
+ * coords: (n_points, 2); nbr: (n_rows, m); values: (n_points,) or NULL;
+ * B, F: may be NULL (log-lik only); partials: 4 doubles.
+ * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, algo) bytes, 256-B aligned.
+ * ------------------------------------------------------------------------- */
+size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo);
+int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, int64_t n_rows, int32_t m, int64_t i0,
+                  int32_t kind, double sigma2, double phi, double tau2, const double *values, double *B, double *F,
+                  double *partials, void *workspace, size_t workspace_bytes, int32_t algo, void *stream);
+
+/* Host helper: -1/2 (n_rows log 2 pi + p[0] + p[1]) from host-resident partials. */
+double nngp_loglik_from_partials(const double *partials_host, int64_t n_rows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NNGP_H */

@@ -1,0 +1,203 @@
+/*
+ * C restatement of the NNGP neighbour-set + B/F + log-likelihood path.
+ *
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py as the checker / timed CPU baseline.  The product
+ * (pynngp_amd, libnngp_hip.so) never links or calls it.
+ *
+ * Reference (bwpriest/pyNNGP, /root/reference):
+ *   oracle_knn_prior  <- NNGP._make_s_neighbor_sets, pyNNGP/nngp.py:49-62
+ *                        (sklearn 1.7.2 KDTree.query, sort_results=True; key is
+ *                         euclidean_rdist64, sklearn/metrics/_dist_metrics.pxd:26-40)
+ *   oracle_bf_sweep   <- _CNs nngp.py:78-82, _Ccross :84-86, _Cs :92-96,
+ *                        _Bsi :73-76, _Fsi :88-90 (stubs in the reference; NNGP
+ *                        definitions of SURVEY.md Appendix A)
+ * Same math as oracle/nngp_oracle.py; that file's header states the pinning.
+ *
+ * Compiled with -ffp-contract=off so rdist is (0 + t0*t0) + t1*t1 exactly as
+ * sklearn's x86-64 build computes it (no FMA).  Ties: lower index first.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+static inline int key_less(double da, int64_t ia, double db, int64_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+/* nngp.py:49-62 -- brute force over j < i, kept sorted by (rdist, j). */
+int oracle_knn_prior(const double *coords, int64_t n, int32_t m, int64_t q0, int64_t q1, int32_t *nbr) {
+    if (m < 0 || q0 < 0 || q1 > n || q0 > q1) return -1;
+    if (m == 0) return 0;
+#pragma omp parallel
+    {
+        double *bd = (double *)malloc(sizeof(double) * (size_t)m);
+        int64_t *bi = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = q0; i < q1; ++i) {
+            int32_t *row = nbr + (i - q0) * m;
+            int64_t k = i < m ? i : m;
+            int64_t cnt = 0;
+            const double qx = coords[2 * i], qy = coords[2 * i + 1];
+            for (int64_t j = 0; j < i; ++j) {
+                double t0 = qx - coords[2 * j];
+                double t1 = qy - coords[2 * j + 1];
+                double d = 0.0;
+                d += t0 * t0;
+                d += t1 * t1;
+                if (cnt == k && !key_less(d, j, bd[k - 1], bi[k - 1])) continue;
+                int64_t s = cnt < k ? cnt++ : k - 1;
+                while (s > 0 && key_less(d, j, bd[s - 1], bi[s - 1])) {
+                    bd[s] = bd[s - 1];
+                    bi[s] = bi[s - 1];
+                    --s;
+                }
+                bd[s] = d;
+                bi[s] = j;
+            }
+            for (int64_t s = 0; s < m; ++s) row[s] = s < k ? (int32_t)bi[s] : -1;
+        }
+        free(bd);
+        free(bi);
+    }
+    return 0;
+}
+
+static inline double cov_eval(int kind, double d, double sigma2, double phi) {
+    double e = exp(-phi * d);
+    if (kind == 1) return sigma2 * (1.0 + phi * d) * e;
+    return sigma2 * e;
+}
+
+static inline double pdist(const double *a, const double *b) {
+    double dx = a[0] - b[0], dy = a[1] - b[1];
+    return sqrt(dx * dx + dy * dy);
+}
+
+/*
+ * Per location: C_N (+tau2 I), c, C_ii -> Cholesky C_N = L L^T (row-oriented),
+ * v = L^-1 c, B = L^-T v, F = C_ii - v.v, r = v_i - B.v_N.
+ * partials[0] = sum log F, partials[1] = sum r^2/F (index order),
+ * partials[2] = first row index whose pivot or F is not > 0 (or -1).
+ * A slot is valid iff its index is >= 0; invalid slots give B = 0.
+ */
+int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t m, int32_t kind,
+                    const double *theta, const double *values, double *Bout, double *Fout, double *partials,
+                    int64_t i0, int64_t i1) {
+    if (m < 0 || i0 < 0 || i1 > n || i0 > i1 || (kind != 0 && kind != 1)) return -1;
+    const double sigma2 = theta[0], phi = theta[1], tau2 = theta[2];
+    const int64_t rows = i1 - i0;
+    double *logF = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1));
+    double *quad = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1));
+    int64_t first_bad = INT64_MAX;
+#pragma omp parallel
+    {
+        const int mm = m > 0 ? m : 1;
+        double *L = (double *)malloc(sizeof(double) * (size_t)mm * mm);
+        double *c = (double *)malloc(sizeof(double) * (size_t)mm);
+        double *v = (double *)malloc(sizeof(double) * (size_t)mm);
+        double *b = (double *)malloc(sizeof(double) * (size_t)mm);
+        int *slot = (int *)malloc(sizeof(int) * (size_t)mm);
+        int64_t bad_local = INT64_MAX;
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < rows; ++r) {
+            const int64_t i = i0 + r;
+            const int32_t *row = nbr + r * m;
+            int k = 0;
+            int bad = 0;
+            for (int s = 0; s < m; ++s)
+                if (row[s] >= 0) {
+                    if (row[s] >= n) bad = 1;
+                    slot[k++] = s;
+                }
+            const double *xi = coords + 2 * i;
+            double F = sigma2 + tau2;
+            double rr = bad ? NAN : (values ? values[i] : 0.0);
+            if (!bad) {
+                for (int a = 0; a < k; ++a) {
+                    const double *xa = coords + 2 * (int64_t)row[slot[a]];
+                    for (int bb = 0; bb < a; ++bb) {
+                        const double *xb = coords + 2 * (int64_t)row[slot[bb]];
+                        L[a * k + bb] = cov_eval(kind, pdist(xa, xb), sigma2, phi);
+                    }
+                    L[a * k + a] = sigma2 + tau2;
+                    c[a] = cov_eval(kind, pdist(xi, xa), sigma2, phi);
+                }
+                /* Cholesky (Cholesky-Banachiewicz, row by row) */
+                for (int a = 0; a < k && !bad; ++a) {
+                    for (int bb = 0; bb <= a; ++bb) {
+                        double s = L[a * k + bb];
+                        for (int q = 0; q < bb; ++q) s -= L[a * k + q] * L[bb * k + q];
+                        if (bb == a) {
+                            if (!(s > 0.0)) { bad = 1; break; }
+                            L[a * k + a] = sqrt(s);
+                        } else {
+                            L[a * k + bb] = s / L[bb * k + bb];
+                        }
+                    }
+                }
+            }
+            if (!bad) {
+                for (int a = 0; a < k; ++a) { /* v = L^-1 c */
+                    double s = c[a];
+                    for (int q = 0; q < a; ++q) s -= L[a * k + q] * v[q];
+                    v[a] = s / L[a * k + a];
+                }
+                for (int a = k - 1; a >= 0; --a) { /* B = L^-T v */
+                    double s = v[a];
+                    for (int q = a + 1; q < k; ++q) s -= L[q * k + a] * b[q];
+                    b[a] = s / L[a * k + a];
+                }
+                double vv = 0.0, bv = 0.0;
+                for (int a = 0; a < k; ++a) vv += v[a] * v[a];
+                F = (sigma2 + tau2) - vv;
+                if (values)
+                    for (int a = 0; a < k; ++a) bv += b[a] * values[row[slot[a]]];
+                rr = values ? values[i] - bv : 0.0;
+                if (!(F > 0.0)) bad = 1;
+            }
+            if (Bout) {
+                double *brow = Bout + r * m;
+                for (int s = 0; s < m; ++s) brow[s] = 0.0;
+                for (int a = 0; a < k; ++a) brow[slot[a]] = bad ? NAN : b[a];
+            }
+            if (bad) {
+                F = NAN;
+                if (i < bad_local) bad_local = i;
+            }
+            if (Fout) Fout[r] = F;
+            logF[r] = log(F);
+            quad[r] = rr * rr / F;
+        }
+#pragma omp critical
+        if (bad_local < first_bad) first_bad = bad_local;
+        free(L);
+        free(c);
+        free(v);
+        free(b);
+        free(slot);
+    }
+    double s0 = 0.0, s1 = 0.0;
+    for (int64_t r = 0; r < rows; ++r) {
+        s0 += logF[r];
+        s1 += quad[r];
+    }
+    partials[0] = s0;
+    partials[1] = s1;
+    partials[2] = first_bad == INT64_MAX ? -1.0 : (double)first_bad;
+    free(logF);
+    free(quad);
+    return 0;
+}

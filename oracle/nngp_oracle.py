@@ -1,0 +1,277 @@
+"""CPU oracle for the NNGP neighbour-set + B/F + log-likelihood path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in ``pynngp_amd`` imports this module; only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+use it, and only as the checker / the timed CPU baseline -- never as the thing
+measured or shipped.
+
+What it restates (reference = ``bwpriest/pyNNGP`` at ``/root/reference``):
+
+* ``knn_prior`` -- ``NNGP._make_s_neighbor_sets`` (``pyNNGP/nngp.py:49-62``): for
+  every i the ``min(m, i)`` nearest points among ``s[0:i]``, ascending distance,
+  self excluded, ``Ns[0] == []``.  The reference delegates to sklearn 1.7.2
+  ``KDTree.query(k, sort_results=True)`` whose ordering key is the fp64 reduced
+  distance ``rdist = (0 + t0*t0) + t1*t1`` with ``t = x_query - x_tree`` and no
+  FMA (``sklearn/metrics/_dist_metrics.pxd:26-40``).  Exact ties are broken by
+  the lower index here (the reference's tie order is arbitrary:
+  ``sklearn/utils/_heap.pyx:45-47``); pinned by ``tests/golden/knn_ref_*.npz``.
+* ``bf_sweep`` -- the per-location algebra the reference stubs out:
+  ``_CNs`` (``nngp.py:78-82``), ``_Ccross`` (``nngp.py:84-86``), ``_Cs``
+  (``nngp.py:92-96``), ``_Bsi`` (``nngp.py:73-76``), ``_Fsi`` (``nngp.py:88-90``),
+  with the NNGP definitions named by those docstrings (Datta et al. 2016;
+  SURVEY.md Appendix A)::
+
+      C_N  = [C(s_a, s_b)]_{a,b in N(i)} + tau2 I
+      c    = [C(s_i, s_b)]_{b in N(i)}
+      C_ii = sigma2 + tau2
+      B_i  = c^T C_N^{-1}          F_i = C_ii - c^T C_N^{-1} c
+      log p(v) = -1/2 sum_i [log 2pi + log F_i + (v_i - B_i v_N(i))^2 / F_i]
+
+  B/F/log-lik are "parity unpinned" by the reference (its methods return None);
+  this restatement is pinned by known answers instead (``tests/test_oracle.py``):
+  m = N-1 equals the dense-GP log density, m = 0 the independent normal, and the
+  result is invariant to permuting a neighbour set.
+
+Covariance kinds (the reference's ``cov`` plug-in, ``nngp.py:6,12``):
+``exponential`` C(d) = sigma2 exp(-phi d); ``matern32``
+C(d) = sigma2 (1 + phi d) exp(-phi d); d is Euclidean distance in fp64.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+KINDS = {"exponential": 0, "matern32": 1}
+LOG_2PI = float(np.log(2.0 * np.pi))
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------
+# neighbour sets (nngp.py:49-62)
+# ----------------------------------------------------------------------------
+def rdist_to_prior(coords: np.ndarray, i: int) -> np.ndarray:
+    """sklearn euclidean_rdist64 of s_i against s[0:i] (``_dist_metrics.pxd:26-40``)."""
+    t = coords[i][None, :] - coords[:i]
+    t0 = t[:, 0]
+    t1 = t[:, 1]
+    return (0.0 + t0 * t0) + t1 * t1  # separate ufuncs: no FMA contraction
+
+
+def knn_prior(coords: np.ndarray, m: int, q0: int = 0, q1: int | None = None) -> np.ndarray:
+    """Ordered prior nearest neighbours, int32 (q1-q0, m) padded with -1."""
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    n = coords.shape[0]
+    q1 = n if q1 is None else q1
+    out = np.full((q1 - q0, m), -1, dtype=np.int32)
+    for i in range(q0, q1):
+        if i == 0 or m == 0:
+            continue
+        d = rdist_to_prior(coords, i)
+        k = min(m, i)
+        if k < i:
+            part = np.argpartition(d, k - 1)[:k]
+            # include every index tied with the k-th value so (rdist, idx) order is exact
+            kth = d[part].max()
+            cand = np.nonzero(d <= kth)[0]
+        else:
+            cand = np.arange(i)
+        order = np.lexsort((cand, d[cand]))[:k]
+        out[i - q0, :k] = cand[order]
+    return out
+
+
+def knn_all(query: np.ndarray, ref: np.ndarray, k: int) -> np.ndarray:
+    """k nearest of every query among all ref points (self included), (rdist, idx) order."""
+    out = np.empty((query.shape[0], k), dtype=np.int64)
+    for q in range(query.shape[0]):
+        t = query[q][None, :] - ref
+        d = (0.0 + t[:, 0] * t[:, 0]) + t[:, 1] * t[:, 1]
+        out[q] = np.lexsort((np.arange(ref.shape[0]), d))[:k]
+    return out
+
+
+def ws_init(t: np.ndarray, y: np.ndarray, s: np.ndarray, k: int = 5) -> np.ndarray:
+    """``_init_ws`` (``nngp.py:45-47``): uniform k-NN regression of y on t at s."""
+    idx = knn_all(s, t, k)
+    return y[idx].mean(axis=1)
+
+
+# ----------------------------------------------------------------------------
+# covariance plug-in and per-location algebra (nngp.py:73-96)
+# ----------------------------------------------------------------------------
+def cov_fn(kind: str, d: np.ndarray, sigma2: float, phi: float) -> np.ndarray:
+    if kind == "exponential":
+        return sigma2 * np.exp(-phi * d)
+    if kind == "matern32":
+        pd = phi * d
+        return sigma2 * (1.0 + pd) * np.exp(-pd)
+    raise ValueError(f"unknown covariance kind {kind!r}")
+
+
+def _pair_dist(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    dx = a[..., 0] - b[..., 0]
+    dy = a[..., 1] - b[..., 1]
+    return np.sqrt(dx * dx + dy * dy)
+
+
+def location_blocks(coords, nbr_row, i, kind, theta):
+    """(C_N, c, C_ii) for one location: ``_CNs``, ``_Ccross``, ``_Cs``."""
+    sigma2, phi, tau2 = theta
+    idx = nbr_row[nbr_row >= 0].astype(np.int64)
+    xs = coords[idx]
+    CN = cov_fn(kind, _pair_dist(xs[:, None, :], xs[None, :, :]), sigma2, phi)
+    CN = CN + tau2 * np.eye(idx.size)
+    c = cov_fn(kind, _pair_dist(coords[i][None, :], xs), sigma2, phi)
+    return CN, c, sigma2 + tau2
+
+
+def bf_location(coords, nbr_row, i, kind, theta):
+    """(B_i over the valid slots, F_i) by Cholesky, ``_Bsi`` / ``_Fsi``."""
+    CN, c, Cii = location_blocks(coords, nbr_row, i, kind, theta)
+    if c.size == 0:
+        return np.zeros(0), Cii
+    L = np.linalg.cholesky(CN)
+    v = np.linalg.solve(L, c)
+    B = np.linalg.solve(L.T, v)
+    return B, Cii - v @ v
+
+
+def bf_sweep(coords, nbr, kind, theta, values=None, i0=0):
+    """Batched fp64 restatement over rows ``i0 .. i0+len(nbr)``.
+
+    Returns ``(B (n, m) padded with 0, F (n,), partials)`` with
+    ``partials = [sum log F, sum r^2/F]`` (r = v_i - B_i v_N(i); 0 without values).
+    Rows are grouped by their valid-neighbour pattern so numpy's batched
+    Cholesky does the work; the math is the per-location ``bf_location``.
+    """
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    nbr = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, m = nbr.shape
+    sigma2, phi, tau2 = theta
+    B = np.zeros((n, m))
+    F = np.empty(n)
+    valid = nbr >= 0
+    k_row = valid.sum(axis=1)
+    # rows whose valid slots are not a prefix are handled one by one
+    prefix = np.all(valid == (np.arange(m)[None, :] < k_row[:, None]), axis=1)
+    rows_i = np.arange(n) + i0
+    for k in np.unique(k_row[prefix]):
+        sel = np.nonzero(prefix & (k_row == k))[0]
+        if k == 0:
+            F[sel] = sigma2 + tau2
+            continue
+        idx = nbr[sel, :k].astype(np.int64)
+        xs = coords[idx]  # (b, k, 2)
+        CN = cov_fn(kind, _pair_dist(xs[:, :, None, :], xs[:, None, :, :]), sigma2, phi)
+        CN = CN + tau2 * np.eye(k)[None]
+        c = cov_fn(kind, _pair_dist(coords[rows_i[sel]][:, None, :], xs), sigma2, phi)
+        L = np.linalg.cholesky(CN)
+        v = np.linalg.solve(L, c[..., None])
+        Bk = np.linalg.solve(np.swapaxes(L, 1, 2), v)[..., 0]
+        B[sel, :k] = Bk
+        F[sel] = (sigma2 + tau2) - np.einsum("bi,bi->b", v[..., 0], v[..., 0])
+    for r in np.nonzero(~prefix)[0]:
+        Bi, Fi = bf_location(coords, nbr[r], rows_i[r], kind, theta)
+        B[r, valid[r]] = Bi
+        F[r] = Fi
+    logF = np.log(F)
+    if values is None:
+        quad = np.zeros(n)
+    else:
+        values = np.asarray(values, dtype=np.float64)
+        vn = np.where(valid, values[np.where(valid, nbr, 0)], 0.0)
+        resid = values[rows_i] - np.einsum("bi,bi->b", B, vn)
+        quad = resid * resid / F
+    partials = np.array([logF.sum(), quad.sum()])
+    return B, F, partials
+
+
+def loglik_from_partials(partials, n):
+    return -0.5 * (n * LOG_2PI + partials[0] + partials[1])
+
+
+def nngp_loglik(coords, nbr, kind, theta, values):
+    _, _, p = bf_sweep(coords, nbr, kind, theta, values)
+    return loglik_from_partials(p, nbr.shape[0])
+
+
+def dense_gp_loglik(coords, kind, theta, values):
+    """Exact GP log density (known answer for m = N-1)."""
+    sigma2, phi, tau2 = theta
+    d = _pair_dist(coords[:, None, :], coords[None, :, :])
+    C = cov_fn(kind, d, sigma2, phi) + tau2 * np.eye(coords.shape[0])
+    L = np.linalg.cholesky(C)
+    z = np.linalg.solve(L, values)
+    n = coords.shape[0]
+    return -0.5 * (n * LOG_2PI + 2.0 * np.log(np.diag(L)).sum() + z @ z)
+
+
+# ----------------------------------------------------------------------------
+# C restatement (oracle/nngp_oracle.c) through ctypes
+# ----------------------------------------------------------------------------
+_C = None
+
+
+def c_oracle_path() -> str:
+    return os.path.join(_HERE, "_build", "libnngp_oracle.so")
+
+
+def build_c_oracle() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return c_oracle_path()
+
+
+def load_c_oracle():
+    global _C
+    if _C is not None:
+        return _C
+    path = c_oracle_path()
+    if not os.path.exists(path):
+        build_c_oracle()
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.oracle_knn_prior.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, P]
+    lib.oracle_knn_prior.restype = ctypes.c_int
+    lib.oracle_bf_sweep.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P,
+                                    ctypes.c_int64, ctypes.c_int64]
+    lib.oracle_bf_sweep.restype = ctypes.c_int
+    lib.oracle_num_threads.restype = ctypes.c_int
+    _C = lib
+    return lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def c_knn_prior(coords, m, q0=0, q1=None):
+    lib = load_c_oracle()
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    n = coords.shape[0]
+    q1 = n if q1 is None else q1
+    out = np.full((q1 - q0, m), -1, dtype=np.int32)
+    rc = lib.oracle_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle_knn_prior failed: {rc}")
+    return out
+
+
+def c_bf_sweep(coords, nbr, kind, theta, values=None, i0=0, want_bf=True):
+    """C restatement; returns (B, F, partials[3]) with partials[2] = first bad row or -1."""
+    lib = load_c_oracle()
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    nbr = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, m = nbr.shape
+    th = np.ascontiguousarray(theta, dtype=np.float64)
+    vals = None if values is None else np.ascontiguousarray(values, dtype=np.float64)
+    B = np.zeros((n, m)) if want_bf else None
+    F = np.zeros(n) if want_bf else None
+    partials = np.zeros(3)
+    rc = lib.oracle_bf_sweep(_ptr(coords), _ptr(nbr), coords.shape[0], m, KINDS[kind], _ptr(th), _ptr(vals),
+                             _ptr(B), _ptr(F), _ptr(partials), i0, i0 + n)
+    if rc != 0:
+        raise RuntimeError(f"oracle_bf_sweep failed: {rc}")
+    return B, F, partials

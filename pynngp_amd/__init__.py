@@ -1,0 +1,19 @@
+"""pynngp_amd -- MI355X-native NNGP neighbour sets, B/F sweep and log-likelihood.
+
+Drop-in for the hot path of bwpriest/pyNNGP (``pyNNGP.NNGP``); see DESIGN.md.
+The compute runs in ``_build/libnngp_hip.so`` (hand-written gfx950 HIP kernels
+behind the C ABI of ``include/nngp.h``); importing this package does not load
+it -- the first call that needs it does, and fails loudly if it is missing.
+"""
+from ._lib import NNGPExtensionError, LIB_PATH, version  # noqa: F401
+from .nngp import NNGP, Covariance, NNGPNumericalError  # noqa: F401
+from .sweep import ShardedLogLik, shard_range, combine_partials  # noqa: F401
+
+__version__ = "0.1.0"
+
+
+def load_ops():
+    """Register ``torch.ops.nngp.*`` (imports torch.library custom ops)."""
+    from . import ops  # noqa: F401
+
+    return ops

@@ -1,0 +1,200 @@
+"""ctypes binding of ``libnngp_hip.so`` (the C ABI in ``include/nngp.h``).
+
+This is the only place that touches the native library.  It loads the in-tree
+build (``pynngp_amd/_build/libnngp_hip.so``, made by ``__graft_entry__.build()``
+or ``make -C pynngp_amd/csrc``) and fails loudly when it is missing or when a
+tensor is not on a ROCm GPU: there is no CPU fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Tuple
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libnngp_hip.so")
+SYMBOLS = (
+    "nngp_version",
+    "nngp_last_error",
+    "nngp_knn_workspace_bytes",
+    "nngp_knn_prior",
+    "nngp_knn_query",
+    "nngp_bf_sweep_workspace_bytes",
+    "nngp_bf_sweep",
+    "nngp_loglik_from_partials",
+)
+
+KIND_CODES = {"exponential": 0, "matern32": 1}
+ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2}
+MAX_M = 63
+
+
+class NNGPExtensionError(RuntimeError):
+    """The native library is missing, failed to load, or returned an error."""
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NNGPExtensionError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C pynngp_amd/csrc` (pynngp_amd has no CPU fallback)"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, D, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
+    lib.nngp_version.restype = ctypes.c_char_p
+    lib.nngp_last_error.restype = ctypes.c_char_p
+    lib.nngp_knn_workspace_bytes.argtypes = [I64, I32]
+    lib.nngp_knn_workspace_bytes.restype = SZ
+    lib.nngp_knn_prior.argtypes = [P, I64, I32, I64, I64, P, P, SZ, P]
+    lib.nngp_knn_prior.restype = ctypes.c_int
+    lib.nngp_knn_query.argtypes = [P, I64, P, I64, I32, P, P, SZ, P]
+    lib.nngp_knn_query.restype = ctypes.c_int
+    lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
+    lib.nngp_bf_sweep_workspace_bytes.restype = SZ
+    lib.nngp_bf_sweep.argtypes = [P, I64, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_sweep.restype = ctypes.c_int
+    lib.nngp_loglik_from_partials.argtypes = [P, I64]
+    lib.nngp_loglik_from_partials.restype = D
+    _lib = lib
+    return lib
+
+
+def version() -> str:
+    return load().nngp_version().decode()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().nngp_last_error().decode()
+        raise NNGPExtensionError(f"{what} failed ({rc}): {msg}")
+
+
+def _require_gpu(*tensors: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise NNGPExtensionError(
+                f"pynngp_amd needs ROCm GPU tensors (got {t.device}); there is no CPU fallback"
+            )
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise NNGPExtensionError(f"tensors on different devices: {dev} vs {t.device}")
+    if dev is None:
+        raise NNGPExtensionError("no tensor arguments")
+    return dev
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _workspace(nbytes: int, dev: torch.device) -> torch.Tensor:
+    # torch's caching allocator returns >= 512-byte aligned blocks
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+
+
+def _as_coords(coords: torch.Tensor) -> torch.Tensor:
+    if coords.dim() != 2 or coords.shape[1] != 2 or coords.dtype != torch.float64:
+        raise ValueError(f"coords must be float64 (N, 2), got {tuple(coords.shape)} {coords.dtype}")
+    return coords.contiguous()
+
+
+def knn_prior(coords: torch.Tensor, m: int, q0: int = 0, q1: Optional[int] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Ordered prior neighbour sets for rows [q0, q1): int32 (q1-q0, m), -1 padded.
+
+    Replaces ``NNGP._make_s_neighbor_sets`` (pyNNGP/nngp.py:49-62).
+    """
+    coords = _as_coords(coords)
+    dev = _require_gpu(coords)
+    n = coords.shape[0]
+    q1 = n if q1 is None else int(q1)
+    if not 0 <= q0 <= q1 <= n:
+        raise ValueError(f"query rows [{q0}, {q1}) outside [0, {n})")
+    if out is None:
+        out = torch.empty((q1 - q0, m), dtype=torch.int32, device=dev)
+    lib = load()
+    ws = _workspace(lib.nngp_knn_workspace_bytes(n, m), dev)
+    _check(lib.nngp_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out), _ptr(ws), ws.numel(), _stream(dev)),
+           "nngp_knn_prior")
+    return out
+
+
+def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
+    """k nearest reference points of every query point (no prior restriction).
+
+    int32 (n_query, k) in (rdist, index) order; -1 padded when k > n_ref.  Used for
+    ``_init_ws`` (pyNNGP/nngp.py:45-47, sklearn KNeighborsRegressor(5)) and the
+    off-reference sets of ``_make_t_neighbor_sets`` (nngp.py:64-71).
+    """
+    ref = _as_coords(ref)
+    query = _as_coords(query)
+    dev = _require_gpu(ref, query)
+    out = torch.empty((query.shape[0], k), dtype=torch.int32, device=dev)
+    lib = load()
+    ws = _workspace(lib.nngp_knn_workspace_bytes(ref.shape[0], k), dev)
+    _check(lib.nngp_knn_query(_ptr(ref), ref.shape[0], _ptr(query), query.shape[0], k, _ptr(out), _ptr(ws),
+                              ws.numel(), _stream(dev)), "nngp_knn_query")
+    return out
+
+
+def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2: float, phi: float,
+             tau2: float = 0.0, values: Optional[torch.Tensor] = None, want_bf: bool = True,
+             algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
+             partials: Optional[torch.Tensor] = None,
+             workspace: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+    """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
+
+    Returns ``(B, F, partials)`` (B, F None when ``want_bf`` is False); partials is a
+    float64 device tensor ``[sum log F, sum r^2/F, first bad-pivot row, first bad-index row]``.
+    Stream-ordered on torch's current stream; no host synchronisation.
+    """
+    coords = _as_coords(coords)
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
+    nbr = nbr.contiguous()
+    if values is not None:
+        if values.dtype != torch.float64 or values.shape != (coords.shape[0],):
+            raise ValueError("values must be float64 (N,)")
+        values = values.contiguous()
+    dev = _require_gpu(coords, nbr, values)
+    rows, m = nbr.shape
+    if kind not in KIND_CODES:
+        raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
+    lib = load()
+    a = ALGO_CODES[algo]
+    if want_bf:
+        B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
+        F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
+    else:
+        B = F = None
+    partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
+    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
+    if workspace is None or workspace.numel() < need:
+        workspace = _workspace(need, dev)
+    _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), rows, m, i0, KIND_CODES[kind],
+                             float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F),
+                             _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
+           "nngp_bf_sweep")
+    return B, F, partials
+
+
+def bf_workspace(rows: int, m: int, algo: str, device) -> torch.Tensor:
+    """Pre-allocate a sweep workspace (reuse it across calls in a hot loop)."""
+    return _workspace(load().nngp_bf_sweep_workspace_bytes(rows, m, ALGO_CODES[algo]), torch.device(device))

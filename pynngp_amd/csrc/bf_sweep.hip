@@ -1,0 +1,339 @@
+// NNGP B/F + log-likelihood sweep on gfx950 (CDNA4).
+//
+// Reference path (bwpriest/pyNNGP, /root/reference; stubs there):
+//   _CNs(i)    nngp.py:78-82  C_{N(s_i)}            -> rows/cols 0..m-1 of the joint block
+//   _Ccross(i) nngp.py:84-86  C_{s_i,N(s_i)}        -> row m of the joint block
+//   _Cs(i)     nngp.py:92-96  C_{s_i,s_i}           -> entry (m, m)
+//   _Bsi(i)    nngp.py:73-76  B_i = c^T C_N^{-1}    -> back-substitution on L_N
+//   _Fsi(i)    nngp.py:88-90  F_i = C_ii - c^T C_N^{-1} c -> last pivot of the joint block
+// plus the log-likelihood sweep the reference never wrote.
+//
+// Formulation: factor the (m+1)x(m+1) joint block
+//   J = [[C_N + tau2 I, c], [c^T, sigma2 + tau2]]   with the value column [v_N; v_i]
+// appended.  After m right-looking elimination steps the last row of L holds
+// v = L_N^{-1} c, the last pivot is F_i and the last entry of the value column
+// is r_i = v_i - B_i v_N(i).  B_i = L_N^{-T} v needs one more back-solve.
+// Neighbour slots with index -1 become identity rows (decoupled, exact).
+//
+// Two kernels, same math, same outputs:
+//   bf_lane<M>   one LANE per location, the whole joint block in VGPRs, fully
+//                unrolled for a compile-time M <= 16.  64 locations per wave;
+//                every lane does useful fp64 work on every instruction.
+//   bf_wave<NR>  one WAVE per location (the north_star layout): lane a owns row a
+//                of the joint block in VGPRs; column values are broadcast with
+//                v_readlane.  Any M <= 63.  Generic path / comparison point.
+// Both write one (sum log F, sum r^2/F) pair per wave into a workspace slab;
+// bf_finalize sums the slab in a fixed order (bit-reproducible).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nngp_math.h"
+#include "nngp_internal.h"
+
+namespace nngp {
+
+// --------------------------------------------------------------------------
+// one lane per location
+// --------------------------------------------------------------------------
+template <int M>
+__global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coords, int64_t n_points,
+                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0,
+                                               int kind, double sigma2, double phi, double tau2,
+                                               const double* __restrict__ values, double* __restrict__ Bout,
+                                               double* __restrict__ Fout, double* __restrict__ wpart,
+                                               unsigned long long* __restrict__ status) {
+    constexpr int N1 = M + 1;  // joint block order
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = r < n_rows;
+    const int64_t rr = live ? r : n_rows - 1;
+    const int64_t i = i0 + rr;
+
+    bool valid[M];
+    int32_t idx[M];
+    bool bad_index = false;
+#pragma unroll
+    for (int a = 0; a < M; ++a) {
+        const int32_t j = nbr[rr * M + a];
+        const bool v = j >= 0 && (int64_t)j < n_points;
+        bad_index |= j >= 0 && !v;
+        valid[a] = v;
+        idx[a] = v ? j : 0;
+    }
+    double px[N1], py[N1], z[N1];
+#pragma unroll
+    for (int a = 0; a < M; ++a) {
+        const double2 x = coords[idx[a]];
+        px[a] = x.x;
+        py[a] = x.y;
+        z[a] = (values != nullptr && valid[a]) ? values[idx[a]] : 0.0;
+    }
+    {
+        const double2 x = coords[i];
+        px[M] = x.x;
+        py[M] = x.y;
+        z[M] = values != nullptr ? values[i] : 0.0;
+    }
+
+    // joint block, lower triangle (A[a][b], b <= a)
+    double A[N1][N1];
+    const double diag = sigma2 + tau2;
+#pragma unroll
+    for (int a = 0; a < N1; ++a) {
+        const bool va = a < M ? valid[a] : true;
+#pragma unroll
+        for (int b = 0; b < a; ++b) {
+            const double c = nngp_cov(kind, nngp_dist(px[a], py[a], px[b], py[b]), sigma2, phi);
+            A[a][b] = (va && valid[b]) ? c : 0.0;
+        }
+        A[a][a] = va ? diag : 1.0;
+    }
+
+    // right-looking elimination of the M neighbour columns
+    double inv[M > 0 ? M : 1];
+    bool bad = false;
+#pragma unroll
+    for (int p = 0; p < M; ++p) {
+        bad |= !(A[p][p] > 0.0);
+        const double ip = nngp_rsqrt(A[p][p]);
+        inv[p] = ip;
+        A[p][p] *= ip;  // L[p][p] = sqrt(pivot)
+#pragma unroll
+        for (int a = p + 1; a < N1; ++a) A[a][p] *= ip;
+        z[p] *= ip;
+#pragma unroll
+        for (int a = p + 1; a < N1; ++a) {
+#pragma unroll
+            for (int b = p + 1; b <= a; ++b) A[a][b] = fma(-A[a][p], A[b][p], A[a][b]);
+            z[a] = fma(-A[a][p], z[p], z[a]);
+        }
+    }
+    const double F = A[M][M];
+    const double res = z[M];
+    bad |= !(F > 0.0);
+
+    if (Bout != nullptr) {
+        double bb[M > 0 ? M : 1];
+#pragma unroll
+        for (int a = M - 1; a >= 0; --a) {
+            double s = A[M][a];
+#pragma unroll
+            for (int q = a + 1; q < M; ++q) s = fma(-A[q][a], bb[q], s);
+            bb[a] = s * inv[a];
+        }
+        if (live) {
+#pragma unroll
+            for (int a = 0; a < M; ++a) Bout[rr * M + a] = valid[a] ? (bad ? NAN : bb[a]) : 0.0;
+        }
+    }
+    if (Fout != nullptr && live) Fout[rr] = bad ? NAN : F;
+
+    double lf = 0.0, q = 0.0;
+    if (live) {
+        lf = log(F);
+        q = res * res / F;
+        if (bad) atomicMin(status + 0, (unsigned long long)i);
+        if (bad_index) atomicMin(status + 1, (unsigned long long)i);
+    }
+    wave_partials_store(lf, q, wpart, r);
+}
+
+// --------------------------------------------------------------------------
+// one wave per location; lane a owns row a of the joint block (NR >= M+1 rows)
+// --------------------------------------------------------------------------
+template <int NR>
+__global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
+                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0, int M,
+                                               int kind, double sigma2, double phi, double tau2,
+                                               const double* __restrict__ values, double* __restrict__ Bout,
+                                               double* __restrict__ Fout, double* __restrict__ wpart,
+                                               unsigned long long* __restrict__ status) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
+    const double diag = sigma2 + tau2;
+
+    for (int64_t rr = wave; rr < n_rows; rr += n_waves) {
+        const int64_t i = i0 + rr;
+        // lane a < M: neighbour slot a; lane M: the location itself; lanes > M: identity rows
+        int32_t j = -1;
+        if (lane < M) j = nbr[rr * M + lane];
+        const bool is_self = lane == M;
+        const bool in_range = j >= 0 && (int64_t)j < n_points;
+        const bool bad_index = j >= 0 && !in_range;
+        const bool valid = is_self || in_range;
+        const int64_t src = is_self ? i : (in_range ? (int64_t)j : 0);
+        const double2 x = coords[src];
+        double zv = (values != nullptr && valid) ? values[src] : 0.0;
+        const unsigned long long vmask = __ballot(valid);
+
+        // row `lane` of the joint block (entries b <= lane are meaningful)
+        double row[NR];
+#pragma unroll
+        for (int b = 0; b < NR; ++b) {
+            const double bx = wave_bcast(x.x, b);
+            const double by = wave_bcast(x.y, b);
+            const bool vb = (vmask >> b) & 1ull;
+            const double c = nngp_cov(kind, nngp_dist(x.x, x.y, bx, by), sigma2, phi);
+            double v = (valid && vb) ? c : 0.0;
+            if (b == lane) v = valid ? diag : 1.0;
+            row[b] = v;
+        }
+        bool bad = false;
+        double ip_mine = 1.0;  // lane p keeps 1/L[p][p]
+#pragma unroll
+        for (int p = 0; p < NR - 1; ++p) {
+            if (p < M) {
+                const double piv = wave_bcast(row[p], p);
+                bad |= !(piv > 0.0);
+                const double ip = nngp_rsqrt(piv);
+                if (lane == p) ip_mine = ip;
+                row[p] *= ip;  // lane > p: L[lane][p]; lane p: sqrt(pivot)
+                const double l = row[p];
+                if (lane == p) zv *= ip;
+                const double zp = wave_bcast(zv, p);
+                if (lane > p) zv = fma(-l, zp, zv);
+#pragma unroll
+                for (int b = p + 1; b < NR; ++b) {
+                    if (b <= M) {
+                        const double lb = wave_bcast(l, b);
+                        if (lane >= b) row[b] = fma(-l, lb, row[b]);
+                    }
+                }
+            }
+        }
+        double F = 0.0;
+#pragma unroll
+        for (int b = 0; b < NR; ++b)
+            if (b == M) F = wave_bcast(row[b], M);
+        const double res = wave_bcast(zv, M);
+        bad |= !(F > 0.0);
+        if (Bout != nullptr) {
+            // B = L_N^{-T} v with v = row M of L; lane a ends with b_a
+            double bmine = 0.0;
+#pragma unroll
+            for (int a = NR - 2; a >= 0; --a) {
+                if (a < M) {
+                    const double term = (lane > a && lane < M) ? row[a] * bmine : 0.0;
+                    const double va = wave_bcast(row[a], M);
+                    const double s = va - wave_sum(term);
+                    const double ipa = wave_bcast(ip_mine, a);
+                    if (lane == a) bmine = s * ipa;
+                }
+            }
+            if (lane < M) Bout[rr * M + lane] = in_range ? (bad ? NAN : bmine) : 0.0;
+        }
+        if (lane == 0) {
+            if (Fout != nullptr) Fout[rr] = bad ? NAN : F;
+            lf_acc += log(F);
+            q_acc += res * res / F;
+            if (bad) atomicMin(status + 0, (unsigned long long)i);
+        }
+        if (__any(bad_index) && lane == 0) atomicMin(status + 1, (unsigned long long)i);
+    }
+    if (lane == 0) {
+        wpart[2 * wave] = lf_acc;
+        wpart[2 * wave + 1] = q_acc;
+    }
+}
+
+// --------------------------------------------------------------------------
+// fixed-order reduction of the per-wave partial slab -> partials[4]
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ wpart, int64_t n_waves,
+                                                    const unsigned long long* __restrict__ status,
+                                                    double* __restrict__ partials) {
+    __shared__ double s0[1024], s1[1024];
+    const int t = threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int64_t w = t; w < n_waves; w += 1024) {
+        a += wpart[2 * w];
+        b += wpart[2 * w + 1];
+    }
+    s0[t] = a;
+    s1[t] = b;
+    __syncthreads();
+    for (int off = 512; off > 0; off >>= 1) {
+        if (t < off) {
+            s0[t] += s0[t + off];
+            s1[t] += s1[t + off];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        partials[0] = s0[0];
+        partials[1] = s1[0];
+        partials[2] = status[0] == ~0ull ? -1.0 : (double)status[0];
+        partials[3] = status[1] == ~0ull ? -1.0 : (double)status[1];
+    }
+}
+
+// --------------------------------------------------------------------------
+// launch
+// --------------------------------------------------------------------------
+template <int M>
+static hipError_t launch_lane(const BfArgs& a, hipStream_t s) {
+    const int64_t blocks = (a.n_rows + 255) / 256;
+    hipLaunchKernelGGL(bf_lane<M>, dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords, a.n_points,
+                       a.nbr, a.n_rows, a.i0, a.kind, a.sigma2, a.phi, a.tau2, a.values, a.B, a.F, a.wpart,
+                       a.status);
+    return hipGetLastError();
+}
+
+template <int NR>
+static hipError_t launch_wave(const BfArgs& a, int64_t n_waves, hipStream_t s) {
+    hipLaunchKernelGGL(bf_wave<NR>, dim3((unsigned)(n_waves / 4)), dim3(256), 0, s, (const double2*)a.coords,
+                       a.n_points, a.nbr, a.n_rows, a.i0, a.m, a.kind, a.sigma2, a.phi, a.tau2, a.values, a.B, a.F,
+                       a.wpart, a.status);
+    return hipGetLastError();
+}
+
+int64_t bf_lane_waves(int64_t n_rows) { return (n_rows + 255) / 256 * 4; }
+
+int64_t bf_wave_waves(int64_t n_rows) {
+    // persistent grid: at most 256 CUs x 8 waves x 4, at least one wave per location
+    int64_t w = n_rows < 8192 ? n_rows : 8192;
+    w = (w + 3) / 4 * 4;
+    return w < 4 ? 4 : w;
+}
+
+hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (a.n_rows == 0) {  // empty shard: partials = [0, 0, -1, -1]
+        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, (int64_t)0, a.status, a.partials);
+        return hipGetLastError();
+    }
+    if (algo == kAlgoLane) {
+        switch (a.m) {
+#define NNGP_LANE_CASE(MM) \
+    case MM:               \
+        e = launch_lane<MM>(a, s); \
+        break;
+            NNGP_LANE_CASE(1) NNGP_LANE_CASE(2) NNGP_LANE_CASE(3) NNGP_LANE_CASE(4) NNGP_LANE_CASE(5)
+            NNGP_LANE_CASE(6) NNGP_LANE_CASE(7) NNGP_LANE_CASE(8) NNGP_LANE_CASE(9) NNGP_LANE_CASE(10)
+            NNGP_LANE_CASE(11) NNGP_LANE_CASE(12) NNGP_LANE_CASE(13) NNGP_LANE_CASE(14) NNGP_LANE_CASE(15)
+            NNGP_LANE_CASE(16)
+#undef NNGP_LANE_CASE
+            default:
+                return hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, bf_lane_waves(a.n_rows), a.status,
+                           a.partials);
+        return hipGetLastError();
+    }
+    const int64_t nw = bf_wave_waves(a.n_rows);
+    if (a.m + 1 <= 16)
+        e = launch_wave<16>(a, nw, s);
+    else if (a.m + 1 <= 32)
+        e = launch_wave<32>(a, nw, s);
+    else if (a.m + 1 <= 64)
+        e = launch_wave<64>(a, nw, s);
+    else
+        return hipErrorInvalidValue;
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, nw, a.status, a.partials);
+    return hipGetLastError();
+}
+
+}  // namespace nngp

@@ -1,0 +1,139 @@
+// C ABI of libnngp_hip.so (declared in include/nngp.h): argument checking,
+// workspace carving and launch.  No host synchronisation, allocation or free.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/nngp.h"
+#include "nngp_internal.h"
+
+namespace {
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(NNGP_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int resolve_algo(int32_t algo, int32_t m) {
+    if (algo == NNGP_ALGO_AUTO) return (m >= 1 && m <= nngp::kLaneMaxM) ? nngp::kAlgoLane : nngp::kAlgoWave;
+    return algo;
+}
+
+int64_t bf_waves(int64_t n_rows, int algo) {
+    return algo == nngp::kAlgoLane ? nngp::bf_lane_waves(n_rows) : nngp::bf_wave_waves(n_rows);
+}
+}  // namespace
+
+extern "C" {
+
+const char* nngp_version(void) { return "pynngp_amd 0.1.0 gfx950"; }
+
+const char* nngp_last_error(void) { return g_err; }
+
+double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
+    return -0.5 * ((double)n_rows * 1.8378770664093453 + p[0] + p[1]);
+}
+
+size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
+    if (n_rows < 0) return 0;
+    const int a = resolve_algo(algo, m);
+    const int64_t nw = n_rows > 0 ? bf_waves(n_rows, a) : 0;
+    return align256(16) + align256((size_t)nw * 2 * sizeof(double));
+}
+
+int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, int64_t n_rows, int32_t m, int64_t i0,
+                  int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
+                  double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
+    if (coords == nullptr || partials == nullptr || workspace == nullptr)
+        return fail(NNGP_EINVAL, "coords, partials and workspace must be non-null");
+    if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
+    if (m > 0 && n_rows > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null for m > 0");
+    if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_points)
+        return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
+                    (long long)n_points);
+    if (kind != NNGP_COV_EXPONENTIAL && kind != NNGP_COV_MATERN32) return fail(NNGP_EINVAL, "unknown kind %d", kind);
+    if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
+        return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
+    if ((B == nullptr) != (F == nullptr)) return fail(NNGP_EINVAL, "B and F must both be given or both be null");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    int a = resolve_algo(algo, m);
+    if (a != nngp::kAlgoLane && a != nngp::kAlgoWave) return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
+        return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
+    const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, algo);
+    if (workspace_bytes < need)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
+
+    hipStream_t s = (hipStream_t)stream;
+    char* w = (char*)workspace;
+    unsigned long long* status = (unsigned long long*)w;
+    double* wpart = (double*)(w + align256(16));
+    hipError_t e = hipMemsetAsync(status, 0xff, 2 * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(status)");
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, values, B, F,
+                      partials, wpart, status};
+    e = nngp::bf_launch(args, a, s);
+    if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
+    return NNGP_OK;
+}
+
+size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m) {
+    (void)m;
+    if (n_points < 1 || n_points > INT32_MAX) return 0;
+    nngp::KnnPlan p;
+    if (nngp::knn_plan(n_points, &p) != hipSuccess) return 0;
+    return p.total_bytes;
+}
+
+int nngp_knn_prior(const double* coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t* nbr,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+    if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
+    if (n_points < 1 || n_points > INT32_MAX) return fail(NNGP_EINVAL, "n_points=%lld outside [1, 2^31)", (long long)n_points);
+    if (m < 0 || m > 64) return fail(NNGP_EUNSUP, "m=%d outside [0, 64]", m);
+    if (q0 < 0 || q1 < q0 || q1 > n_points) return fail(NNGP_EINVAL, "query rows [%lld, %lld) invalid", (long long)q0, (long long)q1);
+    if (q1 > q0 && m > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    nngp::KnnPlan plan;
+    hipError_t e = nngp::knn_plan(n_points, &plan);
+    if (e != hipSuccess) return hip_fail(e, "knn plan");
+    if (workspace_bytes < plan.total_bytes)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
+    if (q1 == q0 || m == 0) return NNGP_OK;
+    e = nngp::knn_launch(true, coords, n_points, m, coords, q0, q1, nbr, workspace, plan, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "knn_prior launch");
+    return NNGP_OK;
+}
+
+int nngp_knn_query(const double* ref, int64_t n_ref, const double* query, int64_t n_query, int32_t k, int32_t* nbr,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+    if (ref == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "ref and workspace must be non-null");
+    if (n_ref < 1 || n_ref > INT32_MAX) return fail(NNGP_EINVAL, "n_ref=%lld outside [1, 2^31)", (long long)n_ref);
+    if (k < 0 || k > 64) return fail(NNGP_EUNSUP, "k=%d outside [0, 64]", k);
+    if (n_query < 0) return fail(NNGP_EINVAL, "n_query < 0");
+    if (n_query > 0 && k > 0 && (query == nullptr || nbr == nullptr))
+        return fail(NNGP_EINVAL, "query and nbr must be non-null");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    nngp::KnnPlan plan;
+    hipError_t e = nngp::knn_plan(n_ref, &plan);
+    if (e != hipSuccess) return hip_fail(e, "knn plan");
+    if (workspace_bytes < plan.total_bytes)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
+    if (n_query == 0 || k == 0) return NNGP_OK;
+    e = nngp::knn_launch(false, ref, n_ref, k, query, 0, n_query, nbr, workspace, plan, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "knn_query launch");
+    return NNGP_OK;
+}
+
+}  // extern "C"

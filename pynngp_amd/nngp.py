@@ -1,0 +1,259 @@
+"""Drop-in ``NNGP`` class (mirrors ``pyNNGP.NNGP``, /root/reference/pyNNGP/nngp.py).
+
+Same constructor ``NNGP(t, y, eps, refType, m, cov)`` (nngp.py:6-18), same
+attributes ``t, y, eps, refType, m, cov, s, wt, ws, Ns, Nt`` and the same
+per-location methods ``_Bsi, _CNs, _Ccross, _Fsi, _Cs`` (nngp.py:73-96) -- but the
+neighbour sets, the B/F algebra and the log-likelihood run on the MI355X through
+``libnngp_hip.so``.  Additions: the device-resident ``nbr`` / ``B`` / ``F`` arrays
+and ``loglik()``, the sweep the reference's ``oneSample`` (nngp.py:98-101) needs.
+
+Differences from the reference, all deliberate:
+* ``cov`` is a :class:`Covariance` (kind + theta) for the device path; a plain
+  Python callable is still accepted and used by ``_CNs/_Ccross/_Cs`` with the
+  coordinate convention (the reference passes index arrays at nngp.py:82, a
+  bug), but ``_Bsi/_Fsi/loglik`` need a :class:`Covariance` because the kernel
+  fuses the covariance.  ``cov=None`` (the reference test) builds neighbour sets only.
+* exact distance ties are ordered by lower index (the reference's is arbitrary).
+* tuple ``refType`` values raise ``NotImplementedError`` (the reference raises
+  ``AttributeError`` at nngp.py:34); an unknown string raises ``ValueError``
+  (the reference silently leaves ``s`` unset, nngp.py:29-31).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Callable, Optional, Union
+
+import numpy as np
+import torch
+
+from . import _lib
+
+LOG_2PI = math.log(2.0 * math.pi)
+
+
+@dataclasses.dataclass(frozen=True)
+class Covariance:
+    """Parent-GP covariance plug-in (the reference's ``cov``, nngp.py:6,12).
+
+    ``exponential``: sigma2 exp(-phi d); ``matern32``: sigma2 (1 + phi d) exp(-phi d);
+    ``tau2`` is a nugget added to the diagonal (response model; 0 = latent model).
+    Called as ``cov(a, b)`` on coordinate rows (numpy or torch), it returns the
+    cross-covariance matrix without the nugget, like a reference plug-in would.
+    """
+
+    kind: str
+    sigma2: float
+    phi: float
+    tau2: float = 0.0
+
+    def __post_init__(self):
+        if self.kind not in _lib.KIND_CODES:
+            raise ValueError(f"unknown covariance kind {self.kind!r}; expected one of {sorted(_lib.KIND_CODES)}")
+        if not (self.sigma2 > 0 and self.phi > 0 and self.tau2 >= 0):
+            raise ValueError("need sigma2 > 0, phi > 0, tau2 >= 0")
+
+    @property
+    def theta(self):
+        return (float(self.sigma2), float(self.phi), float(self.tau2))
+
+    def replace(self, **kw) -> "Covariance":
+        return dataclasses.replace(self, **kw)
+
+    def __call__(self, a, b):
+        lib = torch if isinstance(a, torch.Tensor) else np
+        a = a.reshape(-1, 2)
+        b = b.reshape(-1, 2)
+        dx = a[:, None, 0] - b[None, :, 0]
+        dy = a[:, None, 1] - b[None, :, 1]
+        pd = self.phi * lib.sqrt(dx * dx + dy * dy)
+        e = self.sigma2 * lib.exp(-pd)
+        return e * (1.0 + pd) if self.kind == "matern32" else e
+
+
+CovLike = Union[Covariance, Callable, None]
+
+
+def _default_device(device):
+    if device is not None:
+        return torch.device(device)
+    if not torch.cuda.is_available():
+        raise _lib.NNGPExtensionError("pynngp_amd.NNGP needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class NNGP:
+    """Nearest-neighbour GP over ordinates ``t`` (mirrors ``pyNNGP.NNGP``)."""
+
+    def __init__(self, t, y, eps, refType, m, cov: CovLike, device=None):
+        self.t = t  # ordinates (held by reference, nngp.py:7)
+        self.y = y  # abscissae
+        self.eps = eps  # measurement uncertainties in y (stored, unused: SURVEY Appendix A)
+        self.refType = refType
+        self.m = int(m)
+        self.cov = cov
+        self.device = _default_device(device)
+        if not 0 <= self.m <= _lib.MAX_M:
+            raise ValueError(f"m={m} outside [0, {_lib.MAX_M}]")
+
+        self._init_s()
+        self._init_wt()
+        self._init_ws()
+        self._make_s_neighbor_sets()
+        self._make_t_neighbor_sets()
+        self._B = self._F = None
+
+    # -- construction (nngp.py:21-71) -----------------------------------------
+    def _init_s(self):
+        if isinstance(self.refType, str):
+            if self.refType != "S=T":
+                raise ValueError(f"unknown refType {self.refType!r} (only 'S=T' is a string option)")
+            self.s = self.t
+        elif isinstance(self.refType, tuple):
+            raise NotImplementedError(
+                "tuple refType ('subset', n) / ('random', n, bounds) is SURVEY.md 8(f) 'next' "
+                "(the reference raises AttributeError here, nngp.py:34)")
+        else:
+            raise TypeError(f"refType must be 'S=T' or a tuple, got {type(self.refType).__name__}")
+        self._s_dev = torch.as_tensor(np.ascontiguousarray(self.s, dtype=np.float64)).to(self.device)
+        if self._s_dev.dim() != 2 or self._s_dev.shape[1] != 2:
+            raise ValueError(f"ordinates must be (N, 2), got {tuple(self._s_dev.shape)}")
+        self._t_dev = self._s_dev  # S=T
+
+    def _init_wt(self):
+        self.wt = np.copy(self.y)
+
+    def _init_ws(self, k: int = 5):
+        """5-NN uniform regression of y on t at s (nngp.py:45-47) on the GPU."""
+        n = self._t_dev.shape[0]
+        if n < k:
+            raise ValueError(f"Expected n_neighbors <= n_samples_fit, but n_neighbors = {k}, n_samples_fit = {n}")
+        idx = _lib.knn_query(self._t_dev, self._s_dev, k).long()
+        y = torch.as_tensor(np.asarray(self.y, dtype=np.float64)).to(self.device)
+        self.ws = y[idx].mean(dim=1).cpu().numpy()
+
+    def _make_s_neighbor_sets(self):
+        self.nbr = _lib.knn_prior(self._s_dev, self.m)  # int32 (N, m) on the device, -1 padded
+        self._Ns = None
+
+    def _make_t_neighbor_sets(self):
+        # 'S=T': Nt aliases Ns (nngp.py:65-67)
+        pass
+
+    @property
+    def Ns(self):
+        """Reference format: list with ``Ns[0] == []`` and int64 arrays of min(i, m) indices."""
+        if self._Ns is None:
+            a = self.nbr.cpu().numpy().astype(np.int64)
+            ns = [[]]
+            for i in range(1, a.shape[0]):
+                ns.append(a[i, : min(i, self.m)])
+            self._Ns = ns
+        return self._Ns
+
+    @property
+    def Nt(self):
+        return self.Ns
+
+    # -- covariance plumbing ---------------------------------------------------
+    def _covariance(self) -> Covariance:
+        if not isinstance(self.cov, Covariance):
+            raise TypeError(
+                "the device B/F sweep fuses the covariance: pass cov=pynngp_amd.Covariance(kind, sigma2, phi, tau2) "
+                f"(got {type(self.cov).__name__})")
+        return self.cov
+
+    def _nbr_idx(self, i):
+        row = self.nbr[i]
+        return row[row >= 0].long()
+
+    def _call_cov(self, a, b):
+        if self.cov is None:
+            raise TypeError("cov is None")
+        if isinstance(self.cov, Covariance):
+            return self.cov(a, b)
+        return self.cov(a.cpu().numpy(), b.cpu().numpy())
+
+    # -- per-location algebra (nngp.py:73-96) ----------------------------------
+    def _CNs(self, i):
+        """C_{N(s_i)} (nngp.py:78-82), with the nugget on the diagonal for a Covariance."""
+        x = self._s_dev[self._nbr_idx(i)]
+        c = self._call_cov(x, x)
+        if isinstance(self.cov, Covariance) and self.cov.tau2 > 0:
+            c = c + self.cov.tau2 * torch.eye(x.shape[0], dtype=c.dtype, device=c.device)
+        return c.cpu().numpy() if isinstance(c, torch.Tensor) else c
+
+    def _Ccross(self, i):
+        """C_{s_i, N(s_i)} (nngp.py:84-86), shape (1, k)."""
+        c = self._call_cov(self._s_dev[i][None, :], self._s_dev[self._nbr_idx(i)])
+        return c.cpu().numpy() if isinstance(c, torch.Tensor) else c
+
+    def _Cs(self, i):
+        """C_{s_i, s_i} (nngp.py:92-96), with the nugget for a Covariance."""
+        x = self._s_dev[i][None, :]
+        c = self._call_cov(x, x)
+        if isinstance(self.cov, Covariance):
+            c = c + self.cov.tau2
+        return c.cpu().numpy() if isinstance(c, torch.Tensor) else c
+
+    def _row_bf(self, i):
+        cv = self._covariance()
+        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr[i: i + 1], int(i), cv.kind, *cv.theta)
+        _raise_on_bad(p.cpu().numpy())
+        k = min(int(i), self.m)
+        return B[0, :k].cpu().numpy(), float(F[0].item())
+
+    def _Bsi(self, i):
+        """B_{s_i} = C_{s_i,N} C_N^{-1} (nngp.py:73-76) from the device kernel."""
+        return self._row_bf(i)[0]
+
+    def _Fsi(self, i):
+        """F_{s_i} = C_ii - B_i C_{N,s_i} (nngp.py:88-90) from the device kernel."""
+        return self._row_bf(i)[1]
+
+    # -- whole-field sweep -----------------------------------------------------
+    def compute_BF(self, algo: str = "auto"):
+        """All B (N, m) and F (N,) as device tensors (one fused sweep)."""
+        cv = self._covariance()
+        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr, 0, cv.kind, *cv.theta, algo=algo)
+        _raise_on_bad(p.cpu().numpy())
+        self._B, self._F = B, F
+        return B, F
+
+    @property
+    def B(self):
+        return self.compute_BF()[0] if self._B is None else self._B
+
+    @property
+    def F(self):
+        return self.compute_BF()[1] if self._F is None else self._F
+
+    def loglik(self, values=None, cov: Optional[Covariance] = None, algo: str = "auto") -> float:
+        """NNGP log density of ``values`` (default ``y``): -1/2 sum [log 2pi + log F + r^2/F]."""
+        cv = cov if cov is not None else self._covariance()
+        v = self.y if values is None else values
+        v = torch.as_tensor(np.asarray(v, dtype=np.float64) if not isinstance(v, torch.Tensor) else v,
+                            dtype=torch.float64).to(self.device)
+        if v.dim() != 1:
+            raise ValueError("loglik needs one value per location (1-D values)")
+        _, _, p = _lib.bf_sweep(self._s_dev, self.nbr, 0, cv.kind, *cv.theta, values=v, want_bf=False, algo=algo)
+        ph = p.cpu().numpy()
+        _raise_on_bad(ph)
+        n = self.nbr.shape[0]
+        return -0.5 * (n * LOG_2PI + ph[0] + ph[1])
+
+    def oneSample(self):
+        """Gibbs sweep (nngp.py:98-101 calls methods that do not exist): SURVEY.md 8(f) 'next'."""
+        raise NotImplementedError("the Gibbs sweep is SURVEY.md 8(f) 'next' (the reference has no implementation)")
+
+
+class NNGPNumericalError(ArithmeticError):
+    """A location's neighbour covariance was not positive definite."""
+
+
+def _raise_on_bad(partials_host) -> None:
+    if partials_host[3] >= 0:
+        raise IndexError(f"neighbour index out of range at location {int(partials_host[3])}")
+    if partials_host[2] >= 0:
+        raise NNGPNumericalError(
+            f"non-positive Cholesky pivot or F at location {int(partials_host[2])} (add a nugget tau2 or change phi)")

@@ -1,0 +1,110 @@
+"""Device-resident, optionally sharded NNGP log-likelihood sweep.
+
+SURVEY.md 8(e): every location's B_i, F_i and log-lik term is independent given
+read-only coordinates and values, so locations shard contiguously -- rank r of
+P owns rows [floor(rN/P), floor((r+1)N/P)).  Coordinates and values are
+replicated (neighbours j < i may sit in any earlier shard).  Each rank builds the
+neighbour sets of its own rows only.  The one exchange per sweep is the summed
+log-likelihood: the 4-double partials of every rank are all-gathered (RCCL over
+xGMI with the "nccl" backend; gloo in the CPU tests) and summed in rank order,
+so the result is bit-identical on every rank and run to run.
+
+The per-shard compute and neighbour build are injectable so the distributed
+combination logic is testable on CPU with the oracle (tests/test_distributed.py);
+the default compute is the HIP kernel through ``_lib``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .nngp import Covariance, LOG_2PI, _raise_on_bad
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous shard [lo, hi) of n locations for rank of world."""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+def combine_partials(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """All-gather the (4,) partials and reduce them in rank order.
+
+    [0], [1] are summed; [2], [3] (first bad row or -1) take the smallest non-negative.
+    """
+    if world == 1:
+        return local
+    gathered = torch.empty((world, 4), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(gathered, local.reshape(1, 4), group=group)
+    sums = gathered[:, :2].sum(dim=0)
+    flags = gathered[:, 2:]
+    big = torch.full_like(flags, float("inf"))
+    first = torch.where(flags >= 0, flags, big).amin(dim=0)
+    first = torch.where(torch.isinf(first), torch.full_like(first, -1.0), first)
+    return torch.cat([sums, first])
+
+
+class ShardedLogLik:
+    """Log-likelihood sweep over this rank's contiguous shard of N locations.
+
+    ``coords`` and ``values`` are the full (replicated) arrays on this rank's device.
+    """
+
+    def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
+                 algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None):
+        self.coords = coords
+        self.n = coords.shape[0]
+        self.m = int(m)
+        self.rank, self.world, self.group = rank, world, group
+        self.lo, self.hi = shard_range(self.n, rank, world)
+        self.algo = algo
+        self._compute = compute
+        if build_nbr is None:
+            self.nbr = _lib.knn_prior(coords, self.m, self.lo, self.hi)
+        else:
+            self.nbr = build_nbr(coords, self.m, self.lo, self.hi)
+        self._ws = None
+        self._partials = None
+        if compute is None:
+            self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device)
+            self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
+            self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
+            self._F = torch.empty((self.hi - self.lo,), dtype=torch.float64, device=coords.device)
+
+    def local_partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True) -> torch.Tensor:
+        """Stream-ordered partials of this shard (no host sync)."""
+        if self._compute is not None:
+            return self._compute(self, cov, values, want_bf)
+        B, F = (self._B, self._F) if want_bf else (None, None)
+        _, _, p = _lib.bf_sweep(self.coords, self.nbr, self.lo, cov.kind, *cov.theta, values=values,
+                                want_bf=want_bf, algo=self.algo, B=B, F=F, partials=self._partials,
+                                workspace=self._ws)
+        return p
+
+    def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True) -> torch.Tensor:
+        """Global partials (all ranks), stream-ordered."""
+        return combine_partials(self.local_partials(cov, values, want_bf), self.world, self.group)
+
+    def loglik(self, cov: Covariance, values: torch.Tensor, want_bf: bool = False) -> float:
+        """Global NNGP log-likelihood (synchronises the host)."""
+        p = self.partials(cov, values, want_bf).cpu().numpy()
+        _raise_on_bad(p)
+        return -0.5 * (self.n * LOG_2PI + p[0] + p[1])
+
+    @property
+    def B(self):
+        return self._B
+
+    @property
+    def F(self):
+        return self._F
+
+
+def loglik_from_partials(p, n: int) -> float:
+    return -0.5 * (n * LOG_2PI + float(p[0]) + float(p[1]))
+
+
+__all__ = ["shard_range", "combine_partials", "ShardedLogLik", "loglik_from_partials", "math"]

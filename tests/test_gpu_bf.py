@@ -1,0 +1,190 @@
+"""GPU parity: fused B/F + log-likelihood sweep (nngp_bf_sweep) vs the oracle.
+
+Oracle: oracle/nngp_oracle.c (fp64, libm exp/sqrt, row-oriented Cholesky) on the
+same neighbour sets.  Tolerances (fp64; the kernel uses its own ~1 ulp exp/sqrt
+and a right-looking factorisation, so results differ in the last bits):
+  F:        |dF| / F          <= 1e-10
+  B:        |dB|              <= 1e-9 * (1 + |B|)
+  loglik:   |dl| / |l|        <= max(1e-12, 1e-15 * kappa),  kappa = max_i (sigma2 + tau2) / F_i
+The log-lik bound scales with kappa because F_i = C_ii - c^T C_N^{-1} c is a
+difference of nearly equal numbers when the field is smooth relative to the
+neighbour spacing (Matern-3/2 with tau2 = 0 reaches kappa ~ 3e5 below): its
+relative rounding error, and that of r_i^2 / F_i, is ~ eps * kappa in any fp64
+evaluation order (the oracle's included).
+Bit-reproducibility run to run is exact.  Known answer on the GPU: m = N-1 gives
+the dense-GP log density.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+RTOL_F = 1e-10
+ATOL_B = 1e-9
+RTOL_LL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pynngp_amd import _lib
+
+    return _lib
+
+
+def _field(n, seed):
+    rng = np.random.default_rng(seed)
+    return rng.uniform(0.0, 1.0, (n, 2)), rng.standard_normal(n)
+
+
+def _check(dev, lib, O, coords, nbr, kind, theta, y, algo, i0=0):
+    rows = nbr.shape[0]
+    c = torch.from_numpy(coords).to(dev)
+    v = None if y is None else torch.from_numpy(y).to(dev)
+    B, F, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), i0, kind, *theta, values=v, algo=algo)
+    Bo, Fo, po = O.c_bf_sweep(coords, nbr, kind, theta, y, i0=i0)
+    B, F, p = B.cpu().numpy(), F.cpu().numpy(), p.cpu().numpy()
+    assert p[2] == -1 and p[3] == -1
+    assert np.all(np.abs(F - Fo) <= RTOL_F * Fo), np.max(np.abs(F - Fo) / Fo)
+    assert np.all(np.abs(B - Bo) <= ATOL_B * (1 + np.abs(Bo))), np.max(np.abs(B - Bo))
+    assert np.all(B[nbr < 0] == 0.0)
+    ll = O.loglik_from_partials(p, rows)
+    llo = O.loglik_from_partials(po, rows)
+    kappa = float(np.max((theta[0] + theta[2]) / Fo))
+    assert abs(ll - llo) <= max(RTOL_LL, 1e-15 * kappa) * abs(llo), (ll, llo, kappa)
+    return p
+
+
+CASES = [
+    ("exponential", (1.0, 30.0, 0.0), 15),
+    ("exponential", (1.3, 4.0, 0.1), 10),
+    ("matern32", (1.0, 17.320508075688772, 0.1), 15),
+    ("matern32", (2.0, 40.0, 0.0), 8),
+    ("exponential", (0.7, 12.0, 0.05), 1),
+    ("exponential", (1.0, 30.0, 0.0), 16),
+]
+
+
+@pytest.mark.parametrize("algo", ["lane", "wave"])
+@pytest.mark.parametrize("kind,theta,m", CASES)
+def test_bf_vs_oracle(lib, dev, c_oracle, kind, theta, m, algo):
+    coords, y = _field(6000, m)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, algo)
+
+
+@pytest.mark.parametrize("m", [20, 31, 40, 63])
+def test_bf_wave_large_m(lib, dev, c_oracle, m):
+    coords, y = _field(3000, 100 + m)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 8.0, 0.05), y, "auto")
+    _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, "wave")
+
+
+def test_bf_m0_and_no_values(lib, dev, c_oracle):
+    coords, y = _field(500, 9)
+    nbr = np.zeros((500, 0), dtype=np.int32)
+    p = _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.5, 3.0, 0.2), y, "auto")
+    # m = 0: independent N(0, sigma2 + tau2)
+    ll = c_oracle.loglik_from_partials(p, 500)
+    s = 1.7
+    assert abs(ll - (-0.5 * (500 * np.log(2 * np.pi * s) + (y * y).sum() / s))) < 1e-9
+    nbr = c_oracle.c_knn_prior(coords, 12)
+    p = _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 10.0, 0.0), None, "lane")
+    assert p[1] == 0.0
+
+
+def test_bf_dense_gp_known_answer(lib, dev, c_oracle):
+    """m = N-1: the NNGP density is the exact GP density (Vecchia with full conditioning)."""
+    n = 60
+    coords, y = _field(n, 21)
+    nbr = c_oracle.c_knn_prior(coords, n - 1)
+    for kind, theta in [("exponential", (1.3, 4.0, 0.1)), ("matern32", (1.0, 3.0, 0.05))]:
+        c = torch.from_numpy(coords).to(dev)
+        _, _, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, kind, *theta,
+                               values=torch.from_numpy(y).to(dev))
+        ll = c_oracle.loglik_from_partials(p.cpu().numpy(), n)
+        dense = c_oracle.dense_gp_loglik(coords, kind, theta, y)
+        assert abs(ll - dense) <= 1e-10 * abs(dense), (ll, dense)
+
+
+def test_bf_shards_sum_and_reproducible(lib, dev, c_oracle):
+    coords, y = _field(20000, 3)
+    m = 15
+    nbr = c_oracle.c_knn_prior(coords, m)
+    c = torch.from_numpy(coords).to(dev)
+    v = torch.from_numpy(y).to(dev)
+    nb = torch.from_numpy(nbr).to(dev)
+    theta = (1.0, 30.0, 0.0)
+    B, F, p = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v)
+    B2, F2, p2 = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v)
+    assert torch.equal(B, B2) and torch.equal(F, F2) and torch.equal(p, p2)
+    cuts = [0, 1, 777, 5000, 13333, 20000]
+    tot = torch.zeros(2, dtype=torch.float64, device=dev)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        Bs, Fs, ps = lib.bf_sweep(c, nb[a:b], a, "exponential", *theta, values=v)
+        assert torch.equal(Bs, B[a:b]) and torch.equal(Fs, F[a:b])
+        tot += ps[:2]
+    assert torch.allclose(tot, p[:2], rtol=1e-13, atol=0)
+    _, _, pe = lib.bf_sweep(c, nb[:0], 0, "exponential", *theta, values=v)
+    assert pe.cpu().tolist() == [0.0, 0.0, -1.0, -1.0]
+
+
+def test_bf_flags_bad_rows(lib, dev, c_oracle):
+    coords, y = _field(2000, 4)
+    nbr = c_oracle.c_knn_prior(coords, 10)
+    c = torch.from_numpy(coords).to(dev)
+    sing = nbr.copy()
+    sing[1234, 1] = sing[1234, 0]  # repeated neighbour: C_N singular, second pivot exactly 0 (sigma2 = 1)
+    sing[1500, 1] = sing[1500, 0]
+    for algo in ["lane", "wave"]:
+        B, F, p = lib.bf_sweep(c, torch.from_numpy(sing).to(dev), 0, "exponential", 1.0, 5.0, 0.0, algo=algo)
+        _, _, po = c_oracle.c_bf_sweep(coords, sing, "exponential", (1.0, 5.0, 0.0), None)
+        assert p[2].item() == 1234 == po[2]
+        Fh = F.cpu().numpy()
+        assert np.isnan(Fh[1234]) and np.isnan(Fh[1500]) and np.all(np.isfinite(np.delete(Fh, [1234, 1500])))
+        assert np.all(np.isnan(B.cpu().numpy()[1234]))
+    bad = nbr.copy()
+    bad[1234, 3] = 2000  # out-of-range neighbour index
+    _, _, p = lib.bf_sweep(c, torch.from_numpy(bad).to(dev), 0, "exponential", 1.0, 5.0, 0.1)
+    assert p[3].item() == 1234
+
+
+def test_bf_full_size_properties(lib, dev, c_oracle):
+    """Config 3 size (N=1e6, m=15): lane == wave, sampled rows vs oracle, F in (0, sigma2]."""
+    n, m = 1_000_000, 15
+    coords, y = _field(n, 0)
+    c = torch.from_numpy(coords).to(dev)
+    v = torch.from_numpy(y).to(dev)
+    nb = lib.knn_prior(c, m)
+    theta = (1.0, 30.0, 0.0)
+    B, F, p = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="lane")
+    Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="wave")
+    assert torch.allclose(F, Fw, rtol=1e-12, atol=0)
+    assert torch.allclose(B, Bw, rtol=0, atol=1e-10)
+    ll, llw = (c_oracle.loglik_from_partials(q.cpu().numpy(), n) for q in (p, pw))
+    assert abs(ll - llw) <= 1e-12 * abs(ll)
+    Fh = F.cpu().numpy()
+    assert np.all(Fh > 0) and np.all(Fh <= 1.0 + 1e-12)
+    rows = np.random.default_rng(1).integers(0, n, 4000)
+    rows = np.unique(np.concatenate([rows, np.arange(20)]))
+    nbr_h = nb.cpu().numpy()
+    for r0 in rows[::400]:
+        r1 = min(n, r0 + 400)
+        Bo, Fo, _ = c_oracle.c_bf_sweep(coords, nbr_h[r0:r1], "exponential", theta, y, i0=int(r0))
+        assert np.all(np.abs(Fh[r0:r1] - Fo) <= RTOL_F * Fo)
+        assert np.all(np.abs(B[r0:r1].cpu().numpy() - Bo) <= ATOL_B * (1 + np.abs(Bo)))
+
+
+def test_bf_op_registered(dev, c_oracle):
+    from pynngp_amd import ops
+
+    coords, y = _field(1000, 8)
+    c = torch.from_numpy(coords).to(dev)
+    nb = torch.ops.nngp.knn_prior(c, 10, 0, 1000)
+    B, F, p = torch.ops.nngp.bf_sweep(c, nb, 0, ops.kind_code("matern32"), 1.0, 5.0, 0.1,
+                                      torch.from_numpy(y).to(dev), True, ops.algo_code("auto"))
+    Bo, Fo, po = c_oracle.c_bf_sweep(coords, nb.cpu().numpy(), "matern32", (1.0, 5.0, 0.1), y)
+    assert np.allclose(F.cpu().numpy(), Fo, rtol=RTOL_F, atol=0)
+    _, _, p2 = torch.ops.nngp.bf_sweep(c, nb, 0, 1, 1.0, 5.0, 0.1, None, False, 0)
+    assert abs(p2[0].item() - po[0]) <= 1e-12 * abs(po[0])
