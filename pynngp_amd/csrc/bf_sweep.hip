@@ -15,7 +15,7 @@
 // is r_i = v_i - B_i v_N(i).  B_i = L_N^{-T} v needs one more back-solve.
 // Neighbour slots with index -1 become identity rows (decoupled, exact).
 //
-// Two kernels, same math, same outputs:
+// Two kernels, same math, same outputs (bf_wave lives in bf_wave.hip):
 //   bf_lane<M>   one LANE per location, the whole joint block in VGPRs, fully
 //                unrolled for a compile-time M <= 16.  64 locations per wave;
 //                every lane does useful fp64 work on every instruction.
@@ -32,16 +32,16 @@
 
 namespace nngp {
 
+
 // --------------------------------------------------------------------------
 // one lane per location
 // --------------------------------------------------------------------------
-template <int M>
+template <int M, int KIND>
 __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coords, int64_t n_points,
                                                const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0,
-                                               int kind, double sigma2, double phi, double tau2,
-                                               const double* __restrict__ values, double* __restrict__ Bout,
-                                               double* __restrict__ Fout, double* __restrict__ wpart,
-                                               unsigned long long* __restrict__ status) {
+                                               const CovParams P, const double* __restrict__ values,
+                                               double* __restrict__ Bout, double* __restrict__ Fout,
+                                               double* __restrict__ wpart, unsigned long long* __restrict__ status) {
     constexpr int N1 = M + 1;  // joint block order
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = r < n_rows;
@@ -63,8 +63,8 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
 #pragma unroll
     for (int a = 0; a < M; ++a) {
         const double2 x = coords[idx[a]];
-        px[a] = x.x;
-        py[a] = x.y;
+        px[a] = valid[a] ? x.x : kFar * (a + 1);
+        py[a] = valid[a] ? x.y : 0.0;
         z[a] = (values != nullptr && valid[a]) ? values[idx[a]] : 0.0;
     }
     {
@@ -76,27 +76,21 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
 
     // joint block, lower triangle (A[a][b], b <= a)
     double A[N1][N1];
-    const double diag = sigma2 + tau2;
 #pragma unroll
     for (int a = 0; a < N1; ++a) {
-        const bool va = a < M ? valid[a] : true;
 #pragma unroll
-        for (int b = 0; b < a; ++b) {
-            const double c = nngp_cov(kind, nngp_dist(px[a], py[a], px[b], py[b]), sigma2, phi);
-            A[a][b] = (va && valid[b]) ? c : 0.0;
-        }
-        A[a][a] = va ? diag : 1.0;
+        for (int b = 0; b < a; ++b) A[a][b] = nngp_cov_d2<KIND>(P, nngp_d2(px[a], py[a], px[b], py[b]));
+        A[a][a] = P.diag;
     }
 
-    // right-looking elimination of the M neighbour columns
-    double inv[M > 0 ? M : 1];
+    // right-looking elimination of the M neighbour columns (value column z appended)
+    double inv[M];
     bool bad = false;
 #pragma unroll
     for (int p = 0; p < M; ++p) {
         bad |= !(A[p][p] > 0.0);
         const double ip = nngp_rsqrt(A[p][p]);
         inv[p] = ip;
-        A[p][p] *= ip;  // L[p][p] = sqrt(pivot)
 #pragma unroll
         for (int a = p + 1; a < N1; ++a) A[a][p] *= ip;
         z[p] *= ip;
@@ -112,7 +106,8 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
     bad |= !(F > 0.0);
 
     if (Bout != nullptr) {
-        double bb[M > 0 ? M : 1];
+        // B = L_N^{-T} v, v = row M of L
+        double bb[M];
 #pragma unroll
         for (int a = M - 1; a >= 0; --a) {
             double s = A[M][a];
@@ -122,7 +117,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
         }
         if (live) {
 #pragma unroll
-            for (int a = 0; a < M; ++a) Bout[rr * M + a] = valid[a] ? (bad ? NAN : bb[a]) : 0.0;
+            for (int a = 0; a < M; ++a) Bout[rr * M + a] = bad ? NAN : (valid[a] ? bb[a] : 0.0);
         }
     }
     if (Fout != nullptr && live) Fout[rr] = bad ? NAN : F;
@@ -135,106 +130,6 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
         if (bad_index) atomicMin(status + 1, (unsigned long long)i);
     }
     wave_partials_store(lf, q, wpart, r);
-}
-
-// --------------------------------------------------------------------------
-// one wave per location; lane a owns row a of the joint block (NR >= M+1 rows)
-// --------------------------------------------------------------------------
-template <int NR>
-__global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
-                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0, int M,
-                                               int kind, double sigma2, double phi, double tau2,
-                                               const double* __restrict__ values, double* __restrict__ Bout,
-                                               double* __restrict__ Fout, double* __restrict__ wpart,
-                                               unsigned long long* __restrict__ status) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
-    const double diag = sigma2 + tau2;
-
-    for (int64_t rr = wave; rr < n_rows; rr += n_waves) {
-        const int64_t i = i0 + rr;
-        // lane a < M: neighbour slot a; lane M: the location itself; lanes > M: identity rows
-        int32_t j = -1;
-        if (lane < M) j = nbr[rr * M + lane];
-        const bool is_self = lane == M;
-        const bool in_range = j >= 0 && (int64_t)j < n_points;
-        const bool bad_index = j >= 0 && !in_range;
-        const bool valid = is_self || in_range;
-        const int64_t src = is_self ? i : (in_range ? (int64_t)j : 0);
-        const double2 x = coords[src];
-        double zv = (values != nullptr && valid) ? values[src] : 0.0;
-        const unsigned long long vmask = __ballot(valid);
-
-        // row `lane` of the joint block (entries b <= lane are meaningful)
-        double row[NR];
-#pragma unroll
-        for (int b = 0; b < NR; ++b) {
-            const double bx = wave_bcast(x.x, b);
-            const double by = wave_bcast(x.y, b);
-            const bool vb = (vmask >> b) & 1ull;
-            const double c = nngp_cov(kind, nngp_dist(x.x, x.y, bx, by), sigma2, phi);
-            double v = (valid && vb) ? c : 0.0;
-            if (b == lane) v = valid ? diag : 1.0;
-            row[b] = v;
-        }
-        bool bad = false;
-        double ip_mine = 1.0;  // lane p keeps 1/L[p][p]
-#pragma unroll
-        for (int p = 0; p < NR - 1; ++p) {
-            if (p < M) {
-                const double piv = wave_bcast(row[p], p);
-                bad |= !(piv > 0.0);
-                const double ip = nngp_rsqrt(piv);
-                if (lane == p) ip_mine = ip;
-                row[p] *= ip;  // lane > p: L[lane][p]; lane p: sqrt(pivot)
-                const double l = row[p];
-                if (lane == p) zv *= ip;
-                const double zp = wave_bcast(zv, p);
-                if (lane > p) zv = fma(-l, zp, zv);
-#pragma unroll
-                for (int b = p + 1; b < NR; ++b) {
-                    if (b <= M) {
-                        const double lb = wave_bcast(l, b);
-                        if (lane >= b) row[b] = fma(-l, lb, row[b]);
-                    }
-                }
-            }
-        }
-        double F = 0.0;
-#pragma unroll
-        for (int b = 0; b < NR; ++b)
-            if (b == M) F = wave_bcast(row[b], M);
-        const double res = wave_bcast(zv, M);
-        bad |= !(F > 0.0);
-        if (Bout != nullptr) {
-            // B = L_N^{-T} v with v = row M of L; lane a ends with b_a
-            double bmine = 0.0;
-#pragma unroll
-            for (int a = NR - 2; a >= 0; --a) {
-                if (a < M) {
-                    const double term = (lane > a && lane < M) ? row[a] * bmine : 0.0;
-                    const double va = wave_bcast(row[a], M);
-                    const double s = va - wave_sum(term);
-                    const double ipa = wave_bcast(ip_mine, a);
-                    if (lane == a) bmine = s * ipa;
-                }
-            }
-            if (lane < M) Bout[rr * M + lane] = in_range ? (bad ? NAN : bmine) : 0.0;
-        }
-        if (lane == 0) {
-            if (Fout != nullptr) Fout[rr] = bad ? NAN : F;
-            lf_acc += log(F);
-            q_acc += res * res / F;
-            if (bad) atomicMin(status + 0, (unsigned long long)i);
-        }
-        if (__any(bad_index) && lane == 0) atomicMin(status + 1, (unsigned long long)i);
-    }
-    if (lane == 0) {
-        wpart[2 * wave] = lf_acc;
-        wpart[2 * wave + 1] = q_acc;
-    }
 }
 
 // --------------------------------------------------------------------------
@@ -271,66 +166,49 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ w
 // --------------------------------------------------------------------------
 // launch
 // --------------------------------------------------------------------------
-template <int M>
-static hipError_t launch_lane(const BfArgs& a, hipStream_t s) {
+template <int M, int KIND>
+static void launch_lane(const BfArgs& a, const CovParams& P, hipStream_t s) {
     const int64_t blocks = (a.n_rows + 255) / 256;
-    hipLaunchKernelGGL(bf_lane<M>, dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords, a.n_points,
-                       a.nbr, a.n_rows, a.i0, a.kind, a.sigma2, a.phi, a.tau2, a.values, a.B, a.F, a.wpart,
-                       a.status);
-    return hipGetLastError();
-}
-
-template <int NR>
-static hipError_t launch_wave(const BfArgs& a, int64_t n_waves, hipStream_t s) {
-    hipLaunchKernelGGL(bf_wave<NR>, dim3((unsigned)(n_waves / 4)), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.n_rows, a.i0, a.m, a.kind, a.sigma2, a.phi, a.tau2, a.values, a.B, a.F,
-                       a.wpart, a.status);
-    return hipGetLastError();
+    hipLaunchKernelGGL((bf_lane<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
+                       a.n_points, a.nbr, a.n_rows, a.i0, P, a.values, a.B, a.F, a.wpart, a.status);
 }
 
 int64_t bf_lane_waves(int64_t n_rows) { return (n_rows + 255) / 256 * 4; }
 
-int64_t bf_wave_waves(int64_t n_rows) {
-    // persistent grid: at most 256 CUs x 8 waves x 4, at least one wave per location
-    int64_t w = n_rows < 8192 ? n_rows : 8192;
-    w = (w + 3) / 4 * 4;
-    return w < 4 ? 4 : w;
+template <int KIND>
+static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
+    switch (a.m) {
+#define NNGP_LANE_CASE(MM)              \
+    case MM:                            \
+        launch_lane<MM, KIND>(a, P, s); \
+        return true;
+        NNGP_LANE_CASE(1) NNGP_LANE_CASE(2) NNGP_LANE_CASE(3) NNGP_LANE_CASE(4) NNGP_LANE_CASE(5)
+        NNGP_LANE_CASE(6) NNGP_LANE_CASE(7) NNGP_LANE_CASE(8) NNGP_LANE_CASE(9) NNGP_LANE_CASE(10)
+        NNGP_LANE_CASE(11) NNGP_LANE_CASE(12) NNGP_LANE_CASE(13) NNGP_LANE_CASE(14) NNGP_LANE_CASE(15)
+        NNGP_LANE_CASE(16)
+#undef NNGP_LANE_CASE
+        default:
+            return false;
+    }
 }
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
-    hipError_t e = hipSuccess;
     if (a.n_rows == 0) {  // empty shard: partials = [0, 0, -1, -1]
         hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, (int64_t)0, a.status, a.partials);
         return hipGetLastError();
     }
+    const CovParams P = nngp_cov_params(a.sigma2, a.phi, a.tau2);
+    bool ok;
+    int64_t nw;
     if (algo == kAlgoLane) {
-        switch (a.m) {
-#define NNGP_LANE_CASE(MM) \
-    case MM:               \
-        e = launch_lane<MM>(a, s); \
-        break;
-            NNGP_LANE_CASE(1) NNGP_LANE_CASE(2) NNGP_LANE_CASE(3) NNGP_LANE_CASE(4) NNGP_LANE_CASE(5)
-            NNGP_LANE_CASE(6) NNGP_LANE_CASE(7) NNGP_LANE_CASE(8) NNGP_LANE_CASE(9) NNGP_LANE_CASE(10)
-            NNGP_LANE_CASE(11) NNGP_LANE_CASE(12) NNGP_LANE_CASE(13) NNGP_LANE_CASE(14) NNGP_LANE_CASE(15)
-            NNGP_LANE_CASE(16)
-#undef NNGP_LANE_CASE
-            default:
-                return hipErrorInvalidValue;
-        }
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, bf_lane_waves(a.n_rows), a.status,
-                           a.partials);
-        return hipGetLastError();
+        ok = a.kind == 1 ? launch_lane_m<1>(a, P, s) : launch_lane_m<0>(a, P, s);
+        nw = bf_lane_waves(a.n_rows);
+    } else {
+        nw = bf_wave_waves(a.n_rows);
+        ok = bf_wave_launch(a, P, nw, s);
     }
-    const int64_t nw = bf_wave_waves(a.n_rows);
-    if (a.m + 1 <= 16)
-        e = launch_wave<16>(a, nw, s);
-    else if (a.m + 1 <= 32)
-        e = launch_wave<32>(a, nw, s);
-    else if (a.m + 1 <= 64)
-        e = launch_wave<64>(a, nw, s);
-    else
-        return hipErrorInvalidValue;
+    if (!ok) return hipErrorInvalidValue;
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, nw, a.status, a.partials);
     return hipGetLastError();

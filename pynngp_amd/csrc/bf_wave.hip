@@ -1,0 +1,140 @@
+// One-wave-per-location B/F + log-likelihood kernel (the north_star layout):
+// lane a owns row a of the (m+1)x(m+1) joint block in VGPRs, column values are
+// broadcast with v_readlane, so any m <= 63 runs without LDS.  Same math and
+// outputs as bf_lane (bf_sweep.hip, which documents the formulation and the
+// reference methods nngp.py:73-96 it replaces); used for m > 16 and as the
+// comparison point for the lane kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nngp_math.h"
+#include "nngp_internal.h"
+
+namespace nngp {
+
+// --------------------------------------------------------------------------
+// one wave per location; lane a owns row a of the joint block (NR >= M+1 rows)
+// --------------------------------------------------------------------------
+template <int NR, int KIND>
+__global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
+                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0, int M,
+                                               const CovParams P, const double* __restrict__ values,
+                                               double* __restrict__ Bout, double* __restrict__ Fout,
+                                               double* __restrict__ wpart, unsigned long long* __restrict__ status) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
+
+    for (int64_t rr = wave; rr < n_rows; rr += n_waves) {
+        const int64_t i = i0 + rr;
+        // lane a < M: neighbour slot a; lane M: the location itself; lanes > M: far-away identity rows
+        int32_t j = -1;
+        if (lane < M) j = nbr[rr * M + lane];
+        const bool is_self = lane == M;
+        const bool in_range = j >= 0 && (int64_t)j < n_points;
+        const bool bad_index = j >= 0 && !in_range;
+        const bool valid = is_self || in_range;
+        const int64_t src = is_self ? i : (in_range ? (int64_t)j : 0);
+        const double2 xg = coords[src];
+        const double xx = valid ? xg.x : kFar * (lane + 1), xy = valid ? xg.y : 0.0;
+        double zv = (values != nullptr && valid) ? values[src] : 0.0;
+
+        // row `lane` of the joint block (entries b <= lane are meaningful)
+        double row[NR];
+#pragma unroll
+        for (int b = 0; b < NR; ++b) {
+            const double bx = wave_bcast(xx, b);
+            const double by = wave_bcast(xy, b);
+            const double c = nngp_cov_d2<KIND>(P, nngp_d2(xx, xy, bx, by));
+            row[b] = b == lane ? P.diag : c;
+        }
+        bool bad = false;
+        double ip_mine = 1.0;  // lane p keeps 1/L[p][p]
+#pragma unroll
+        for (int p = 0; p < NR - 1; ++p) {
+            if (p < M) {
+                const double piv = wave_bcast(row[p], p);
+                bad |= !(piv > 0.0);
+                const double ip = nngp_rsqrt(piv);
+                if (lane == p) ip_mine = ip;
+                row[p] *= ip;  // lane > p: L[lane][p]; lane p: sqrt(pivot)
+                const double l = row[p];
+                if (lane == p) zv *= ip;
+                const double zp = wave_bcast(zv, p);
+                if (lane > p) zv = fma(-l, zp, zv);
+#pragma unroll
+                for (int b = p + 1; b < NR; ++b) {
+                    if (b <= M) {
+                        const double lb = wave_bcast(l, b);
+                        if (lane >= b) row[b] = fma(-l, lb, row[b]);
+                    }
+                }
+            }
+        }
+        double F = 0.0;
+#pragma unroll
+        for (int b = 0; b < NR; ++b)
+            if (b == M) F = wave_bcast(row[b], M);
+        const double res = wave_bcast(zv, M);
+        bad |= !(F > 0.0);
+        if (Bout != nullptr) {
+            // B = L_N^{-T} v with v = row M of L; lane a ends with b_a
+            double bmine = 0.0;
+#pragma unroll
+            for (int a = NR - 2; a >= 0; --a) {
+                if (a < M) {
+                    const double term = (lane > a && lane < M) ? row[a] * bmine : 0.0;
+                    const double va = wave_bcast(row[a], M);
+                    const double s = va - wave_sum(term);
+                    const double ipa = wave_bcast(ip_mine, a);
+                    if (lane == a) bmine = s * ipa;
+                }
+            }
+            if (lane < M) Bout[rr * M + lane] = bad ? NAN : (in_range ? bmine : 0.0);
+        }
+        if (lane == 0) {
+            if (Fout != nullptr) Fout[rr] = bad ? NAN : F;
+            lf_acc += log(F);
+            q_acc += res * res / F;
+            if (bad) atomicMin(status + 0, (unsigned long long)i);
+        }
+        if (__any(bad_index) && lane == 0) atomicMin(status + 1, (unsigned long long)i);
+    }
+    if (lane == 0) {
+        wpart[2 * wave] = lf_acc;
+        wpart[2 * wave + 1] = q_acc;
+    }
+}
+
+template <int NR, int KIND>
+static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s) {
+    hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)(n_waves / 4)), dim3(256), 0, s, (const double2*)a.coords,
+                       a.n_points, a.nbr, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.wpart, a.status);
+}
+
+int64_t bf_wave_waves(int64_t n_rows) {
+    // persistent grid: at most 8192 waves (256 CUs x 32), at least one wave per location
+    int64_t w = n_rows < 8192 ? n_rows : 8192;
+    w = (w + 3) / 4 * 4;
+    return w < 4 ? 4 : w;
+}
+
+template <int KIND>
+static bool launch_wave_m_k(const BfArgs& a, const CovParams& P, int64_t nw, hipStream_t s) {
+    if (a.m + 1 <= 16)
+        launch_wave<16, KIND>(a, P, nw, s);
+    else if (a.m + 1 <= 32)
+        launch_wave<32, KIND>(a, P, nw, s);
+    else if (a.m + 1 <= 64)
+        launch_wave<64, KIND>(a, P, nw, s);
+    else
+        return false;
+    return true;
+}
+
+bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nw, hipStream_t s) {
+    return a.kind == 1 ? launch_wave_m_k<1>(a, P, nw, s) : launch_wave_m_k<0>(a, P, nw, s);
+}
+
+}  // namespace nngp

@@ -66,7 +66,8 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, in
     if (kind != NNGP_COV_EXPONENTIAL && kind != NNGP_COV_MATERN32) return fail(NNGP_EINVAL, "unknown kind %d", kind);
     if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
-    if ((B == nullptr) != (F == nullptr)) return fail(NNGP_EINVAL, "B and F must both be given or both be null");
+    if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
+    if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
     int a = resolve_algo(algo, m);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave) return fail(NNGP_EINVAL, "unknown algo %d", algo);

@@ -3,7 +3,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "nngp_math.h"
+
 namespace nngp {
+
+// Invalid neighbour slots (index -1) are moved "infinitely" far away: slot a sits
+// at (kFar * (a + 1), 0), so every covariance involving it is sigma2 * 2^-(huge) = 0
+// (ldexp underflow) and its row/column of the joint block is a decoupled diagonal
+// entry.  That keeps the pair loops free of per-entry selects; B is zeroed at the
+// store.  (kFar * 64)^2 stays finite.
+constexpr double kFar = 1e150;
 
 constexpr int kAlgoAuto = 0;
 constexpr int kAlgoLane = 1;
@@ -28,6 +37,7 @@ struct BfArgs {
 };
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
+bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s);
 int64_t bf_lane_waves(int64_t n_rows);
 int64_t bf_wave_waves(int64_t n_rows);
 

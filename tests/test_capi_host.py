@@ -1,0 +1,105 @@
+"""CPU: the C-ABI library loads, exports every symbol include/nngp.h declares, and
+rejects bad arguments before touching the GPU (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "nngp.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nngp_[a-z_0-9]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from pynngp_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail(f"{_lib.LIB_PATH} missing: run __graft_entry__.build()")
+    return _lib.load()
+
+
+def test_header_symbols_exported(lib):
+    syms = header_symbols()
+    assert len(syms) >= 8
+    for s in syms:
+        assert hasattr(lib, s), s
+    from pynngp_amd import _lib
+
+    assert sorted(_lib.SYMBOLS) == syms
+
+
+def test_version_and_loglik_helper(lib):
+    from pynngp_amd import _lib
+
+    assert _lib.version().startswith("pynngp_amd") and "gfx950" in _lib.version()
+    p = (ctypes.c_double * 2)(3.0, 4.0)
+    got = lib.nngp_loglik_from_partials(ctypes.cast(p, ctypes.c_void_p), 10)
+    assert abs(got - (-0.5 * (10 * 1.8378770664093453 + 7.0))) < 1e-12
+
+
+def test_workspace_sizes(lib):
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0) >= 16 + 2 * 8 * (1_000_000 // 64)
+    assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0) == 0
+    assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0) > 0
+
+
+def _sweep(lib, **kw):
+    a = dict(coords=1, n_points=10, nbr=1, n_rows=10, m=15, i0=0, kind=0, sigma2=1.0, phi=1.0, tau2=0.0,
+             values=None, B=None, F=None, partials=1, workspace=256, workspace_bytes=1 << 20, algo=0, stream=None)
+    a.update(kw)
+    P = lambda v: None if v is None else ctypes.c_void_p(v)  # noqa: E731
+    return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], P(a["nbr"]), a["n_rows"], a["m"], a["i0"], a["kind"],
+                             a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]),
+                             P(a["partials"]), P(a["workspace"]), a["workspace_bytes"], a["algo"], P(a["stream"]))
+
+
+@pytest.mark.parametrize("kw,code,msg", [
+    (dict(coords=None), -1, "non-null"),
+    (dict(m=64), -4, "m=64"),
+    (dict(m=-1), -4, "m=-1"),
+    (dict(n_rows=11), -1, "outside"),
+    (dict(i0=5), -1, "outside"),
+    (dict(kind=7), -1, "unknown kind"),
+    (dict(sigma2=0.0), -1, "theta"),
+    (dict(phi=float("nan")), -1, "theta"),
+    (dict(tau2=-1.0), -1, "theta"),
+    (dict(B=256), -1, "B given without F"),
+    (dict(F=256), -1, "F given without B"),
+    (dict(workspace=257), -1, "aligned"),
+    (dict(algo=1, m=17), -4, "lane kernel"),
+    (dict(algo=9), -1, "unknown algo"),
+    (dict(workspace_bytes=16), -1, "workspace too small"),
+])
+def test_bf_sweep_rejects(lib, kw, code, msg):
+    assert _sweep(lib, **kw) == code
+    assert msg in lib.nngp_last_error().decode()
+
+
+def test_knn_rejects(lib):
+    P = ctypes.c_void_p
+    assert lib.nngp_knn_prior(None, 10, 5, 0, 10, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_prior(P(1), 10, 65, 0, 10, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_prior(P(1), 10, 5, 3, 2, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_prior(P(1), 0, 5, 0, 0, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_query(P(1), 10, None, 5, 3, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_query(P(1), 10, P(1), 5, 99, P(1), P(256), 1 << 20, None) == -4
+
+
+def test_no_cpu_fallback():
+    import torch
+
+    from pynngp_amd import _lib
+
+    c = torch.zeros((4, 2), dtype=torch.float64)
+    with pytest.raises(_lib.NNGPExtensionError, match="no CPU fallback"):
+        _lib.knn_prior(c, 3)
+    with pytest.raises(_lib.NNGPExtensionError, match="no CPU fallback"):
+        _lib.bf_sweep(c, torch.zeros((4, 3), dtype=torch.int32), 0, "exponential", 1.0, 1.0)

@@ -1,0 +1,87 @@
+"""CPU, world_size 2 (gloo): the sharded sweep's host logic.
+
+Contiguous shards, per-rank neighbour build for its own rows
+only, and the rank-order combination of the 4-double partials must reproduce the
+single-process log-likelihood.  The per-shard compute here is the C oracle
+(injected; the GPU path runs the HIP kernel through the same ShardedLogLik).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pynngp_amd.sweep import ShardedLogLik, combine_partials, shard_range
+
+
+def test_shard_range_covers():
+    for n in [0, 1, 7, 1000, 10_000_001]:
+        for world in [1, 2, 3, 8]:
+            bounds = [shard_range(n, r, world) for r in range(world)]
+            assert bounds[0][0] == 0 and bounds[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(bounds[:-1], bounds[1:]))
+            sizes = [hi - lo for lo, hi in bounds]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_build(coords, m, lo, hi):
+    from oracle import nngp_oracle as O
+
+    return torch.from_numpy(O.c_knn_prior(coords.numpy(), m, lo, hi))
+
+
+def _oracle_compute(sweep, cov, values, want_bf):
+    from oracle import nngp_oracle as O
+
+    _, _, p = O.c_bf_sweep(sweep.coords.numpy(), sweep.nbr.numpy(), cov.kind, cov.theta,
+                           None if values is None else values.numpy(), i0=sweep.lo)
+    return torch.tensor([p[0], p[1], p[2], -1.0], dtype=torch.float64)
+
+
+def _worker(rank, world, port, n, m, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pynngp_amd import Covariance
+
+    rng = np.random.default_rng(0)
+    coords = torch.from_numpy(rng.uniform(size=(n, 2)))
+    values = torch.from_numpy(rng.standard_normal(n))
+    sweep = ShardedLogLik(coords, m, rank, world, build_nbr=_oracle_build, compute=_oracle_compute)
+    cov = Covariance("matern32", 1.0, 12.0, 0.1)
+    ll = sweep.loglik(cov, values)
+    # flags: smallest non-negative over ranks, -1 if none
+    f = torch.tensor([0.0, 0.0, -1.0 if rank == 0 else 5.0 + rank, 9.0 if rank == 0 else -1.0], dtype=torch.float64)
+    comb = combine_partials(f, world).tolist()
+    out[rank] = (ll, sweep.lo, sweep.hi, comb)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_sharded_loglik_matches_single(world):
+    from oracle import nngp_oracle as O
+
+    n, m = 3001, 10
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n, m, out), nprocs=world, join=True)
+    rng = np.random.default_rng(0)
+    coords = rng.uniform(size=(n, 2))
+    values = rng.standard_normal(n)
+    nbr = O.c_knn_prior(coords, m)
+    _, _, p = O.c_bf_sweep(coords, nbr, "matern32", (1.0, 12.0, 0.1), values)
+    want = O.loglik_from_partials(p, n)
+    lls = [out[r][0] for r in range(world)]
+    assert lls[0] == lls[1]  # every rank sees the same (rank-order) sum
+    assert abs(lls[0] - want) <= 1e-12 * abs(want)
+    assert [(out[r][1], out[r][2]) for r in range(world)] == [shard_range(n, r, world) for r in range(world)]
+    assert out[0][3] == [0.0, 0.0, 6.0, 9.0]

@@ -1,0 +1,100 @@
+"""GPU: the drop-in NNGP class (mirrors pyNNGP.NNGP, /root/reference/pyNNGP/nngp.py).
+
+Attributes against the reference's own output (tests/golden/knn_ref_*.npz):
+Ns (list format, Ns[0] == []), Nt aliasing Ns, s aliasing t, wt a copy of y, ws
+the 5-NN uniform regression; per-location _CNs/_Ccross/_Cs/_Bsi/_Fsi and the
+whole-field loglik against the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["knn_ref_n200_m3", "knn_ref_n1000_m10", "knn_ref_n5000_m15"])
+def test_constructor_matches_reference(dev, name):
+    from pynngp_amd import NNGP
+
+    g = load_golden(name)
+    m = int(g["m"])
+    model = NNGP(g["coords"], g["y"], np.full_like(g["y"], 1e-3), "S=T", m, None)
+    assert model.s is model.t and model.Nt is model.Ns
+    np.testing.assert_array_equal(model.wt, g["y"])
+    assert model.wt is not model.y
+    assert model.Ns[0] == []
+    for i in range(1, len(model.Ns)):
+        assert model.Ns[i].dtype == np.int64
+        np.testing.assert_array_equal(model.Ns[i], g["Ns"][i, : min(i, m)])
+    np.testing.assert_allclose(model.ws, g["ws"], rtol=0, atol=1e-15)
+
+
+def test_reference_test_init_shape(dev):
+    """tests/test_init.py: 2-column y and eps, m=3, cov=None; self never a neighbour."""
+    from pynngp_amd import NNGP
+
+    rng = np.random.default_rng(0)
+    t = rng.uniform(size=(200, 2))
+    model = NNGP(t, np.zeros_like(t), np.ones_like(t) * 0.001, "S=T", 3, None)
+    for i in range(200):
+        assert i not in model.Ns[i]
+    assert model.ws.shape == (200, 2)
+
+
+def test_per_location_methods_vs_oracle(dev, c_oracle):
+    from pynngp_amd import NNGP, Covariance
+
+    rng = np.random.default_rng(1)
+    t = rng.uniform(size=(800, 2))
+    y = rng.standard_normal(800)
+    cov = Covariance("matern32", 1.2, 9.0, 0.05)
+    model = NNGP(t, y, None, "S=T", 12, cov)
+    nbr = model.nbr.cpu().numpy()
+    np.testing.assert_array_equal(nbr, c_oracle.c_knn_prior(t, 12))
+    for i in [0, 1, 5, 12, 13, 400, 799]:
+        CN, c, Cii = c_oracle.location_blocks(t, nbr[i], i, "matern32", cov.theta)
+        np.testing.assert_allclose(model._CNs(i), CN, rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(model._Ccross(i)[0], c, rtol=1e-13, atol=1e-15)
+        assert abs(float(np.asarray(model._Cs(i)).ravel()[0]) - Cii) < 1e-14
+        Bo, Fo = c_oracle.bf_location(t, nbr[i], i, "matern32", cov.theta)
+        np.testing.assert_allclose(model._Bsi(i), Bo, rtol=0, atol=1e-10)
+        assert abs(model._Fsi(i) - Fo) <= 1e-10 * Fo
+    B, F = model.compute_BF()
+    Bo, Fo, po = c_oracle.c_bf_sweep(t, nbr, "matern32", cov.theta, y)
+    np.testing.assert_allclose(F.cpu().numpy(), Fo, rtol=1e-10)
+    ll = model.loglik()
+    want = c_oracle.loglik_from_partials(po, 800)
+    assert abs(ll - want) <= 1e-12 * abs(want)
+    ll2 = model.loglik(cov=cov.replace(phi=4.0))
+    _, _, p2 = c_oracle.c_bf_sweep(t, nbr, "matern32", (1.2, 4.0, 0.05), y)
+    assert abs(ll2 - c_oracle.loglik_from_partials(p2, 800)) <= 1e-12 * abs(ll2)
+
+
+def test_callable_cov_and_errors(dev):
+    from pynngp_amd import NNGP, Covariance, NNGPNumericalError
+
+    rng = np.random.default_rng(2)
+    t = rng.uniform(size=(100, 2))
+    y = rng.standard_normal(100)
+
+    def user_cov(a, b):
+        d = np.sqrt(((a[:, None, :] - b[None, :, :]) ** 2).sum(-1))
+        return 2.0 * np.exp(-3.0 * d)
+
+    model = NNGP(t, y, None, "S=T", 4, user_cov)
+    assert model._CNs(10).shape == (4, 4)
+    with pytest.raises(TypeError):
+        model._Bsi(10)
+    with pytest.raises(NotImplementedError):
+        model.oneSample()
+    with pytest.raises(NotImplementedError):
+        NNGP(t, y, None, ("subset", 10), 4, None)
+    with pytest.raises(ValueError):
+        NNGP(t, y, None, "S=X", 4, None)
+    dup = t.copy()
+    model = NNGP(dup, y, None, "S=T", 4, Covariance("exponential", 1.0, 3.0, 0.0))
+    model.nbr[50, 1] = model.nbr[50, 0]
+    with pytest.raises(NNGPNumericalError, match="location 50"):
+        model.loglik()
