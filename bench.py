@@ -106,8 +106,9 @@ def main():
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=["exponential", "matern32"])
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
-    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
+    ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
@@ -132,7 +133,7 @@ def main():
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo)
+    sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order)
     torch.cuda.synchronize()
     knn_s = time.perf_counter() - t0
     want_bf = not args.loglik_only
@@ -193,6 +194,7 @@ def main():
                 "kind": args.kind,
                 "theta": [sigma2, phi, tau2],
                 "algo": args.algo,
+                "row_order": "index" if args.no_order else "z-order",
                 "write_BF": want_bf,
                 "global_batch": n_total,
                 "parallelism": f"dp{world} (contiguous location shards, all-gather of 4 partials per sweep)",

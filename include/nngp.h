@@ -41,6 +41,8 @@ extern "C" {
 #define NNGP_ALGO_AUTO 0 /* lane kernel for m <= 16, wave kernel above */
 #define NNGP_ALGO_LANE 1 /* one lane per location (m <= 16)           */
 #define NNGP_ALGO_WAVE 2 /* one wavefront per location (m <= 63)      */
+#define NNGP_ALGO_PAIR 3 /* two lanes per location (m in 10,15,16,20)   */
+#define NNGP_ALGO_QUAD 4 /* four lanes per location (m in 10,15,16,20)  */
 
 #define NNGP_MAX_M 63
 
@@ -92,14 +94,33 @@ int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_
  *   log-lik = -1/2 (n_rows log 2 pi + partials[0] + partials[1]).
  * Rows flagged in partials[2] get B = F = NaN.  The sum order is fixed, so the
  * partials are bit-reproducible run to run.
- * coords: (n_points, 2); nbr: (n_rows, m); values: (n_points,) or NULL;
+ * coords: (n_points, 2); nbr: (n_rows, m); order: NULL (row t of nbr is location
+ * i0 + t) or the nngp_row_order layout (row t of nbr is location i0 + order[t],
+ * i.e. pass nbr_sorted); values: (n_points,) or NULL;
  * B, F: may be NULL (log-lik only); partials: 4 doubles.
  * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, algo) bytes, 256-B aligned.
  * ------------------------------------------------------------------------- */
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo);
-int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, int64_t n_rows, int32_t m, int64_t i0,
-                  int32_t kind, double sigma2, double phi, double tau2, const double *values, double *B, double *F,
-                  double *partials, void *workspace, size_t workspace_bytes, int32_t algo, void *stream);
+int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, const int32_t *order, int64_t n_rows,
+                  int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2, const double *values,
+                  double *B, double *F, double *partials, void *workspace, size_t workspace_bytes, int32_t algo,
+                  void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Visiting order for nngp_bf_sweep (a speed option; no reference counterpart:
+ * the reference visits locations in input order, nngp.py:51).
+ * order[t] = the t-th local row (0 .. n_rows-1) of locations i0 .. i0+n_rows-1
+ * in Z-order of their coordinates, ties by row; if nbr_sorted is non-NULL it
+ * receives nbr's rows in that order (nbr_sorted[t] = nbr[order[t]], (n_rows, m)).
+ * Passing (nbr_sorted, order) to nngp_bf_sweep keeps each block's / XCD's
+ * neighbour gathers spatially compact (L2 hits) and its index reads coalesced;
+ * B and F are bit-identical with or without it (still written at their natural
+ * rows), the partials' summation order follows it.
+ * Workspace: nngp_row_order_workspace_bytes(n_rows).
+ * ------------------------------------------------------------------------- */
+size_t nngp_row_order_workspace_bytes(int64_t n_rows);
+int nngp_row_order(const double *coords, int64_t n_points, const int32_t *nbr, int32_t m, int64_t i0, int64_t n_rows,
+                   int32_t *order, int32_t *nbr_sorted, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Host helper: -1/2 (n_rows log 2 pi + p[0] + p[1]) from host-resident partials. */
 double nngp_loglik_from_partials(const double *partials_host, int64_t n_rows);

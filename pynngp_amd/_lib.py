@@ -24,10 +24,12 @@ SYMBOLS = (
     "nngp_bf_sweep_workspace_bytes",
     "nngp_bf_sweep",
     "nngp_loglik_from_partials",
+    "nngp_row_order_workspace_bytes",
+    "nngp_row_order",
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1}
-ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2}
+ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4}
 MAX_M = 63
 
 
@@ -60,7 +62,11 @@ def load() -> ctypes.CDLL:
     lib.nngp_knn_query.restype = ctypes.c_int
     lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
     lib.nngp_bf_sweep_workspace_bytes.restype = SZ
-    lib.nngp_bf_sweep.argtypes = [P, I64, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_sweep.argtypes = [P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_row_order_workspace_bytes.argtypes = [I64]
+    lib.nngp_row_order_workspace_bytes.restype = SZ
+    lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
+    lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_loglik_from_partials.argtypes = [P, I64]
     lib.nngp_loglik_from_partials.restype = D
@@ -157,13 +163,16 @@ def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
 def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2: float, phi: float,
              tau2: float = 0.0, values: Optional[torch.Tensor] = None, want_bf: bool = True,
              algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
-             partials: Optional[torch.Tensor] = None,
-             workspace: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+             partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+             order: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
 
     Returns ``(B, F, partials)`` (B, F None when ``want_bf`` is False); partials is a
     float64 device tensor ``[sum log F, sum r^2/F, first bad-pivot row, first bad-index row]``.
-    Stream-ordered on torch's current stream; no host synchronisation.
+    Stream-ordered on torch's current stream; no host synchronisation.  With
+    ``order`` (int32 (rows,), from :func:`row_order`) row t of ``nbr`` must hold the
+    neighbours of location ``i0 + order[t]`` (pass ``nbr_sorted``); only the visiting
+    order changes, B and F are written at their natural rows.
     """
     coords = _as_coords(coords)
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
@@ -173,8 +182,10 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
         if values.dtype != torch.float64 or values.shape != (coords.shape[0],):
             raise ValueError("values must be float64 (N,)")
         values = values.contiguous()
-    dev = _require_gpu(coords, nbr, values)
+    dev = _require_gpu(coords, nbr, values, order)
     rows, m = nbr.shape
+    if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
+        raise ValueError("order must be int32 (rows,)")
     if kind not in KIND_CODES:
         raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
     lib = load()
@@ -188,11 +199,40 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
-    _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), rows, m, i0, KIND_CODES[kind],
+    _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
                              float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
     return B, F, partials
+
+
+def row_order(coords: torch.Tensor, i0: int = 0, rows: Optional[int] = None,
+              nbr: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Z-order visiting order of locations i0 .. i0+rows-1 for :func:`bf_sweep`.
+
+    Returns ``(order, nbr_sorted)``: ``order`` int32 (rows,) and, when ``nbr`` (the
+    natural-order neighbour rows of those locations) is given, ``nbr_sorted[t] =
+    nbr[order[t]]``.  Sweep with ``bf_sweep(coords, nbr_sorted, i0, ..., order=order)``.
+    """
+    coords = _as_coords(coords)
+    dev = _require_gpu(coords, nbr)
+    n = coords.shape[0]
+    rows = n - i0 if rows is None else int(rows)
+    m = 0 if nbr is None else nbr.shape[1]
+    if nbr is not None:
+        if nbr.dtype != torch.int32 or nbr.shape[0] != rows:
+            raise ValueError("nbr must be int32 (rows, m)")
+        nbr = nbr.contiguous()
+    out = torch.empty((rows,), dtype=torch.int32, device=dev)
+    srt = None if nbr is None else torch.empty_like(nbr)
+    lib = load()
+    need = lib.nngp_row_order_workspace_bytes(rows)
+    if need == 0:
+        raise NNGPExtensionError("nngp_row_order_workspace_bytes failed")
+    ws = _workspace(need, dev)
+    _check(lib.nngp_row_order(_ptr(coords), n, _ptr(nbr), m, i0, rows, _ptr(out), _ptr(srt), _ptr(ws), ws.numel(),
+                              _stream(dev)), "nngp_row_order")
+    return out, srt
 
 
 def bf_workspace(rows: int, m: int, algo: str, device) -> torch.Tensor:

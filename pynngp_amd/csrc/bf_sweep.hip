@@ -38,14 +38,16 @@ namespace nngp {
 // --------------------------------------------------------------------------
 template <int M, int KIND>
 __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coords, int64_t n_points,
-                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0,
+                                               const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
+                                               int64_t n_rows, int64_t i0,
                                                const CovParams P, const double* __restrict__ values,
                                                double* __restrict__ Bout, double* __restrict__ Fout,
                                                double* __restrict__ wpart, unsigned long long* __restrict__ status) {
     constexpr int N1 = M + 1;  // joint block order
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const bool live = r < n_rows;
-    const int64_t rr = live ? r : n_rows - 1;
+    const int64_t rl = live ? r : n_rows - 1;
+    const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
     const int64_t i = i0 + rr;
 
     bool valid[M];
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
     bool bad_index = false;
 #pragma unroll
     for (int a = 0; a < M; ++a) {
-        const int32_t j = nbr[rr * M + a];
+        const int32_t j = nbr[rl * M + a];
         const bool v = j >= 0 && (int64_t)j < n_points;
         bad_index |= j >= 0 && !v;
         valid[a] = v;
@@ -170,7 +172,7 @@ template <int M, int KIND>
 static void launch_lane(const BfArgs& a, const CovParams& P, hipStream_t s) {
     const int64_t blocks = (a.n_rows + 255) / 256;
     hipLaunchKernelGGL((bf_lane<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.n_rows, a.i0, P, a.values, a.B, a.F, a.wpart, a.status);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.wpart, a.status);
 }
 
 int64_t bf_lane_waves(int64_t n_rows) { return (n_rows + 255) / 256 * 4; }
@@ -203,6 +205,10 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     if (algo == kAlgoLane) {
         ok = a.kind == 1 ? launch_lane_m<1>(a, P, s) : launch_lane_m<0>(a, P, s);
         nw = bf_lane_waves(a.n_rows);
+    } else if (algo == kAlgoPair || algo == kAlgoQuad) {
+        const int lanes = algo == kAlgoPair ? 2 : 4;
+        ok = bf_group_launch(a, P, lanes, s);
+        nw = bf_group_waves(a.n_rows, lanes);
     } else {
         nw = bf_wave_waves(a.n_rows);
         ok = bf_wave_launch(a, P, nw, s);

@@ -17,7 +17,8 @@ namespace nngp {
 // --------------------------------------------------------------------------
 template <int NR, int KIND>
 __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
-                                               const int32_t* __restrict__ nbr, int64_t n_rows, int64_t i0, int M,
+                                               const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
+                                               int64_t n_rows, int64_t i0, int M,
                                                const CovParams P, const double* __restrict__ values,
                                                double* __restrict__ Bout, double* __restrict__ Fout,
                                                double* __restrict__ wpart, unsigned long long* __restrict__ status) {
@@ -26,11 +27,12 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
 
-    for (int64_t rr = wave; rr < n_rows; rr += n_waves) {
+    for (int64_t rl = wave; rl < n_rows; rl += n_waves) {
+        const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
         const int64_t i = i0 + rr;
         // lane a < M: neighbour slot a; lane M: the location itself; lanes > M: far-away identity rows
         int32_t j = -1;
-        if (lane < M) j = nbr[rr * M + lane];
+        if (lane < M) j = nbr[rl * M + lane];
         const bool is_self = lane == M;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
         const bool bad_index = j >= 0 && !in_range;
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
 template <int NR, int KIND>
 static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s) {
     hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)(n_waves / 4)), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.wpart, a.status);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.wpart, a.status);
 }
 
 int64_t bf_wave_waves(int64_t n_rows) {

@@ -32,7 +32,10 @@ int resolve_algo(int32_t algo, int32_t m) {
 }
 
 int64_t bf_waves(int64_t n_rows, int algo) {
-    return algo == nngp::kAlgoLane ? nngp::bf_lane_waves(n_rows) : nngp::bf_wave_waves(n_rows);
+    if (algo == nngp::kAlgoLane) return nngp::bf_lane_waves(n_rows);
+    if (algo == nngp::kAlgoPair) return nngp::bf_group_waves(n_rows, 2);
+    if (algo == nngp::kAlgoQuad) return nngp::bf_group_waves(n_rows, 4);
+    return nngp::bf_wave_waves(n_rows);
 }
 }  // namespace
 
@@ -53,7 +56,8 @@ size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
     return align256(16) + align256((size_t)nw * 2 * sizeof(double));
 }
 
-int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, int64_t n_rows, int32_t m, int64_t i0,
+int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
+                  int32_t m, int64_t i0,
                   int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
                   double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
     if (coords == nullptr || partials == nullptr || workspace == nullptr)
@@ -70,9 +74,11 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, in
     if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
     int a = resolve_algo(algo, m);
-    if (a != nngp::kAlgoLane && a != nngp::kAlgoWave) return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    if (a < nngp::kAlgoLane || a > nngp::kAlgoQuad) return fail(NNGP_EINVAL, "unknown algo %d", algo);
     if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
         return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
+    if ((a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !nngp::bf_group_supported(m, a == nngp::kAlgoPair ? 2 : 4))
+        return fail(NNGP_EUNSUP, "no %s-lane kernel instantiated for m=%d", a == nngp::kAlgoPair ? "2" : "4", m);
     const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, algo);
     if (workspace_bytes < need)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
@@ -83,10 +89,33 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, in
     double* wpart = (double*)(w + align256(16));
     hipError_t e = hipMemsetAsync(status, 0xff, 2 * sizeof(unsigned long long), s);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(status)");
-    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, values, B, F,
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, B, F,
                       partials, wpart, status};
     e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
+    return NNGP_OK;
+}
+
+size_t nngp_row_order_workspace_bytes(int64_t n_rows) { return nngp::row_order_workspace_bytes(n_rows); }
+
+int nngp_row_order(const double* coords, int64_t n_points, const int32_t* nbr, int32_t m, int64_t i0, int64_t n_rows,
+                   int32_t* order, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes, void* stream) {
+    if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
+    if (n_rows < 0 || i0 < 0 || i0 + n_rows > n_points)
+        return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
+                    (long long)n_points);
+    if (n_rows > INT32_MAX) return fail(NNGP_EINVAL, "n_rows must be < 2^31");
+    if (n_rows > 0 && order == nullptr) return fail(NNGP_EINVAL, "order must be non-null");
+    if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
+    if (nbr_sorted != nullptr && m > 0 && n_rows > 0 && nbr == nullptr)
+        return fail(NNGP_EINVAL, "nbr must be non-null when nbr_sorted is requested");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    const size_t need = nngp::row_order_workspace_bytes(n_rows);
+    if (need == 0 || workspace_bytes < need)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
+    hipError_t e = nngp::row_order_launch(coords, i0, n_rows, order, nbr, m, nbr_sorted, workspace, workspace_bytes,
+                                          (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "row_order launch");
     return NNGP_OK;
 }
 

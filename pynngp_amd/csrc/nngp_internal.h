@@ -17,17 +17,20 @@ constexpr double kFar = 1e150;
 constexpr int kAlgoAuto = 0;
 constexpr int kAlgoLane = 1;
 constexpr int kAlgoWave = 2;
+constexpr int kAlgoPair = 3;  // bf_group, 2 lanes per location
+constexpr int kAlgoQuad = 4;  // bf_group, 4 lanes per location
 constexpr int kLaneMaxM = 16;
 
 struct BfArgs {
     const double* coords;  // (n_points, 2) row-major
     int64_t n_points;
-    const int32_t* nbr;  // (n_rows, m), -1 padded; row r is location i0 + r
+    const int32_t* nbr;  // (n_rows, m), -1 padded; row t is location i0 + (order ? order[t] : t)
     int64_t n_rows;
     int64_t i0;
     int m;
     int kind;
     double sigma2, phi, tau2;
+    const int32_t* order;      // (n_rows,) local row of nbr row t (nngp_row_order layout), or null (identity)
     const double* values;      // (n_points,) or null
     double* B;                 // (n_rows, m) or null
     double* F;                 // (n_rows,) or null
@@ -38,6 +41,9 @@ struct BfArgs {
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
 bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s);
+bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t s);
+bool bf_group_supported(int m, int lanes);
+int64_t bf_group_waves(int64_t n_rows, int lanes);
 int64_t bf_lane_waves(int64_t n_rows);
 int64_t bf_wave_waves(int64_t n_rows);
 
@@ -55,6 +61,20 @@ hipError_t knn_plan(int64_t n_points, KnnPlan* plan);
 // prior mode: rows [q0, q1) of coords against coords[0:i]; query mode: query[q0:q1] against all coords
 hipError_t knn_launch(bool prior, const double* coords, int64_t n_points, int m, const double* query, int64_t q0,
                       int64_t q1, int32_t* nbr, void* workspace, const KnnPlan& plan, hipStream_t s);
+
+// row-order plan (nngp_row_order): Morton-sorted local rows for cache locality
+size_t row_order_workspace_bytes(int64_t n_rows);
+hipError_t row_order_launch(const double* coords, int64_t i0, int64_t n_rows, int32_t* order, const int32_t* nbr,
+                            int m, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes, hipStream_t s);
+
+// Bijective XCD-aware block remap: blocks are dealt round-robin over the 8 XCDs
+// (b % 8 shares an L2), so give each XCD a contiguous range of logical blocks;
+// with Morton-ordered rows that keeps one XCD's gathers inside one spatial region
+// (its own L2).  Speed only: any placement gives identical results.
+__device__ __forceinline__ int64_t xcd_logical_block(int64_t b, int64_t nb) {
+    const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
 
 // ---------------------------------------------------------------- wave helpers
 __device__ __forceinline__ double wave_bcast(double v, int lane) {

@@ -134,6 +134,8 @@ class NNGP:
 
     def _make_s_neighbor_sets(self):
         self.nbr = _lib.knn_prior(self._s_dev, self.m)  # int32 (N, m) on the device, -1 padded
+        # Z-order visiting order + neighbour rows in that order, for the sweeps (speed only)
+        self._order, self._nbr_sorted = _lib.row_order(self._s_dev, nbr=self.nbr)
         self._Ns = None
 
     def _make_t_neighbor_sets(self):
@@ -215,7 +217,7 @@ class NNGP:
     def compute_BF(self, algo: str = "auto"):
         """All B (N, m) and F (N,) as device tensors (one fused sweep)."""
         cv = self._covariance()
-        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr, 0, cv.kind, *cv.theta, algo=algo)
+        B, F, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, algo=algo, order=self._order)
         _raise_on_bad(p.cpu().numpy())
         self._B, self._F = B, F
         return B, F
@@ -236,7 +238,8 @@ class NNGP:
                             dtype=torch.float64).to(self.device)
         if v.dim() != 1:
             raise ValueError("loglik needs one value per location (1-D values)")
-        _, _, p = _lib.bf_sweep(self._s_dev, self.nbr, 0, cv.kind, *cv.theta, values=v, want_bf=False, algo=algo)
+        _, _, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, values=v, want_bf=False,
+                                algo=algo, order=self._order)
         ph = p.cpu().numpy()
         _raise_on_bad(ph)
         n = self.nbr.shape[0]

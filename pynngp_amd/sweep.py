@@ -54,7 +54,8 @@ class ShardedLogLik:
     """
 
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
-                 algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None):
+                 algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
+                 spatial_order: bool = True):
         self.coords = coords
         self.n = coords.shape[0]
         self.m = int(m)
@@ -68,7 +69,11 @@ class ShardedLogLik:
             self.nbr = build_nbr(coords, self.m, self.lo, self.hi)
         self._ws = None
         self._partials = None
+        self.order = None
         if compute is None:
+            self._nbr_sweep = self.nbr
+            if spatial_order and self.hi > self.lo:
+                self.order, self._nbr_sweep = _lib.row_order(coords, self.lo, self.hi - self.lo, self.nbr)
             self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device)
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
             self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
@@ -79,9 +84,9 @@ class ShardedLogLik:
         if self._compute is not None:
             return self._compute(self, cov, values, want_bf)
         B, F = (self._B, self._F) if want_bf else (None, None)
-        _, _, p = _lib.bf_sweep(self.coords, self.nbr, self.lo, cov.kind, *cov.theta, values=values,
+        _, _, p = _lib.bf_sweep(self.coords, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
                                 want_bf=want_bf, algo=self.algo, B=B, F=F, partials=self._partials,
-                                workspace=self._ws)
+                                workspace=self._ws, order=self.order)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True) -> torch.Tensor:

@@ -56,7 +56,7 @@ def _sweep(lib, **kw):
              values=None, B=None, F=None, partials=1, workspace=256, workspace_bytes=1 << 20, algo=0, stream=None)
     a.update(kw)
     P = lambda v: None if v is None else ctypes.c_void_p(v)  # noqa: E731
-    return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], P(a["nbr"]), a["n_rows"], a["m"], a["i0"], a["kind"],
+    return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], P(a["nbr"]), None, a["n_rows"], a["m"], a["i0"], a["kind"],
                              a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]),
                              P(a["partials"]), P(a["workspace"]), a["workspace_bytes"], a["algo"], P(a["stream"]))
 
@@ -81,6 +81,15 @@ def _sweep(lib, **kw):
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code
     assert msg in lib.nngp_last_error().decode()
+
+
+def test_row_order_rejects(lib):
+    P = ctypes.c_void_p
+    assert lib.nngp_row_order(None, 10, None, 0, 0, 10, P(1), None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, None, 0, 5, 6, P(1), None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, None, 0, 0, 10, None, None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, None, 5, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, P(1), 70, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -4
 
 
 def test_knn_rejects(lib):

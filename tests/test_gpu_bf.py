@@ -65,20 +65,29 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("algo", ["lane", "wave"])
+GROUP_M = (10, 15, 16, 20)  # instantiated for the 2- and 4-lane kernels
+
+
+@pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad"])
 @pytest.mark.parametrize("kind,theta,m", CASES)
 def test_bf_vs_oracle(lib, dev, c_oracle, kind, theta, m, algo):
+    if algo in ("pair", "quad") and m not in GROUP_M:
+        pytest.skip("not instantiated")
     coords, y = _field(6000, m)
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, algo)
 
 
-@pytest.mark.parametrize("m", [20, 31, 40, 63])
-def test_bf_wave_large_m(lib, dev, c_oracle, m):
+@pytest.mark.parametrize("m", [20, 24, 31, 40, 63])
+def test_bf_large_m(lib, dev, c_oracle, m):
     coords, y = _field(3000, 100 + m)
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 8.0, 0.05), y, "auto")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, "wave")
+    if m in GROUP_M:
+        for algo in ("pair", "quad"):
+            _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, algo)
+            _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 30.0, 0.0), y, algo)
 
 
 def test_bf_m0_and_no_values(lib, dev, c_oracle):
@@ -137,7 +146,7 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     sing = nbr.copy()
     sing[1234, 1] = sing[1234, 0]  # repeated neighbour: C_N singular, second pivot exactly 0 (sigma2 = 1)
     sing[1500, 1] = sing[1500, 0]
-    for algo in ["lane", "wave"]:
+    for algo in ["lane", "wave", "pair", "quad"]:
         B, F, p = lib.bf_sweep(c, torch.from_numpy(sing).to(dev), 0, "exponential", 1.0, 5.0, 0.0, algo=algo)
         _, _, po = c_oracle.c_bf_sweep(coords, sing, "exponential", (1.0, 5.0, 0.0), None)
         assert p[2].item() == 1234 == po[2]
@@ -159,11 +168,13 @@ def test_bf_full_size_properties(lib, dev, c_oracle):
     nb = lib.knn_prior(c, m)
     theta = (1.0, 30.0, 0.0)
     B, F, p = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="lane")
-    Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="wave")
-    assert torch.allclose(F, Fw, rtol=1e-12, atol=0)
-    assert torch.allclose(B, Bw, rtol=0, atol=1e-10)
-    ll, llw = (c_oracle.loglik_from_partials(q.cpu().numpy(), n) for q in (p, pw))
-    assert abs(ll - llw) <= 1e-12 * abs(ll)
+    ll = c_oracle.loglik_from_partials(p.cpu().numpy(), n)
+    for algo in ("wave", "pair", "quad"):
+        Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo=algo)
+        assert torch.allclose(F, Fw, rtol=1e-12, atol=0)
+        assert torch.allclose(B, Bw, rtol=0, atol=1e-10)
+        llw = c_oracle.loglik_from_partials(pw.cpu().numpy(), n)
+        assert abs(ll - llw) <= 1e-12 * abs(ll)
     Fh = F.cpu().numpy()
     assert np.all(Fh > 0) and np.all(Fh <= 1.0 + 1e-12)
     rows = np.random.default_rng(1).integers(0, n, 4000)
@@ -188,3 +199,25 @@ def test_bf_op_registered(dev, c_oracle):
     assert np.allclose(F.cpu().numpy(), Fo, rtol=RTOL_F, atol=0)
     _, _, p2 = torch.ops.nngp.bf_sweep(c, nb, 0, 1, 1.0, 5.0, 0.1, None, False, 0)
     assert abs(p2[0].item() - po[0]) <= 1e-12 * abs(po[0])
+
+
+@pytest.mark.parametrize("algo", ["lane", "pair", "quad", "wave"])
+def test_bf_row_order_bit_identical(lib, dev, c_oracle, algo):
+    """Visiting rows in Z-order (nngp_row_order) changes nothing per row."""
+    coords, y = _field(30000, 12)
+    c = torch.from_numpy(coords).to(dev)
+    v = torch.from_numpy(y).to(dev)
+    nb = lib.knn_prior(c, 15)
+    for i0, rows in [(0, 30000), (777, 10000), (29990, 10)]:
+        order, srt = lib.row_order(c, i0, rows, nb[i0:i0 + rows])
+        oh = order.cpu().numpy()
+        assert np.array_equal(np.sort(oh), np.arange(rows))
+        assert torch.equal(srt, nb[i0:i0 + rows][order.long()])
+        B1, F1, p1 = lib.bf_sweep(c, nb[i0:i0 + rows], i0, "exponential", 1.0, 30.0, 0.0, values=v, algo=algo)
+        B2, F2, p2 = lib.bf_sweep(c, srt, i0, "exponential", 1.0, 30.0, 0.0, values=v, algo=algo, order=order)
+        assert torch.equal(B1, B2) and torch.equal(F1, F2)
+        assert torch.allclose(p1[:2], p2[:2], rtol=1e-13, atol=0) and torch.equal(p1[2:], p2[2:])
+    # Z-order really is spatially coherent: consecutive rows are close
+    order = lib.row_order(c)[0].cpu().numpy()
+    step = np.linalg.norm(np.diff(coords[order], axis=0), axis=1)
+    assert np.median(step) < 0.01
