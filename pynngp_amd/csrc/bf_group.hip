@@ -1,237 +1,30 @@
-// B/F + log-likelihood sweep with P lanes per location (P = 1, 2, 4).
-//
-// Same formulation and outputs as bf_lane (bf_sweep.hip documents it and the
-// reference methods nngp.py:73-96 it replaces): the (m+1)x(m+1) joint block
-// [[C_N + tau2 I, c], [c^T, sigma2 + tau2]] with the value column appended, m
-// right-looking elimination steps, B = L_N^{-T} v.
-//
-// Why P > 1: with one lane per location the whole joint block lives in one
-// lane's VGPRs (136 doubles at m = 15), which pins the kernel at one wave per
-// SIMD and leaves every latency exposed.  Here the block's rows are dealt
-// cyclically over the P lanes of a group (lane q owns rows a = P*s + q), so a
-// lane holds ~1/P of it and two or more waves fit per SIMD.  Column values move
-// between the lanes of a group with DPP quad_perm broadcasts (the groups are
-// aligned inside DPP quads), never through LDS:
-//   * build: every lane computes the covariances of its own rows (~1/P of the
-//     pairs) against the group-broadcast neighbour coordinates;
-//   * step p: the pivot and column p are broadcast from their owner lanes, each
-//     lane updates its own rows;
-//   * back-substitution: per-lane partial dot products + a group butterfly sum.
-// Rows are padded to a multiple of P with far-away (decoupled) slots.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "nngp_math.h"
-#include "nngp_internal.h"
+// Dispatch for the P-lanes-per-location sweep kernels (template in bf_group.h,
+// instantiations in bf_pair_*.hip / bf_quad.hip).
+#include "bf_group.h"
 
 namespace nngp {
 
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const long long u = __double_as_longlong(v);
-    // bound_ctrl: every lane reads a valid source lane, so no "old" value (and no init mov) is needed
-    const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffll), CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xf, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
-
-// value of v in lane `src` of this lane's P-group (src folds to a constant after unrolling)
-template <int P>
-__device__ __forceinline__ double grp_bcast(double v, int src) {
-    if (P == 1) return v;
-    if (P == 2) return src == 0 ? dpp_f64<0xA0>(v) : dpp_f64<0xF5>(v);  // quad_perm [s,s,s+2,s+2]
-    switch (src) {                                                      // quad_perm [s,s,s,s]
-        case 0:
-            return dpp_f64<0x00>(v);
-        case 1:
-            return dpp_f64<0x55>(v);
-        case 2:
-            return dpp_f64<0xAA>(v);
-        default:
-            return dpp_f64<0xFF>(v);
-    }
-}
-
-// sum of v over the P lanes of the group (same value, same rounding, in every lane)
-template <int P>
-__device__ __forceinline__ double grp_sum(double v) {
-    if (P == 1) return v;
-    v = v + dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
-    if (P == 4) v = v + dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
-    return v;
-}
-
-template <int M, int KIND, int P>
-__global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coords, int64_t n_points,
-                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
-                                                int64_t n_rows, int64_t i0,
-                                                const CovParams Pc, const double* __restrict__ values,
-                                                double* __restrict__ Bout, double* __restrict__ Fout,
-                                                double* __restrict__ wpart, unsigned long long* __restrict__ status) {
-    constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
-    constexpr int S = (NR + P - 1) / P;     // local rows per lane
-    const int64_t tid = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int q = (int)(threadIdx.x % P);
-    const int64_t r = tid / P;
-    const bool live = r < n_rows;
-    const int64_t rl = live ? r : n_rows - 1;
-    const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
-    const int64_t i = i0 + rr;
-
-    // ---- own rows a = P*s + q: neighbour slot (a < M), the location (a == M), padding (a > M)
-    double ox[S], oy[S], z[S];
-    bool oval[S];
-    bool bad_index = false;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        const int a = P * s + q;
-        int32_t j = -1;
-        if (a < M) j = nbr[rl * M + a];
-        const bool in_range = j >= 0 && (int64_t)j < n_points;
-        bad_index |= j >= 0 && !in_range;
-        const bool valid = in_range || a == M;
-        oval[s] = in_range;
-        const int64_t src = a == M ? i : (in_range ? (int64_t)j : 0);
-        const double2 x = coords[src];
-        ox[s] = valid ? x.x : kFar * (a + 1);
-        oy[s] = valid ? x.y : 0.0;
-        z[s] = (values != nullptr && valid) ? values[src] : 0.0;
-    }
-
-    // ---- joint block rows: R[s][b], b < min(P*s + P, NR)
-    double R[S][NR];
-    {
-        double X[NR], Y[NR];
-#pragma unroll
-        for (int b = 0; b < NR; ++b) {
-            X[b] = grp_bcast<P>(ox[b / P], b % P);
-            Y[b] = grp_bcast<P>(oy[b / P], b % P);
-        }
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int a = P * s + q;
-#pragma unroll
-            for (int b = 0; b < NR; ++b) {
-                if (b >= P * s + P) continue;  // beyond this local row's width
-                if (b < P * s) {
-                    R[s][b] = nngp_cov_d2<KIND>(Pc, nngp_d2(ox[s], oy[s], X[b], Y[b]));
-                } else if (b < P * s + P - 1) {  // diagonal block: lane-dependent
-                    const double c = nngp_cov_d2<KIND>(Pc, nngp_d2(ox[s], oy[s], X[b], Y[b]));
-                    R[s][b] = b < a ? c : (b == a ? Pc.diag : 0.0);
-                } else {
-                    R[s][b] = b == a ? Pc.diag : 0.0;
-                }
-            }
-        }
-    }
-
-    // ---- right-looking elimination; the owner of row p keeps 1/L[p][p] in R[p/P][p]
-    bool bad = false;
-#pragma unroll
-    for (int p = 0; p < M; ++p) {
-        const int qp = p % P, sp = p / P;
-        const double piv = grp_bcast<P>(R[sp][p], qp);
-        bad |= !(piv > 0.0);
-        const double ip = nngp_rsqrt(piv);
-        R[sp][p] = q == qp ? ip : R[sp][p] * ip;
-#pragma unroll
-        for (int s = sp + 1; s < S; ++s) R[s][p] *= ip;
-        z[sp] = q == qp ? z[sp] * ip : z[sp];
-        const double zp = grp_bcast<P>(z[sp], qp);
-        double lb[NR];
-#pragma unroll
-        for (int b = p + 1; b < NR; ++b) lb[b] = grp_bcast<P>(R[b / P][p], b % P);
-#pragma unroll
-        for (int s = sp; s < S; ++s) {
-#pragma unroll
-            for (int b = p + 1; b < NR; ++b) {
-                if (b >= P * s + P) continue;
-                R[s][b] = fma(-R[s][p], lb[b], R[s][b]);
-            }
-            if (s == sp) {
-                if (P > 1) z[s] = q > qp ? fma(-R[s][p], zp, z[s]) : z[s];
-            } else {
-                z[s] = fma(-R[s][p], zp, z[s]);
-            }
-        }
-    }
-    const double F = grp_bcast<P>(R[M / P][M], M % P);
-    const double res = grp_bcast<P>(z[M / P], M % P);
-    bad |= !(F > 0.0);
-
-    if (Bout != nullptr) {
-        // B = L_N^{-T} v, v = row M of L; lane q ends with bown[s] = b_{P*s+q}
-        double bown[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) bown[s] = 0.0;
-#pragma unroll
-        for (int a = M - 1; a >= 0; --a) {
-            double part = 0.0;
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                if (P * s + P - 1 <= a) continue;  // every row of this local row is <= a
-                const int ar = P * s + q;
-                const double t = R[s][a] * bown[s];
-                part = (ar > a && ar < M) ? part + t : part;
-            }
-            const double tot = grp_sum<P>(part);
-            const double va = grp_bcast<P>(R[M / P][a], M % P);
-            const double iva = grp_bcast<P>(R[a / P][a], a % P);
-            const double ba = (va - tot) * iva;
-            bown[a / P] = q == a % P ? ba : bown[a / P];
-        }
-        if (live) {
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const int a = P * s + q;
-                if (a < M) Bout[rr * M + a] = bad ? NAN : (oval[s] ? bown[s] : 0.0);
-            }
-        }
-    }
-    const bool lead = live && q == 0;
-    if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
-
-    double lf = 0.0, qq = 0.0;
-    if (lead) {
-        lf = log(F);
-        qq = res * res / F;
-        if (bad) atomicMin(status + 0, (unsigned long long)i);
-    }
-    if (live && bad_index) atomicMin(status + 1, (unsigned long long)i);
-    wave_partials_store(lf, qq, wpart, tid);
-}
-
-template <int M, int KIND, int P>
-static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    const int64_t blocks = (a.n_rows * P + 255) / 256;
-    hipLaunchKernelGGL((bf_group<M, KIND, P>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.wpart, a.status);
-}
+bool bf_pair_launch_a(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_pair_launch_b(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_pair_launch_c(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_pair_launch_d(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_quad_launch(const BfArgs&, const CovParams&, hipStream_t);
 
 int64_t bf_group_waves(int64_t n_rows, int P) { return (n_rows * P + 255) / 256 * 4; }
 
-template <int KIND, int P>
-static bool launch_group_m(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    switch (a.m) {
-#define NNGP_GROUP_CASE(MM)                       \
-    case MM:                                      \
-        launch_group_mkp<MM, KIND, P>(a, Pc, s); \
-        return true;
-        NNGP_GROUP_CASE(10) NNGP_GROUP_CASE(15) NNGP_GROUP_CASE(16) NNGP_GROUP_CASE(20)
-#undef NNGP_GROUP_CASE
-        default:
-            return false;
-    }
-}
-
 bool bf_group_supported(int m, int P) {
-    return (P == 2 || P == 4) && (m == 10 || m == 15 || m == 16 || m == 20);
+    if (P == 2) return m >= 10 && m <= 20;
+    if (P == 4) return m == 15 || m == 16 || m == 20;
+    return false;
 }
 
 bool bf_group_launch(const BfArgs& a, const CovParams& Pc, int P, hipStream_t s) {
-    if (P == 2) return a.kind == 1 ? launch_group_m<1, 2>(a, Pc, s) : launch_group_m<0, 2>(a, Pc, s);
-    if (P == 4) return a.kind == 1 ? launch_group_m<1, 4>(a, Pc, s) : launch_group_m<0, 4>(a, Pc, s);
-    return false;
+    if (!bf_group_supported(a.m, P)) return false;
+    if (P == 4) return bf_quad_launch(a, Pc, s);
+    if (a.m <= 13) return bf_pair_launch_a(a, Pc, s);
+    if (a.m <= 16) return bf_pair_launch_b(a, Pc, s);
+    if (a.m <= 18) return bf_pair_launch_c(a, Pc, s);
+    return bf_pair_launch_d(a, Pc, s);
 }
 
 }  // namespace nngp

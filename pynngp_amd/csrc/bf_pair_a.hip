@@ -1,0 +1,14 @@
+// Instantiations of bf_group (bf_group.h) with 2 lanes per location for m in {10, 11, 12, 13}.
+// Split into several translation units so the (large, fully unrolled) kernels compile in parallel.
+#include "bf_group.h"
+
+namespace nngp {
+
+bool bf_pair_launch_a(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
+    return launch_group_if<10, 2>(a, Pc, s) ||
+           launch_group_if<11, 2>(a, Pc, s) ||
+           launch_group_if<12, 2>(a, Pc, s) ||
+           launch_group_if<13, 2>(a, Pc, s);
+}
+
+}  // namespace nngp

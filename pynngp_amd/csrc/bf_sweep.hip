@@ -50,30 +50,30 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
     const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
     const int64_t i = i0 + rr;
 
+    // branch-free loads: neighbour rows first, then every gather unconditionally
+    // (invalid slots read a far point / a zero value from tables in global memory)
     bool valid[M];
-    int32_t idx[M];
+    int32_t jn[M];
     bool bad_index = false;
 #pragma unroll
-    for (int a = 0; a < M; ++a) {
-        const int32_t j = nbr[rl * M + a];
-        const bool v = j >= 0 && (int64_t)j < n_points;
-        bad_index |= j >= 0 && !v;
-        valid[a] = v;
-        idx[a] = v ? j : 0;
-    }
+    for (int a = 0; a < M; ++a) jn[a] = nbr[rl * M + a];
     double px[N1], py[N1], z[N1];
 #pragma unroll
     for (int a = 0; a < M; ++a) {
-        const double2 x = coords[idx[a]];
-        px[a] = valid[a] ? x.x : kFar * (a + 1);
-        py[a] = valid[a] ? x.y : 0.0;
-        z[a] = (values != nullptr && valid[a]) ? values[idx[a]] : 0.0;
+        const int32_t j = jn[a];
+        const bool v = j >= 0 && (int64_t)j < n_points;
+        bad_index |= j >= 0 && !v;
+        valid[a] = v;
+        const double2 x = *(v ? coords + j : kFarPoints + a);
+        px[a] = x.x;
+        py[a] = x.y;
+        z[a] = *((values != nullptr && v) ? values + j : kZeroValue);
     }
     {
         const double2 x = coords[i];
         px[M] = x.x;
         py[M] = x.y;
-        z[M] = values != nullptr ? values[i] : 0.0;
+        z[M] = *(values != nullptr ? values + i : kZeroValue);
     }
 
     // joint block, lower triangle (A[a][b], b <= a)

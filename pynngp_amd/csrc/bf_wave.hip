@@ -31,16 +31,16 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
         const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
         const int64_t i = i0 + rr;
         // lane a < M: neighbour slot a; lane M: the location itself; lanes > M: far-away identity rows
-        int32_t j = -1;
-        if (lane < M) j = nbr[rl * M + lane];
+        const int32_t jr = M > 0 ? nbr[rl * M + (lane < M ? lane : 0)] : -1;  // nbr may be null for m = 0
+        const int32_t j = (lane < M) ? jr : -1;
         const bool is_self = lane == M;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
         const bool bad_index = j >= 0 && !in_range;
-        const bool valid = is_self || in_range;
-        const int64_t src = is_self ? i : (in_range ? (int64_t)j : 0);
-        const double2 xg = coords[src];
-        const double xx = valid ? xg.x : kFar * (lane + 1), xy = valid ? xg.y : 0.0;
-        double zv = (values != nullptr && valid) ? values[src] : 0.0;
+        const double2* pc = is_self ? coords + i : (in_range ? coords + j : kFarPoints + lane);
+        const double* pv = values == nullptr ? kZeroValue : (is_self ? values + i : (in_range ? values + j : kZeroValue));
+        const double2 xg = *pc;
+        const double xx = xg.x, xy = xg.y;
+        double zv = *pv;
 
         // row `lane` of the joint block (entries b <= lane are meaningful)
         double row[NR];

@@ -138,6 +138,15 @@ class NNGP:
         self._order, self._nbr_sorted = _lib.row_order(self._s_dev, nbr=self.nbr)
         self._Ns = None
 
+    def set_neighbor_sets(self, nbr: torch.Tensor):
+        """Replace the neighbour sets (int32 (N, m) device tensor, -1 padded, prior indices)."""
+        if nbr.shape != self.nbr.shape or nbr.dtype != torch.int32:
+            raise ValueError(f"nbr must be int32 {tuple(self.nbr.shape)}")
+        self.nbr = nbr.to(self.device).contiguous()
+        self._order, self._nbr_sorted = _lib.row_order(self._s_dev, nbr=self.nbr)
+        self._Ns = None
+        self._B = self._F = None
+
     def _make_t_neighbor_sets(self):
         # 'S=T': Nt aliases Ns (nngp.py:65-67)
         pass

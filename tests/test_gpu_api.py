@@ -95,6 +95,8 @@ def test_callable_cov_and_errors(dev):
         NNGP(t, y, None, "S=X", 4, None)
     dup = t.copy()
     model = NNGP(dup, y, None, "S=T", 4, Covariance("exponential", 1.0, 3.0, 0.0))
-    model.nbr[50, 1] = model.nbr[50, 0]
+    nb = model.nbr.clone()
+    nb[50, 1] = nb[50, 0]
+    model.set_neighbor_sets(nb)
     with pytest.raises(NNGPNumericalError, match="location 50"):
         model.loglik()

@@ -65,13 +65,15 @@ CASES = [
 ]
 
 
-GROUP_M = (10, 15, 16, 20)  # instantiated for the 2- and 4-lane kernels
+PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
+QUAD_M = (15, 16, 20)  # and for the 4-lane kernel
+GROUP_M = QUAD_M
 
 
 @pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad"])
 @pytest.mark.parametrize("kind,theta,m", CASES)
 def test_bf_vs_oracle(lib, dev, c_oracle, kind, theta, m, algo):
-    if algo in ("pair", "quad") and m not in GROUP_M:
+    if (algo == "pair" and m not in PAIR_M) or (algo == "quad" and m not in QUAD_M):
         pytest.skip("not instantiated")
     coords, y = _field(6000, m)
     nbr = c_oracle.c_knn_prior(coords, m)
@@ -84,10 +86,18 @@ def test_bf_large_m(lib, dev, c_oracle, m):
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 8.0, 0.05), y, "auto")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, "wave")
-    if m in GROUP_M:
-        for algo in ("pair", "quad"):
+    for algo in ("pair", "quad"):
+        if m in (PAIR_M if algo == "pair" else QUAD_M):
             _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, algo)
             _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 30.0, 0.0), y, algo)
+
+
+@pytest.mark.parametrize("m", list(range(10, 21)))
+def test_bf_pair_all_m(lib, dev, c_oracle, m):
+    coords, y = _field(2500, 200 + m)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.0), y, "pair")
+    _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "pair")
 
 
 def test_bf_m0_and_no_values(lib, dev, c_oracle):
