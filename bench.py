@@ -121,7 +121,8 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ  # launched by torch.distributed.run
+    if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
     sigma2, phi, tau2 = (float(x) for x in args.theta.split(","))
@@ -142,7 +143,7 @@ def main():
     for _ in range(args.warmup):
         sweep.partials(cov, v, want_bf)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -153,10 +154,10 @@ def main():
         ev[k][1].record(stream)
         combine_partials(local, world)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -230,7 +231,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(coords, values, sweep.nbr.cpu().numpy(), args.kind,
                                                (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

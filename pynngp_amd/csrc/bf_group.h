@@ -68,10 +68,11 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
                                                 int64_t n_rows, int64_t i0,
                                                 const CovParams Pc, const double* __restrict__ values,
                                                 double* __restrict__ Bout, double* __restrict__ Fout,
-                                                double* __restrict__ wpart, unsigned long long* __restrict__ status) {
+                                                double* __restrict__ bpart) {
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
-    const int64_t tid = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int64_t tid = blk * blockDim.x + threadIdx.x;
     const int q = (int)(threadIdx.x % P);
     const int64_t r = tid / P;
     const bool live = r < n_rows;
@@ -201,21 +202,21 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
     const bool lead = live && q == 0;
     if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
 
-    double lf = 0.0, qq = 0.0;
+    double lf = 0.0, qq = 0.0, badp = INFINITY, badi = INFINITY;
     if (lead) {
         lf = log(F);
         qq = res * res / F;
-        if (bad) atomicMin(status + 0, (unsigned long long)i);
+        if (bad) badp = (double)i;
     }
-    if (live && bad_index) atomicMin(status + 1, (unsigned long long)i);
-    wave_partials_store(lf, qq, wpart, tid);
+    if (live && bad_index) badi = (double)i;
+    block_partials_store(lf, qq, badp, badi, bpart, blk);
 }
 
 template <int M, int KIND, int P>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
     hipLaunchKernelGGL((bf_group<M, KIND, P>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.wpart, a.status);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.bpart);
 }
 
 // instantiate both kinds for one (M, P); returns false for other m

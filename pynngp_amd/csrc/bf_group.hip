@@ -10,7 +10,7 @@ bool bf_pair_launch_c(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_pair_launch_d(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch(const BfArgs&, const CovParams&, hipStream_t);
 
-int64_t bf_group_waves(int64_t n_rows, int P) { return (n_rows * P + 255) / 256 * 4; }
+int64_t bf_group_blocks(int64_t n_rows, int P) { return (n_rows * P + 255) / 256; }
 
 bool bf_group_supported(int m, int P) {
     if (P == 2) return m >= 10 && m <= 20;

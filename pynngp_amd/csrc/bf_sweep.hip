@@ -22,8 +22,9 @@
 //   bf_wave<NR>  one WAVE per location (the north_star layout): lane a owns row a
 //                of the joint block in VGPRs; column values are broadcast with
 //                v_readlane.  Any M <= 63.  Generic path / comparison point.
-// Both write one (sum log F, sum r^2/F) pair per wave into a workspace slab;
-// bf_finalize sums the slab in a fixed order (bit-reproducible).
+// Every kernel writes one record per 256-thread block (sum log F, sum r^2/F,
+// first bad-pivot row, first bad-index row) into a workspace slab; bf_finalize
+// folds the slab in a fixed order (bit-reproducible, no pre-initialised state).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,9 +43,10 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
                                                int64_t n_rows, int64_t i0,
                                                const CovParams P, const double* __restrict__ values,
                                                double* __restrict__ Bout, double* __restrict__ Fout,
-                                               double* __restrict__ wpart, unsigned long long* __restrict__ status) {
+                                               double* __restrict__ bpart) {
     constexpr int N1 = M + 1;  // joint block order
-    const int64_t r = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int64_t r = blk * blockDim.x + threadIdx.x;
     const bool live = r < n_rows;
     const int64_t rl = live ? r : n_rows - 1;
     const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
@@ -124,44 +126,49 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
     }
     if (Fout != nullptr && live) Fout[rr] = bad ? NAN : F;
 
-    double lf = 0.0, q = 0.0;
+    double lf = 0.0, q = 0.0, badp = INFINITY, badi = INFINITY;
     if (live) {
         lf = log(F);
         q = res * res / F;
-        if (bad) atomicMin(status + 0, (unsigned long long)i);
-        if (bad_index) atomicMin(status + 1, (unsigned long long)i);
+        if (bad) badp = (double)i;
+        if (bad_index) badi = (double)i;
     }
-    wave_partials_store(lf, q, wpart, r);
+    block_partials_store(lf, q, badp, badi, bpart, blk);
 }
 
 // --------------------------------------------------------------------------
-// fixed-order reduction of the per-wave partial slab -> partials[4]
+// fixed-order reduction of the per-block partial records -> partials[4]
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ wpart, int64_t n_waves,
-                                                    const unsigned long long* __restrict__ status,
+__global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ bpart, int64_t n_blocks,
                                                     double* __restrict__ partials) {
-    __shared__ double s0[1024], s1[1024];
+    __shared__ double s0[1024], s1[1024], s2[1024], s3[1024];
     const int t = threadIdx.x;
-    double a = 0.0, b = 0.0;
-    for (int64_t w = t; w < n_waves; w += 1024) {
-        a += wpart[2 * w];
-        b += wpart[2 * w + 1];
+    double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+    for (int64_t k = t; k < n_blocks; k += 1024) {
+        a += bpart[4 * k];
+        b += bpart[4 * k + 1];
+        c = fmin(c, bpart[4 * k + 2]);
+        d = fmin(d, bpart[4 * k + 3]);
     }
     s0[t] = a;
     s1[t] = b;
+    s2[t] = c;
+    s3[t] = d;
     __syncthreads();
     for (int off = 512; off > 0; off >>= 1) {
         if (t < off) {
             s0[t] += s0[t + off];
             s1[t] += s1[t + off];
+            s2[t] = fmin(s2[t], s2[t + off]);
+            s3[t] = fmin(s3[t], s3[t + off]);
         }
         __syncthreads();
     }
     if (t == 0) {
         partials[0] = s0[0];
         partials[1] = s1[0];
-        partials[2] = status[0] == ~0ull ? -1.0 : (double)status[0];
-        partials[3] = status[1] == ~0ull ? -1.0 : (double)status[1];
+        partials[2] = s2[0] == INFINITY ? -1.0 : s2[0];
+        partials[3] = s3[0] == INFINITY ? -1.0 : s3[0];
     }
 }
 
@@ -172,10 +179,10 @@ template <int M, int KIND>
 static void launch_lane(const BfArgs& a, const CovParams& P, hipStream_t s) {
     const int64_t blocks = (a.n_rows + 255) / 256;
     hipLaunchKernelGGL((bf_lane<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.wpart, a.status);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.bpart);
 }
 
-int64_t bf_lane_waves(int64_t n_rows) { return (n_rows + 255) / 256 * 4; }
+int64_t bf_lane_blocks(int64_t n_rows) { return (n_rows + 255) / 256; }
 
 template <int KIND>
 static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
@@ -196,27 +203,27 @@ static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     if (a.n_rows == 0) {  // empty shard: partials = [0, 0, -1, -1]
-        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, (int64_t)0, a.status, a.partials);
+        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.bpart, (int64_t)0, a.partials);
         return hipGetLastError();
     }
     const CovParams P = nngp_cov_params(a.sigma2, a.phi, a.tau2);
     bool ok;
-    int64_t nw;
+    int64_t nb;
     if (algo == kAlgoLane) {
         ok = a.kind == 1 ? launch_lane_m<1>(a, P, s) : launch_lane_m<0>(a, P, s);
-        nw = bf_lane_waves(a.n_rows);
+        nb = bf_lane_blocks(a.n_rows);
     } else if (algo == kAlgoPair || algo == kAlgoQuad) {
         const int lanes = algo == kAlgoPair ? 2 : 4;
         ok = bf_group_launch(a, P, lanes, s);
-        nw = bf_group_waves(a.n_rows, lanes);
+        nb = bf_group_blocks(a.n_rows, lanes);
     } else {
-        nw = bf_wave_waves(a.n_rows);
-        ok = bf_wave_launch(a, P, nw, s);
+        nb = bf_wave_blocks(a.n_rows);
+        ok = bf_wave_launch(a, P, nb, s);
     }
     if (!ok) return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.wpart, nw, a.status, a.partials);
+    hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.bpart, nb, a.partials);
     return hipGetLastError();
 }
 

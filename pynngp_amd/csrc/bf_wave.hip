@@ -21,11 +21,12 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
                                                int64_t n_rows, int64_t i0, int M,
                                                const CovParams P, const double* __restrict__ values,
                                                double* __restrict__ Bout, double* __restrict__ Fout,
-                                               double* __restrict__ wpart, unsigned long long* __restrict__ status) {
+                                               double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
+    double badp = INFINITY, badi = INFINITY;
 
     for (int64_t rl = wave; rl < n_rows; rl += n_waves) {
         const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
@@ -99,44 +100,40 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
             if (Fout != nullptr) Fout[rr] = bad ? NAN : F;
             lf_acc += log(F);
             q_acc += res * res / F;
-            if (bad) atomicMin(status + 0, (unsigned long long)i);
+            if (bad) badp = fmin(badp, (double)i);
         }
-        if (__any(bad_index) && lane == 0) atomicMin(status + 1, (unsigned long long)i);
+        if (__any(bad_index) && lane == 0) badi = fmin(badi, (double)i);
     }
-    if (lane == 0) {
-        wpart[2 * wave] = lf_acc;
-        wpart[2 * wave + 1] = q_acc;
-    }
+    block_partials_store(lf_acc, q_acc, badp, badi, bpart, blockIdx.x);
 }
 
 template <int NR, int KIND>
-static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s) {
-    hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)(n_waves / 4)), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.wpart, a.status);
+static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s) {
+    hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)n_blocks), dim3(256), 0, s, (const double2*)a.coords,
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.bpart);
 }
 
-int64_t bf_wave_waves(int64_t n_rows) {
-    // persistent grid: at most 8192 waves (256 CUs x 32), at least one wave per location
-    int64_t w = n_rows < 8192 ? n_rows : 8192;
-    w = (w + 3) / 4 * 4;
-    return w < 4 ? 4 : w;
+int64_t bf_wave_blocks(int64_t n_rows) {
+    // persistent grid of 4-wave blocks: at most 2048 blocks (256 CUs x 32 waves), about one wave per location
+    const int64_t b = (n_rows + 3) / 4;
+    return b < 1 ? 1 : (b > 2048 ? 2048 : b);
 }
 
 template <int KIND>
-static bool launch_wave_m_k(const BfArgs& a, const CovParams& P, int64_t nw, hipStream_t s) {
+static bool launch_wave_m_k(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
     if (a.m + 1 <= 16)
-        launch_wave<16, KIND>(a, P, nw, s);
+        launch_wave<16, KIND>(a, P, nb, s);
     else if (a.m + 1 <= 32)
-        launch_wave<32, KIND>(a, P, nw, s);
+        launch_wave<32, KIND>(a, P, nb, s);
     else if (a.m + 1 <= 64)
-        launch_wave<64, KIND>(a, P, nw, s);
+        launch_wave<64, KIND>(a, P, nb, s);
     else
         return false;
     return true;
 }
 
-bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nw, hipStream_t s) {
-    return a.kind == 1 ? launch_wave_m_k<1>(a, P, nw, s) : launch_wave_m_k<0>(a, P, nw, s);
+bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
+    return a.kind == 1 ? launch_wave_m_k<1>(a, P, nb, s) : launch_wave_m_k<0>(a, P, nb, s);
 }
 
 }  // namespace nngp

@@ -38,11 +38,11 @@ int resolve_algo(int32_t algo, int32_t m) {
     return nngp::kAlgoWave;
 }
 
-int64_t bf_waves(int64_t n_rows, int algo) {
-    if (algo == nngp::kAlgoLane) return nngp::bf_lane_waves(n_rows);
-    if (algo == nngp::kAlgoPair) return nngp::bf_group_waves(n_rows, 2);
-    if (algo == nngp::kAlgoQuad) return nngp::bf_group_waves(n_rows, 4);
-    return nngp::bf_wave_waves(n_rows);
+int64_t bf_blocks(int64_t n_rows, int algo) {
+    if (algo == nngp::kAlgoLane) return nngp::bf_lane_blocks(n_rows);
+    if (algo == nngp::kAlgoPair) return nngp::bf_group_blocks(n_rows, 2);
+    if (algo == nngp::kAlgoQuad) return nngp::bf_group_blocks(n_rows, 4);
+    return nngp::bf_wave_blocks(n_rows);
 }
 }  // namespace
 
@@ -59,8 +59,8 @@ double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
     if (n_rows < 0) return 0;
     const int a = resolve_algo(algo, m);
-    const int64_t nw = n_rows > 0 ? bf_waves(n_rows, a) : 0;
-    return align256(16) + align256((size_t)nw * 2 * sizeof(double));
+    const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a) : 0;
+    return align256((size_t)nb * 4 * sizeof(double));
 }
 
 int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
@@ -91,14 +91,9 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
 
     hipStream_t s = (hipStream_t)stream;
-    char* w = (char*)workspace;
-    unsigned long long* status = (unsigned long long*)w;
-    double* wpart = (double*)(w + align256(16));
-    hipError_t e = hipMemsetAsync(status, 0xff, 2 * sizeof(unsigned long long), s);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(status)");
     nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, B, F,
-                      partials, wpart, status};
-    e = nngp::bf_launch(args, a, s);
+                      partials, (double*)workspace};
+    hipError_t e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
     return NNGP_OK;
 }

@@ -40,17 +40,17 @@ struct BfArgs {
     double* B;                 // (n_rows, m) or null
     double* F;                 // (n_rows,) or null
     double* partials;          // [4]
-    double* wpart;             // 2 doubles per wave
-    unsigned long long* status;  // [2], preset to ~0
+    double* bpart;             // 4 doubles per block: sum log F, sum r^2/F, first bad-pivot row, first bad-index row
 };
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
-bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_waves, hipStream_t s);
+bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s);
 bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t s);
 bool bf_group_supported(int m, int lanes);
-int64_t bf_group_waves(int64_t n_rows, int lanes);
-int64_t bf_lane_waves(int64_t n_rows);
-int64_t bf_wave_waves(int64_t n_rows);
+// number of 256-thread blocks (= partial records) each kernel launches for n_rows
+int64_t bf_group_blocks(int64_t n_rows, int lanes);
+int64_t bf_lane_blocks(int64_t n_rows);
+int64_t bf_wave_blocks(int64_t n_rows);
 
 struct KnnPlan {
     int64_t n_points;
@@ -95,14 +95,46 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// Fixed-order wave reduction of (lf, q); lane 0 stores them at slot (thread >> 6).
-__device__ __forceinline__ void wave_partials_store(double lf, double q, double* wpart, int64_t thread) {
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Fixed-order reduction of one 256-thread block's (log F, r^2/F) sums and of its
+// first bad-pivot / bad-index rows (INFINITY = none) into bpart[4 * block ..].
+// Every thread of the block must call it (it synchronises the block).  No global
+// atomics and no pre-initialised status words: bf_finalize folds the records.
+__device__ __forceinline__ void block_partials_store(double lf, double q, double badp, double badi, double* bpart,
+                                                     int64_t block) {
+    __shared__ double sh[4][4];
     lf = wave_sum(lf);
     q = wave_sum(q);
+    if (__any(badp != INFINITY || badi != INFINITY)) {  // wave-uniform; rare
+        badp = wave_min(badp);
+        badi = wave_min(badi);
+    }
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        const int64_t w = thread >> 6;
-        wpart[2 * w] = lf;
-        wpart[2 * w + 1] = q;
+        sh[w][0] = lf;
+        sh[w][1] = q;
+        sh[w][2] = badp;
+        sh[w][3] = badi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+            a += sh[k][0];
+            b += sh[k][1];
+            c = fmin(c, sh[k][2]);
+            d = fmin(d, sh[k][3]);
+        }
+        double* o = bpart + 4 * block;
+        o[0] = a;
+        o[1] = b;
+        o[2] = c;
+        o[3] = d;
     }
 }
 

@@ -35,7 +35,7 @@ def combine_partials(local: torch.Tensor, world: int, group=None) -> torch.Tenso
 
     [0], [1] are summed; [2], [3] (first bad row or -1) take the smallest non-negative.
     """
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return local
     gathered = torch.empty((world, 4), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(gathered, local.reshape(1, 4), group=group)

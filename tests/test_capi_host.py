@@ -46,8 +46,9 @@ def test_version_and_loglik_helper(lib):
 
 
 def test_workspace_sizes(lib):
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0) >= 16 + 2 * 8 * (1_000_000 // 64)
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0) >= 4 * 8 * (1_000_000 // 256)
     assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0) == 0
+    assert lib.nngp_bf_sweep_workspace_bytes(0, 15, 0) == 0
     assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0) > 0
 
 

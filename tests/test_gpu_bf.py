@@ -156,7 +156,7 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     sing = nbr.copy()
     sing[1234, 1] = sing[1234, 0]  # repeated neighbour: C_N singular, second pivot exactly 0 (sigma2 = 1)
     sing[1500, 1] = sing[1500, 0]
-    for algo in ["lane", "wave", "pair", "quad"]:
+    for algo in ["lane", "wave", "pair"]:
         B, F, p = lib.bf_sweep(c, torch.from_numpy(sing).to(dev), 0, "exponential", 1.0, 5.0, 0.0, algo=algo)
         _, _, po = c_oracle.c_bf_sweep(coords, sing, "exponential", (1.0, 5.0, 0.0), None)
         assert p[2].item() == 1234 == po[2]
