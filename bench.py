@@ -98,6 +98,11 @@ def cpu_baseline(coords, values, nbr_host, kind, theta, budget_s, F_gpu):
 
 
 def main():
+    # The result must be the only line on stdout: libraries (RCCL prints a version
+    # banner at communicator creation) write to fd 1 too, so point fd 1 at stderr
+    # for the whole run and keep a private handle for the JSON line.
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -230,7 +235,8 @@ def main():
                 F_gpu = F_t.cpu().numpy()
             out["cpu_baseline"] = cpu_baseline(coords, values, sweep.nbr.cpu().numpy(), args.kind,
                                                (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if distributed:
         dist.destroy_process_group()
 

@@ -122,6 +122,15 @@ size_t nngp_row_order_workspace_bytes(int64_t n_rows);
 int nngp_row_order(const double *coords, int64_t n_points, const int32_t *nbr, int32_t m, int64_t i0, int64_t n_rows,
                    int32_t *order, int32_t *nbr_sorted, void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Multi-GPU: fold the all-gathered partials of `world` ranks (device array
+ * (world, 4), rank-major, e.g. from an RCCL all-gather) in rank order:
+ * partials[0..1] = sums, partials[2..3] = smallest non-negative flag or -1.
+ * Every rank gets the bit-identical result.  No reference counterpart (the
+ * reference is single-process).
+ * ------------------------------------------------------------------------- */
+int nngp_combine_partials(const double *gathered, int32_t world, double *partials, void *stream);
+
 /* Host helper: -1/2 (n_rows log 2 pi + p[0] + p[1]) from host-resident partials. */
 double nngp_loglik_from_partials(const double *partials_host, int64_t n_rows);
 

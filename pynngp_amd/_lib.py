@@ -26,6 +26,7 @@ SYMBOLS = (
     "nngp_loglik_from_partials",
     "nngp_row_order_workspace_bytes",
     "nngp_row_order",
+    "nngp_combine_partials",
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1}
@@ -67,6 +68,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_row_order_workspace_bytes.restype = SZ
     lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
+    lib.nngp_combine_partials.argtypes = [P, I32, P, P]
+    lib.nngp_combine_partials.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_loglik_from_partials.argtypes = [P, I64]
     lib.nngp_loglik_from_partials.restype = D
@@ -233,6 +236,18 @@ def row_order(coords: torch.Tensor, i0: int = 0, rows: Optional[int] = None,
     _check(lib.nngp_row_order(_ptr(coords), n, _ptr(nbr), m, i0, rows, _ptr(out), _ptr(srt), _ptr(ws), ws.numel(),
                               _stream(dev)), "nngp_row_order")
     return out, srt
+
+
+def combine_partials(gathered: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rank-order fold of all-gathered (world, 4) partials into (4,) (one tiny kernel)."""
+    if gathered.dtype != torch.float64 or gathered.dim() != 2 or gathered.shape[1] != 4:
+        raise ValueError("gathered must be float64 (world, 4)")
+    gathered = gathered.contiguous()
+    dev = _require_gpu(gathered, out)
+    out = torch.empty(4, dtype=torch.float64, device=dev) if out is None else out
+    _check(load().nngp_combine_partials(_ptr(gathered), gathered.shape[0], _ptr(out), _stream(dev)),
+           "nngp_combine_partials")
+    return out
 
 
 def bf_workspace(rows: int, m: int, algo: str, device) -> torch.Tensor:

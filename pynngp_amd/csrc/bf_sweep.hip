@@ -143,12 +143,24 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
                                                     double* __restrict__ partials) {
     __shared__ double s0[1024], s1[1024], s2[1024], s3[1024];
     const int t = threadIdx.x;
+    // thread t folds the contiguous chunk [t*C, t*C + C) in order (independent 32-B loads)
+    const int64_t C = (n_blocks + 1023) / 1024;
+    const double4* rec = (const double4*)bpart;
     double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
-    for (int64_t k = t; k < n_blocks; k += 1024) {
-        a += bpart[4 * k];
-        b += bpart[4 * k + 1];
-        c = fmin(c, bpart[4 * k + 2]);
-        d = fmin(d, bpart[4 * k + 3]);
+    for (int64_t k0 = (int64_t)t * C; k0 < (int64_t)(t + 1) * C; k0 += 4) {
+        double4 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = k0 + u;
+            r[u] = (k < (int64_t)(t + 1) * C && k < n_blocks) ? rec[k] : make_double4(0.0, 0.0, INFINITY, INFINITY);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a += r[u].x;
+            b += r[u].y;
+            c = fmin(c, r[u].z);
+            d = fmin(d, r[u].w);
+        }
     }
     s0[t] = a;
     s1[t] = b;
@@ -170,6 +182,29 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
         partials[2] = s2[0] == INFINITY ? -1.0 : s2[0];
         partials[3] = s3[0] == INFINITY ? -1.0 : s3[0];
     }
+}
+
+// Rank-order combination of all-gathered (world, 4) partials: sums for [0], [1],
+// smallest non-negative (else -1) for the bad-row flags [2], [3].
+__global__ __launch_bounds__(64) void combine_partials_kernel(const double* __restrict__ g, int world,
+                                                              double* __restrict__ out) {
+    if (threadIdx.x != 0) return;
+    double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+    for (int r = 0; r < world; ++r) {
+        a += g[4 * r];
+        b += g[4 * r + 1];
+        if (g[4 * r + 2] >= 0.0) c = fmin(c, g[4 * r + 2]);
+        if (g[4 * r + 3] >= 0.0) d = fmin(d, g[4 * r + 3]);
+    }
+    out[0] = a;
+    out[1] = b;
+    out[2] = c == INFINITY ? -1.0 : c;
+    out[3] = d == INFINITY ? -1.0 : d;
+}
+
+hipError_t combine_partials_launch(const double* gathered, int world, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(combine_partials_kernel, dim3(1), dim3(64), 0, s, gathered, world, out);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------

@@ -98,6 +98,14 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
     return NNGP_OK;
 }
 
+int nngp_combine_partials(const double* gathered, int32_t world, double* partials, void* stream) {
+    if (gathered == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "gathered and partials must be non-null");
+    if (world < 1) return fail(NNGP_EINVAL, "world=%d < 1", world);
+    hipError_t e = nngp::combine_partials_launch(gathered, world, partials, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "combine_partials launch");
+    return NNGP_OK;
+}
+
 size_t nngp_row_order_workspace_bytes(int64_t n_rows) { return nngp::row_order_workspace_bytes(n_rows); }
 
 int nngp_row_order(const double* coords, int64_t n_points, const int32_t* nbr, int32_t m, int64_t i0, int64_t n_rows,

@@ -44,6 +44,7 @@ struct BfArgs {
 };
 
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
+hipError_t combine_partials_launch(const double* gathered, int world, double* out, hipStream_t s);
 bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s);
 bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t s);
 bool bf_group_supported(int m, int lanes);

@@ -231,3 +231,12 @@ def test_bf_row_order_bit_identical(lib, dev, c_oracle, algo):
     order = lib.row_order(c)[0].cpu().numpy()
     step = np.linalg.norm(np.diff(coords[order], axis=0), axis=1)
     assert np.median(step) < 0.01
+
+
+def test_combine_partials_rank_order(lib, dev):
+    g = torch.tensor([[1.5, 2.0, -1.0, 7.0], [0.25, 3.0, 5.0, -1.0], [1e-17, 1.0, 9.0, 2.0]],
+                     dtype=torch.float64, device=dev)
+    out = lib.combine_partials(g).cpu().tolist()
+    assert out == [(1.5 + 0.25) + 1e-17, (2.0 + 3.0) + 1.0, 5.0, 2.0]
+    out = lib.combine_partials(g[:1, :]).cpu().tolist()
+    assert out == [1.5, 2.0, -1.0, 7.0]
