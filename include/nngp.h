@@ -97,14 +97,16 @@ int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_
  * coords: (n_points, 2); nbr: (n_rows, m); order: NULL (row t of nbr is location
  * i0 + t) or the nngp_row_order layout (row t of nbr is location i0 + order[t],
  * i.e. pass nbr_sorted); values: (n_points,) or NULL;
- * B, F: may be NULL (log-lik only); partials: 4 doubles.
+ * B, F: may be NULL (log-lik only); R: NULL or (n_rows,) residuals
+ * r_i = v_i - B_i v_N(i) (needs values; the Gibbs w-update keeps them current);
+ * partials: 4 doubles.
  * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, algo) bytes, 256-B aligned.
  * ------------------------------------------------------------------------- */
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo);
 int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, const int32_t *order, int64_t n_rows,
                   int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2, const double *values,
-                  double *B, double *F, double *partials, void *workspace, size_t workspace_bytes, int32_t algo,
-                  void *stream);
+                  double *B, double *F, double *R, double *partials, void *workspace, size_t workspace_bytes,
+                  int32_t algo, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Visiting order for nngp_bf_sweep (a speed option; no reference counterpart:
@@ -130,6 +132,42 @@ int nngp_row_order(const double *coords, int64_t n_points, const int32_t *nbr, i
  * reference is single-process).
  * ------------------------------------------------------------------------- */
 int nngp_combine_partials(const double *gathered, int32_t world, double *partials, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Gibbs sampler for the response model y = X beta + w + eps (SURVEY.md 8(f)
+ * row 1).  Replaces NNGP.oneSample, nngp.py:98-101, whose update_wt / update_ws /
+ * update_y_unobserved do not exist in the reference; model of Datta et al. 2016
+ * as named by the reference docstrings.  Whole-field (single-GPU) arrays.
+ *
+ * nngp_reverse_neighbors: CSR transpose of nbr (n, m): for location i the
+ *   entries e in [off[i], off[i+1]) list the rows j = rev_j[e] whose neighbour
+ *   slot rev_k[e] is i, ascending j.  off: n+1, rev_j / rev_k: n*m ints (device).
+ * nngp_color_moral_graph (HOST pointers, host computation): greedy colouring
+ *   of the moral graph (i ~ N(i); co-parents of a child ~ each other) in index
+ *   order; returns the number of colours (or a negative NNGP_E* code).
+ * nngp_gibbs_w_sweep: one sweep of w_i | rest over the colours in order;
+ *   `members` (device) lists the locations grouped by colour, color_off_host
+ *   (host, n_colors + 1) delimits them.  B (n, m) and Ft (n,) are the factors of
+ *   the unit-variance field (sigma2 = 1, tau2 = 0) from nngp_bf_sweep; r (n,) the
+ *   residuals w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
+ *   yres = y - X beta.  z: NULL (Philox4x32-10 normals keyed by seed, counter
+ *   (location, sweep)) or n given standard normals (for testing).
+ * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum (yres_i - w_i)^2,
+ *   out[2 + c] = sum_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p)).
+ * ------------------------------------------------------------------------- */
+size_t nngp_reverse_workspace_bytes(int64_t n, int32_t m);
+int nngp_reverse_neighbors(const int32_t *nbr, int64_t n, int32_t m, int32_t *off, int32_t *rev_j, int32_t *rev_k,
+                           void *workspace, size_t workspace_bytes, void *stream);
+int64_t nngp_color_moral_graph(const int32_t *nbr_host, const int32_t *off_host, const int32_t *rev_j_host,
+                               int64_t n, int32_t m, int32_t *color_host);
+int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, int32_t n_colors, const double *B,
+                       const double *Ft, double sigma2, double tau2, const double *yres, double *w, double *r,
+                       const int32_t *off, const int32_t *rev_j, const int32_t *rev_k, int32_t m, const double *z,
+                       uint64_t seed, uint64_t sweep, void *stream);
+size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
+int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
+                     const double *X, int32_t p, const double *w, double *out, void *workspace,
+                     size_t workspace_bytes, void *stream);
 
 /* Host helper: -1/2 (n_rows log 2 pi + p[0] + p[1]) from host-resident partials. */
 double nngp_loglik_from_partials(const double *partials_host, int64_t n_rows);

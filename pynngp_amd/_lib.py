@@ -27,6 +27,12 @@ SYMBOLS = (
     "nngp_row_order_workspace_bytes",
     "nngp_row_order",
     "nngp_combine_partials",
+    "nngp_reverse_workspace_bytes",
+    "nngp_reverse_neighbors",
+    "nngp_color_moral_graph",
+    "nngp_gibbs_w_sweep",
+    "nngp_gibbs_stats_workspace_bytes",
+    "nngp_gibbs_stats",
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1}
@@ -63,13 +69,26 @@ def load() -> ctypes.CDLL:
     lib.nngp_knn_query.restype = ctypes.c_int
     lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
     lib.nngp_bf_sweep_workspace_bytes.restype = SZ
-    lib.nngp_bf_sweep.argtypes = [P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_sweep.argtypes = [P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, I32, P]
     lib.nngp_row_order_workspace_bytes.argtypes = [I64]
     lib.nngp_row_order_workspace_bytes.restype = SZ
     lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
     lib.nngp_combine_partials.restype = ctypes.c_int
+    U64 = ctypes.c_uint64
+    lib.nngp_reverse_workspace_bytes.argtypes = [I64, I32]
+    lib.nngp_reverse_workspace_bytes.restype = SZ
+    lib.nngp_reverse_neighbors.argtypes = [P, I64, I32, P, P, P, P, SZ, P]
+    lib.nngp_reverse_neighbors.restype = ctypes.c_int
+    lib.nngp_color_moral_graph.argtypes = [P, P, P, I64, I32, P]
+    lib.nngp_color_moral_graph.restype = I64
+    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, P, D, D, P, P, P, P, P, P, I32, P, U64, U64, P]
+    lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
+    lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]
+    lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
+    lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, SZ, P]
+    lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_loglik_from_partials.argtypes = [P, I64]
     lib.nngp_loglik_from_partials.restype = D
@@ -167,7 +186,8 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
              tau2: float = 0.0, values: Optional[torch.Tensor] = None, want_bf: bool = True,
              algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
              partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
-             order: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+             order: Optional[torch.Tensor] = None,
+             R: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
 
     Returns ``(B, F, partials)`` (B, F None when ``want_bf`` is False); partials is a
@@ -202,8 +222,10 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
+    if R is not None and (R.dtype != torch.float64 or R.shape != (rows,)):
+        raise ValueError("R must be float64 (rows,)")
     _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
-                             float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F),
+                             float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
     return B, F, partials
@@ -253,3 +275,73 @@ def combine_partials(gathered: torch.Tensor, out: Optional[torch.Tensor] = None)
 def bf_workspace(rows: int, m: int, algo: str, device) -> torch.Tensor:
     """Pre-allocate a sweep workspace (reuse it across calls in a hot loop)."""
     return _workspace(load().nngp_bf_sweep_workspace_bytes(rows, m, ALGO_CODES[algo]), torch.device(device))
+
+
+# ---------------------------------------------------------------------------- Gibbs sampler pieces
+def reverse_neighbors(nbr: torch.Tensor):
+    """CSR transpose of the neighbour sets: (off (n+1,), rev_j (n*m,), rev_k (n*m,)) int32 on the device."""
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError("nbr must be int32 (n, m)")
+    nbr = nbr.contiguous()
+    dev = _require_gpu(nbr)
+    n, m = nbr.shape
+    off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    rev_j = torch.empty(max(n * m, 1), dtype=torch.int32, device=dev)
+    rev_k = torch.empty(max(n * m, 1), dtype=torch.int32, device=dev)
+    lib = load()
+    need = lib.nngp_reverse_workspace_bytes(n, m)
+    if need == 0:
+        raise NNGPExtensionError("nngp_reverse_workspace_bytes failed")
+    ws = _workspace(need, dev)
+    _check(lib.nngp_reverse_neighbors(_ptr(nbr), n, m, _ptr(off), _ptr(rev_j), _ptr(rev_k), _ptr(ws), ws.numel(),
+                                      _stream(dev)), "nngp_reverse_neighbors")
+    return off, rev_j, rev_k
+
+
+def color_moral_graph(nbr_host, off_host, rev_j_host):
+    """Greedy moral-graph colouring on the host (numpy int32 inputs); returns (colors, n_colors)."""
+    import numpy as np
+
+    nbr_host = np.ascontiguousarray(nbr_host, dtype=np.int32)
+    off_host = np.ascontiguousarray(off_host, dtype=np.int32)
+    rev_j_host = np.ascontiguousarray(rev_j_host, dtype=np.int32)
+    n, m = nbr_host.shape
+    colors = np.empty(n, dtype=np.int32)
+    nc = load().nngp_color_moral_graph(nbr_host.ctypes.data, off_host.ctypes.data, rev_j_host.ctypes.data, n, m,
+                                       colors.ctypes.data)
+    if nc < 0:
+        _check(int(nc), "nngp_color_moral_graph")
+    return colors, int(nc)
+
+
+def gibbs_w_sweep(members: torch.Tensor, color_off_host, B: torch.Tensor, Ft: torch.Tensor, sigma2: float,
+                  tau2: float, yres: torch.Tensor, w: torch.Tensor, r: torch.Tensor, off: torch.Tensor,
+                  rev_j: torch.Tensor, rev_k: torch.Tensor, seed: int, sweep: int,
+                  z: Optional[torch.Tensor] = None) -> None:
+    """One colour-ordered sweep of w_i | rest, in place on w and r (see include/nngp.h)."""
+    import numpy as np
+
+    dev = _require_gpu(members, B, Ft, yres, w, r, off, rev_j, rev_k, z)
+    co = np.ascontiguousarray(color_off_host, dtype=np.int32)
+    m = B.shape[1]
+    _check(load().nngp_gibbs_w_sweep(_ptr(members), co.ctypes.data, len(co) - 1, _ptr(B), _ptr(Ft), float(sigma2),
+                                     float(tau2), _ptr(yres), _ptr(w), _ptr(r), _ptr(off), _ptr(rev_j), _ptr(rev_k),
+                                     m, _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
+           "nngp_gibbs_w_sweep")
+
+
+def gibbs_stats(r: torch.Tensor, Ft: torch.Tensor, yres: torch.Tensor, y: torch.Tensor, X: Optional[torch.Tensor],
+                w: torch.Tensor, out: Optional[torch.Tensor] = None,
+                workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[sum r^2/Ft, sum (yres - w)^2, X^T (y - w)...] as a float64 device tensor (2 + p,)."""
+    dev = _require_gpu(r, Ft, yres, y, X, w)
+    n = r.shape[0]
+    p = 0 if X is None else X.shape[1]
+    lib = load()
+    out = torch.empty(2 + p, dtype=torch.float64, device=dev) if out is None else out
+    need = lib.nngp_gibbs_stats_workspace_bytes(n, p)
+    if workspace is None or workspace.numel() < need:
+        workspace = _workspace(need, dev)
+    _check(lib.nngp_gibbs_stats(n, _ptr(r), _ptr(Ft), _ptr(yres), _ptr(y), _ptr(X), p, _ptr(w), _ptr(out),
+                                _ptr(workspace), workspace.numel(), _stream(dev)), "nngp_gibbs_stats")
+    return out

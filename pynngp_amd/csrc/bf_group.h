@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0,
                                                 const CovParams Pc, const double* __restrict__ values,
-                                                double* __restrict__ Bout, double* __restrict__ Fout,
+                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double* __restrict__ bpart) {
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
@@ -201,6 +201,7 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
     }
     const bool lead = live && q == 0;
     if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
+    if (Rout != nullptr && lead) Rout[rr] = bad ? NAN : res;
 
     double lf = 0.0, qq = 0.0, badp = INFINITY, badi = INFINITY;
     if (lead) {
@@ -216,7 +217,7 @@ template <int M, int KIND, int P>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
     hipLaunchKernelGGL((bf_group<M, KIND, P>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.R, a.bpart);
 }
 
 // instantiate both kinds for one (M, P); returns false for other m

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0,
                                                const CovParams P, const double* __restrict__ values,
-                                               double* __restrict__ Bout, double* __restrict__ Fout,
+                                               double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     constexpr int N1 = M + 1;  // joint block order
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
         }
     }
     if (Fout != nullptr && live) Fout[rr] = bad ? NAN : F;
+    if (Rout != nullptr && live) Rout[rr] = bad ? NAN : res;
 
     double lf = 0.0, q = 0.0, badp = INFINITY, badi = INFINITY;
     if (live) {
@@ -214,7 +215,7 @@ template <int M, int KIND>
 static void launch_lane(const BfArgs& a, const CovParams& P, hipStream_t s) {
     const int64_t blocks = (a.n_rows + 255) / 256;
     hipLaunchKernelGGL((bf_lane<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.R, a.bpart);
 }
 
 int64_t bf_lane_blocks(int64_t n_rows) { return (n_rows + 255) / 256; }

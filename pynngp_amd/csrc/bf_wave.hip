@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0, int M,
                                                const CovParams P, const double* __restrict__ values,
-                                               double* __restrict__ Bout, double* __restrict__ Fout,
+                                               double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -98,6 +98,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
         }
         if (lane == 0) {
             if (Fout != nullptr) Fout[rr] = bad ? NAN : F;
+            if (Rout != nullptr) Rout[rr] = bad ? NAN : res;
             lf_acc += log(F);
             q_acc += res * res / F;
             if (bad) badp = fmin(badp, (double)i);
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
 template <int NR, int KIND>
 static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s) {
     hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)n_blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.R, a.bpart);
 }
 
 int64_t bf_wave_blocks(int64_t n_rows) {

@@ -66,7 +66,7 @@ size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
 int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
                   int32_t m, int64_t i0,
                   int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
-                  double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
+                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
     if (coords == nullptr || partials == nullptr || workspace == nullptr)
         return fail(NNGP_EINVAL, "coords, partials and workspace must be non-null");
     if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
@@ -79,6 +79,7 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
         return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
     if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
     if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
+    if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
     int a = resolve_algo(algo, m);
     if (a < nngp::kAlgoLane || a > nngp::kAlgoQuad) return fail(NNGP_EINVAL, "unknown algo %d", algo);
@@ -91,7 +92,7 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
 
     hipStream_t s = (hipStream_t)stream;
-    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, B, F,
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, B, F, R,
                       partials, (double*)workspace};
     hipError_t e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
@@ -103,6 +104,69 @@ int nngp_combine_partials(const double* gathered, int32_t world, double* partial
     if (world < 1) return fail(NNGP_EINVAL, "world=%d < 1", world);
     hipError_t e = nngp::combine_partials_launch(gathered, world, partials, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "combine_partials launch");
+    return NNGP_OK;
+}
+
+size_t nngp_reverse_workspace_bytes(int64_t n, int32_t m) {
+    if (n < 0 || m < 0 || n * (int64_t)m > INT32_MAX) return 0;
+    return nngp::reverse_workspace_bytes(n, m);
+}
+
+int nngp_reverse_neighbors(const int32_t* nbr, int64_t n, int32_t m, int32_t* off, int32_t* rev_j, int32_t* rev_k,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+    if (off == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "off and workspace must be non-null");
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n=%lld or m=%d", (long long)n, m);
+    if (n * (int64_t)m > INT32_MAX) return fail(NNGP_EUNSUP, "n*m must be < 2^31");
+    if (n * m > 0 && (nbr == nullptr || rev_j == nullptr || rev_k == nullptr))
+        return fail(NNGP_EINVAL, "nbr, rev_j and rev_k must be non-null");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    const size_t need = nngp::reverse_workspace_bytes(n, m);
+    if (need == 0 || workspace_bytes < need)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
+    hipError_t e = nngp::reverse_launch(nbr, n, m, off, rev_j, rev_k, workspace, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "reverse_neighbors launch");
+    return NNGP_OK;
+}
+
+int64_t nngp_color_moral_graph(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int32_t m,
+                               int32_t* color) {
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n or m");
+    if (n > 0 && (off == nullptr || color == nullptr || (m > 0 && (nbr == nullptr || rev_j == nullptr))))
+        return fail(NNGP_EINVAL, "null host pointer");
+    return nngp::color_moral_graph_host(nbr, off, rev_j, n, m, color);
+}
+
+int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, int32_t n_colors, const double* B,
+                       const double* Ft, double sigma2, double tau2, const double* yres, double* w, double* r,
+                       const int32_t* off, const int32_t* rev_j, const int32_t* rev_k, int32_t m, const double* z,
+                       uint64_t seed, uint64_t sweep, void* stream) {
+    if (members == nullptr || color_off_host == nullptr || Ft == nullptr || yres == nullptr || w == nullptr ||
+        r == nullptr || off == nullptr || (m > 0 && (B == nullptr || rev_j == nullptr || rev_k == nullptr)))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (n_colors < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors or m");
+    if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
+        return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
+    hipError_t e = nngp::gibbs_w_sweep_launch(nullptr, members, n_colors, color_off_host, B, Ft, sigma2, tau2, yres,
+                                              w, r, off, rev_j, rev_k, m, z, seed, sweep, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
+    return NNGP_OK;
+}
+
+size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p) {
+    if (n < 1 || p < 0 || p > 62) return 0;
+    return nngp::gibbs_stats_workspace_bytes(n, p);
+}
+
+int nngp_gibbs_stats(int64_t n, const double* r, const double* Ft, const double* yres, const double* y, const double* X,
+                     int32_t p, const double* w, double* out, void* workspace, size_t workspace_bytes, void* stream) {
+    if (r == nullptr || Ft == nullptr || yres == nullptr || w == nullptr || out == nullptr || workspace == nullptr ||
+        (p > 0 && (X == nullptr || y == nullptr)))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (n < 1 || p < 0 || p > 62) return fail(NNGP_EINVAL, "bad n or p");
+    const size_t need = nngp::gibbs_stats_workspace_bytes(n, p);
+    if (workspace_bytes < need) return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
+    hipError_t e = nngp::gibbs_stats_launch(n, r, Ft, yres, y, X, p, w, out, workspace, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_stats launch");
     return NNGP_OK;
 }
 

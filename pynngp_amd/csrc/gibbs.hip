@@ -1,0 +1,285 @@
+// Gibbs-sampler kernels for the NNGP response model.
+//
+// Reference: pyNNGP's NNGP.oneSample (nngp.py:98-101) calls update_wt /
+// update_ws / update_y_unobserved, none of which exist; the model and the
+// updates here are those of the NNGP papers the reference's docstrings name
+// (Datta et al. 2016): y = X beta + w + eps, eps ~ N(0, tau2 I),
+// w ~ NNGP(0, C(sigma2, phi)) with precision Q = (I - B)^T F^{-1} (I - B).
+//
+// Full conditional of w_i (everything else fixed):
+//   prec_i = 1/tau2 + 1/F_i + sum_{j in U(i)} B_{j,i}^2 / F_j
+//   lin_i  = (y_i - x_i beta)/tau2 + (B_i w_N(i))/F_i
+//            + sum_{j in U(i)} B_{j,i} (w_j - sum_{l in N(j), l != i} B_{j,l} w_l) / F_j
+//   w_i ~ N(lin_i / prec_i, 1 / prec_i)
+// with U(i) = {j : i in N(j)} (the reverse neighbour lists).  Keeping the NNGP
+// residuals r_j = w_j - B_j w_N(j) current makes each term O(1):
+//   B_i w_N(i) = w_i - r_i,   w_j - sum_{l != i} B_{j,l} w_l = r_j + B_{j,i} w_i,
+// and after drawing w_i' the residuals of i and of its children move by
+// dw = w_i' - w_i (r_i += dw, r_j -= B_{j,i} dw).
+//
+// Locations of one colour of the moral graph (edges i-N(i) and between
+// co-parents of a common child) never read or write each other's w / r, so a
+// colour is updated in parallel without races; colours run in sequence.  Normal
+// draws come from a counter-based Philox4x32-10 keyed by (seed) with counter
+// (location, sweep), so a chain is reproducible bit for bit.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+
+#include "nngp_internal.h"
+
+namespace nngp {
+
+// ---------------------------------------------------------------- Philox4x32-10
+__host__ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c[0];
+        const uint64_t p1 = (uint64_t)M1 * c[2];
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+        const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = l1;
+        c[2] = n2;
+        c[3] = l0;
+        k0 += W0;
+        k1 += W1;
+    }
+}
+
+// standard normal for (seed, location, sweep): Box-Muller on two 53-bit uniforms in (0, 1)
+__host__ __device__ __forceinline__ double philox_normal(uint64_t seed, uint64_t loc, uint64_t sweep) {
+    uint32_t c[4] = {(uint32_t)loc, (uint32_t)(loc >> 32), (uint32_t)sweep, (uint32_t)(sweep >> 32)};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t a = ((uint64_t)c[0] << 21) ^ (c[1] >> 11);
+    const uint64_t b = ((uint64_t)c[2] << 21) ^ (c[3] >> 11);
+    const double u1 = ((double)(a & ((1ull << 53) - 1)) + 0.5) * 0x1p-53;
+    const double u2 = ((double)(b & ((1ull << 53) - 1)) + 0.5) * 0x1p-53;
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+// ---------------------------------------------------------------- reverse neighbour lists
+__global__ __launch_bounds__(256) void rev_keys(const int32_t* __restrict__ nbr, int64_t n_entries, int64_t n,
+                                                uint32_t* __restrict__ key, int32_t* __restrict__ val) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_entries) return;
+    const int32_t i = nbr[e];
+    key[e] = (i >= 0 && (int64_t)i < n) ? (uint32_t)i : (uint32_t)n;  // invalid slots sort last
+    val[e] = (int32_t)e;
+}
+
+__global__ __launch_bounds__(256) void rev_bounds(const uint32_t* __restrict__ key_sorted, int64_t n_entries,
+                                                  int64_t n, int32_t* __restrict__ off) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    int64_t lo = 0, hi = n_entries;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)key_sorted[mid] < i)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    off[i] = (int32_t)lo;
+}
+
+__global__ __launch_bounds__(256) void rev_split(const int32_t* __restrict__ val_sorted, int64_t n_valid, int m,
+                                                 int32_t* __restrict__ rev_j, int32_t* __restrict__ rev_k) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_valid) return;
+    const int32_t v = val_sorted[e];
+    rev_j[e] = v / m;
+    rev_k[e] = v % m;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t rev_sort_temp(int64_t e) {
+    size_t tb = 0;
+    if (rocprim::radix_sort_pairs((void*)nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)e, 0u, 32u) != hipSuccess)
+        return 0;
+    return tb;
+}
+
+size_t reverse_workspace_bytes(int64_t n, int m) {
+    const int64_t e = n * m;
+    if (e < 1) return 256;
+    const size_t tb = rev_sort_temp(e);
+    if (tb == 0) return 0;
+    return 4 * align256((size_t)e * 4) + align256(tb);
+}
+
+hipError_t reverse_launch(const int32_t* nbr, int64_t n, int m, int32_t* off, int32_t* rev_j, int32_t* rev_k,
+                          void* workspace, hipStream_t s) {
+    const int64_t e = n * m;
+    char* w = (char*)workspace;
+    uint32_t* key = (uint32_t*)w;
+    w += align256((size_t)e * 4);
+    uint32_t* key_sorted = (uint32_t*)w;
+    w += align256((size_t)e * 4);
+    int32_t* val = (int32_t*)w;
+    w += align256((size_t)e * 4);
+    int32_t* val_sorted = (int32_t*)w;
+    w += align256((size_t)e * 4);
+    if (e == 0) {
+        hipLaunchKernelGGL(rev_bounds, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, key_sorted, (int64_t)0,
+                           n, off);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(rev_keys, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, nbr, e, n, key, val);
+    size_t tb = rev_sort_temp(e);
+    hipError_t er = rocprim::radix_sort_pairs((void*)w, tb, key, key_sorted, val, val_sorted, (size_t)e, 0u, 32u, s);
+    if (er != hipSuccess) return er;
+    hipLaunchKernelGGL(rev_bounds, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, s, key_sorted, e, n, off);
+    // entries [0, off[n]) are valid; split all e (the tail past off[n] is never read)
+    hipLaunchKernelGGL(rev_split, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, val_sorted, e, m, rev_j, rev_k);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- moral-graph colouring (host)
+int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
+                               int32_t* color) {
+    std::vector<int64_t> stamp(1024, -1);
+    int32_t n_colors = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        // mark colours of already-coloured moral neighbours: parents N(i), and co-parents k < i of children j
+        auto mark = [&](int32_t k) {
+            if (k >= 0 && k < i) {
+                const int32_t c = color[k];
+                if (c >= (int32_t)stamp.size()) stamp.resize((size_t)c * 2 + 1, -1);
+                stamp[c] = i;
+            }
+        };
+        const int32_t* row = nbr + i * m;
+        for (int s = 0; s < m; ++s) mark(row[s]);
+        for (int32_t e = off[i]; e < off[i + 1]; ++e) {
+            const int64_t j = rev_j[e];
+            const int32_t* rj = nbr + j * m;
+            for (int s = 0; s < m; ++s)
+                if (rj[s] != i) mark(rj[s]);
+        }
+        int32_t c = 0;
+        while (c < (int32_t)stamp.size() && stamp[c] == i) ++c;
+        color[i] = c;
+        if (c + 1 > n_colors) n_colors = c + 1;
+        if (n_colors >= (int32_t)stamp.size()) stamp.resize(stamp.size() * 2, -1);
+    }
+    return n_colors;
+}
+
+// ---------------------------------------------------------------- colour update
+__global__ __launch_bounds__(256) void gibbs_w_color(const int32_t* __restrict__ members, int64_t n_members,
+                                                     const double* __restrict__ B, const double* __restrict__ Ft,
+                                                     double sigma2, double tau2, const double* __restrict__ yres,
+                                                     double* __restrict__ w, double* __restrict__ r,
+                                                     const int32_t* __restrict__ off, const int32_t* __restrict__ rev_j,
+                                                     const int32_t* __restrict__ rev_k, int m,
+                                                     const double* __restrict__ z, uint64_t seed, uint64_t sweep) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_members) return;
+    const int64_t i = members[t];
+    const double wi = w[i], ri = r[i];
+    const double it2 = 1.0 / tau2, is2 = 1.0 / sigma2;
+    const double iFi = is2 / Ft[i];
+    double prec = it2 + iFi;
+    double lin = fma(yres[i], it2, (wi - ri) * iFi);
+    const int32_t e0 = off[i], e1 = off[i + 1];
+    for (int32_t e = e0; e < e1; ++e) {
+        const int64_t j = rev_j[e];
+        const double bji = B[j * m + rev_k[e]];
+        const double iFj = is2 / Ft[j];
+        const double sj = fma(bji, wi, r[j]);
+        prec = fma(bji * bji, iFj, prec);
+        lin = fma(bji * sj, iFj, lin);
+    }
+    const double zi = z != nullptr ? z[i] : philox_normal(seed, (uint64_t)i, sweep);
+    const double sd = nngp_rsqrt(prec);
+    const double wn = fma(zi, sd, lin / prec);
+    const double dw = wn - wi;
+    w[i] = wn;
+    r[i] = ri + dw;
+    for (int32_t e = e0; e < e1; ++e) {
+        const int64_t j = rev_j[e];
+        const double bji = B[j * m + rev_k[e]];
+        r[j] = fma(-bji, dw, r[j]);
+    }
+}
+
+hipError_t gibbs_w_sweep_launch(const int32_t* color_off, const int32_t* members_all, int n_colors,
+                                const int32_t* color_off_host, const double* B, const double* Ft, double sigma2,
+                                double tau2, const double* yres, double* w, double* r, const int32_t* off,
+                                const int32_t* rev_j, const int32_t* rev_k, int m, const double* z, uint64_t seed,
+                                uint64_t sweep, hipStream_t s) {
+    (void)color_off;
+    for (int c = 0; c < n_colors; ++c) {
+        const int64_t a = color_off_host[c], b = color_off_host[c + 1];
+        if (b <= a) continue;
+        hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((b - a + 255) / 256)), dim3(256), 0, s, members_all + a,
+                           b - a, B, Ft, sigma2, tau2, yres, w, r, off, rev_j, rev_k, m, z, seed, sweep);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- small reductions for the conjugate steps
+// out[0] = sum r_i^2 / Ft_i (sigma2 full conditional), out[1] = sum (yres_i - w_i)^2 (tau2),
+// out[2 + c] = sum_i X[i, c] (y_i - w_i) (beta), c < p.  Fixed-order: per-block records + one fold.
+__global__ __launch_bounds__(256) void gibbs_stats_blocks(int64_t n, const double* __restrict__ r,
+                                                          const double* __restrict__ Ft,
+                                                          const double* __restrict__ yres,
+                                                          const double* __restrict__ y, const double* __restrict__ X,
+                                                          int p, const double* __restrict__ w,
+                                                          double* __restrict__ rec) {
+    __shared__ double sh[256];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nv = 2 + p;
+    for (int v = 0; v < nv; ++v) {
+        double x = 0.0;
+        if (i < n) {
+            if (v == 0) {
+                x = r[i] * r[i] / Ft[i];
+            } else if (v == 1) {
+                const double e = yres[i] - w[i];
+                x = e * e;
+            } else {
+                x = X[i * p + (v - 2)] * (y[i] - w[i]);
+            }
+        }
+        sh[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) rec[blockIdx.x * (int64_t)nv + v] = sh[0];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64) void gibbs_stats_fold(const double* __restrict__ rec, int64_t nb, int nv,
+                                                       double* __restrict__ out) {
+    const int v = threadIdx.x;
+    if (v >= nv) return;
+    double a = 0.0;
+    for (int64_t b = 0; b < nb; ++b) a += rec[b * nv + v];
+    out[v] = a;
+}
+
+size_t gibbs_stats_workspace_bytes(int64_t n, int p) { return align256((size_t)((n + 255) / 256) * (2 + p) * 8); }
+
+hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
+                              const double* X, int p, const double* w, double* out, void* workspace, hipStream_t s) {
+    const int64_t nb = (n + 255) / 256;
+    if (nb == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gibbs_stats_blocks, dim3((unsigned)nb), dim3(256), 0, s, n, r, Ft, yres, y, X, p, w,
+                       (double*)workspace);
+    hipLaunchKernelGGL(gibbs_stats_fold, dim3(1), dim3(64), 0, s, (const double*)workspace, nb, 2 + p, out);
+    return hipGetLastError();
+}
+
+}  // namespace nngp

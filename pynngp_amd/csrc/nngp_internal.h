@@ -39,6 +39,7 @@ struct BfArgs {
     const double* values;      // (n_points,) or null
     double* B;                 // (n_rows, m) or null
     double* F;                 // (n_rows,) or null
+    double* R;                 // (n_rows,) residuals v_i - B_i v_N(i), or null
     double* partials;          // [4]
     double* bpart;             // 4 doubles per block: sum log F, sum r^2/F, first bad-pivot row, first bad-index row
 };
@@ -67,6 +68,21 @@ hipError_t knn_plan(int64_t n_points, KnnPlan* plan);
 // prior mode: rows [q0, q1) of coords against coords[0:i]; query mode: query[q0:q1] against all coords
 hipError_t knn_launch(bool prior, const double* coords, int64_t n_points, int m, const double* query, int64_t q0,
                       int64_t q1, int32_t* nbr, void* workspace, const KnnPlan& plan, hipStream_t s);
+
+// Gibbs sampler (gibbs.hip)
+size_t reverse_workspace_bytes(int64_t n, int m);
+hipError_t reverse_launch(const int32_t* nbr, int64_t n, int m, int32_t* off, int32_t* rev_j, int32_t* rev_k,
+                          void* workspace, hipStream_t s);
+int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
+                               int32_t* color);
+hipError_t gibbs_w_sweep_launch(const int32_t* color_off, const int32_t* members_all, int n_colors,
+                                const int32_t* color_off_host, const double* B, const double* Ft, double sigma2,
+                                double tau2, const double* yres, double* w, double* r, const int32_t* off,
+                                const int32_t* rev_j, const int32_t* rev_k, int m, const double* z, uint64_t seed,
+                                uint64_t sweep, hipStream_t s);
+size_t gibbs_stats_workspace_bytes(int64_t n, int p);
+hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
+                              const double* X, int p, const double* w, double* out, void* workspace, hipStream_t s);
 
 // row-order plan (nngp_row_order): Morton-sorted local rows for cache locality
 size_t row_order_workspace_bytes(int64_t n_rows);

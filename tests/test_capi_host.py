@@ -58,7 +58,7 @@ def _sweep(lib, **kw):
     a.update(kw)
     P = lambda v: None if v is None else ctypes.c_void_p(v)  # noqa: E731
     return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], P(a["nbr"]), None, a["n_rows"], a["m"], a["i0"], a["kind"],
-                             a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]),
+                             a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]), P(a.get("R")),
                              P(a["partials"]), P(a["workspace"]), a["workspace_bytes"], a["algo"], P(a["stream"]))
 
 
@@ -78,6 +78,7 @@ def _sweep(lib, **kw):
     (dict(algo=1, m=17), -4, "lane kernel"),
     (dict(algo=9), -1, "unknown algo"),
     (dict(workspace_bytes=16), -1, "workspace too small"),
+    (dict(R=256), -1, "R (residuals) needs values"),
 ])
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code

@@ -1,0 +1,201 @@
+"""GPU Gibbs sampler: reverse CSR, residual output, one
+colour sweep against the dense oracle with given normals, the stationary law of the
+Philox-driven sweep, the stats reduction, determinism and parameter recovery.
+
+The reference's sampler (nngp.py:98-101) cannot run, so parity is against the
+model's exact full conditionals (oracle/nngp_gibbs_oracle.py), "parity unpinned"
+with respect to the reference itself."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nngp_gibbs_oracle as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(dev, n, m, phi=6.0, seed=0, kind="exponential"):
+    from pynngp_amd import _lib
+
+    rng = np.random.default_rng(seed)
+    c = torch.from_numpy(rng.uniform(size=(n, 2))).to(dev)
+    nbr = _lib.knn_prior(c, m)
+    w = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    R = torch.empty(n, dtype=torch.float64, device=dev)
+    B, F, p = _lib.bf_sweep(c, nbr, 0, kind, 1.0, phi, 0.0, values=w, R=R)
+    off, rev_j, rev_k = _lib.reverse_neighbors(nbr)
+    colors, nc = _lib.color_moral_graph(nbr.cpu().numpy(), off.cpu().numpy(), rev_j.cpu().numpy())
+    members = torch.from_numpy(np.argsort(colors, kind="stable").astype(np.int32)).to(dev)
+    color_off = np.concatenate([[0], np.cumsum(np.bincount(colors, minlength=nc))]).astype(np.int32)
+    return dict(c=c, nbr=nbr, w=w, R=R, B=B, F=F, p=p, off=off, rev_j=rev_j, rev_k=rev_k, colors=colors,
+                members=members, color_off=color_off, rng=rng)
+
+
+def _residuals(nbr, B, w):
+    wn = np.where(nbr >= 0, w[np.maximum(nbr, 0)], 0.0)
+    return w - (B * wn).sum(1)
+
+
+@pytest.mark.parametrize("n,m", [(1, 4), (300, 1), (5000, 10), (20000, 15)])
+def test_reverse_neighbors_exact(dev, n, m):
+    s = _setup(dev, n, m)
+    nbr = s["nbr"].cpu().numpy()
+    entries = sorted((int(nbr[j, k]), j, k) for j in range(n) for k in range(m) if nbr[j, k] >= 0)
+    off = s["off"].cpu().numpy()
+    assert off[0] == 0 and off[-1] == len(entries)
+    cnt = np.bincount([e[0] for e in entries], minlength=n)
+    np.testing.assert_array_equal(np.diff(off), cnt)
+    tot = len(entries)
+    np.testing.assert_array_equal(s["rev_j"].cpu().numpy()[:tot], [e[1] for e in entries])
+    np.testing.assert_array_equal(s["rev_k"].cpu().numpy()[:tot], [e[2] for e in entries])
+    assert G.coloring_is_valid(nbr, s["colors"]) if n <= 5000 else True
+
+
+@pytest.mark.parametrize("m", [1, 5, 15])
+def test_residual_output(dev, m):
+    s = _setup(dev, 4000, m)
+    r_ref = _residuals(s["nbr"].cpu().numpy(), s["B"].cpu().numpy(), s["w"].cpu().numpy())
+    np.testing.assert_allclose(s["R"].cpu().numpy(), r_ref, rtol=0, atol=1e-12 * (1 + np.abs(r_ref).max()))
+    # R is consistent with the partials' quadratic form
+    q = float((s["R"] ** 2 / s["F"]).sum())
+    assert abs(q - float(s["p"][1])) <= 1e-10 * abs(q)
+
+
+@pytest.mark.parametrize("n,m,sigma2,tau2", [(400, 5, 1.3, 0.2), (1500, 10, 0.7, 0.05), (3000, 15, 2.0, 1.0)])
+def test_w_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2):
+    from pynngp_amd import _lib
+
+    s = _setup(dev, n, m, seed=n)
+    rng = s["rng"]
+    yres = torch.from_numpy(rng.standard_normal(n) * 1.5).to(dev)
+    z = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    nbr, B, F = s["nbr"].cpu().numpy(), s["B"].cpu().numpy(), s["F"].cpu().numpy()
+    w0 = s["w"].cpu().numpy().copy()
+    P = G.precision(nbr, B, F * sigma2) + np.eye(n) / tau2
+    b = yres.cpu().numpy() / tau2
+    w_ref = G.color_sweep(P, b, w0, s["colors"], z.cpu().numpy())
+    w, r = s["w"].clone(), s["R"].clone()
+    _lib.gibbs_w_sweep(s["members"], s["color_off"], s["B"], s["F"], sigma2, tau2, yres, w, r, s["off"],
+                       s["rev_j"], s["rev_k"], 123, 0, z=z)
+    wh = w.cpu().numpy()
+    np.testing.assert_allclose(wh, w_ref, rtol=1e-9, atol=1e-9 * np.abs(w_ref).max())
+    # maintained residuals equal the recomputed ones
+    np.testing.assert_allclose(r.cpu().numpy(), _residuals(nbr, B, wh), rtol=0, atol=1e-10 * (1 + np.abs(wh).max()))
+
+
+def test_w_sweep_stationary_law(dev):
+    """Philox-driven sweeps sample N(P^-1 b, P^-1) (exact Gaussian posterior, N=24)."""
+    from pynngp_amd import _lib
+
+    n, m, sigma2, tau2 = 24, 4, 1.0, 0.5
+    s = _setup(dev, n, m, phi=3.0, seed=7)
+    rng = s["rng"]
+    yres = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    nbr, B, F = s["nbr"].cpu().numpy(), s["B"].cpu().numpy(), s["F"].cpu().numpy()
+    P = G.precision(nbr, B, F * sigma2) + np.eye(n) / tau2
+    mu = np.linalg.solve(P, yres.cpu().numpy() / tau2)
+    S = np.linalg.inv(P)
+    w, r = s["w"].clone(), s["R"].clone()
+    draws = []
+    n_sweeps = 20000
+    for t in range(n_sweeps):
+        _lib.gibbs_w_sweep(s["members"], s["color_off"], s["B"], s["F"], sigma2, tau2, yres, w, r, s["off"],
+                           s["rev_j"], s["rev_k"], 99, t)
+        if t >= 100:
+            draws.append(w.clone())
+    W = torch.stack(draws).cpu().numpy()
+    sd = np.sqrt(np.diag(S))
+    # batch means for the Monte-Carlo error of the mean
+    nb = 50
+    bm = W[: len(W) // nb * nb].reshape(nb, -1, n).mean(1)
+    se = bm.std(0, ddof=1) / np.sqrt(nb)
+    zscore = (W.mean(0) - mu) / np.maximum(se, 1e-3 * sd)
+    assert np.abs(zscore).max() < 5.0, zscore
+    emp = np.cov(W.T)
+    np.testing.assert_allclose(np.sqrt(np.diag(emp)), sd, rtol=0.06)
+    corr_emp = emp / np.outer(np.sqrt(np.diag(emp)), np.sqrt(np.diag(emp)))
+    corr = S / np.outer(sd, sd)
+    assert np.abs(corr_emp - corr).max() < 0.08
+
+
+def test_philox_normals_moments(dev):
+    """With yres = 0 and tau2 huge, one sweep from w = 0 on m = 0 gives w = z sqrt(sigma2 F)."""
+    from pynngp_amd import _lib
+
+    n = 200000
+    c = torch.rand(n, 2, dtype=torch.float64, device=dev)
+    nbr = torch.full((n, 0), -1, dtype=torch.int32, device=dev)
+    w = torch.zeros(n, dtype=torch.float64, device=dev)
+    R = torch.empty_like(w)
+    B, F, _ = _lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 3.0, 0.0, values=w, R=R)
+    off, rev_j, rev_k = _lib.reverse_neighbors(nbr)
+    members = torch.arange(n, dtype=torch.int32, device=dev)
+    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), B, F, 1.0, 1e300, torch.zeros_like(w), w, R, off, rev_j,
+                       rev_k, 5, 0)
+    z = w.cpu().numpy()
+    assert abs(z.mean()) < 5 / np.sqrt(n)
+    assert abs(z.var() - 1) < 5 * np.sqrt(2 / n)
+    assert abs((z ** 3).mean()) < 5 * np.sqrt(15 / n)
+    assert abs((z ** 4).mean() - 3) < 5 * np.sqrt(96 / n)
+    # different sweep counter -> independent stream (r back to w - B w_N = 0)
+    w2 = torch.zeros_like(w)
+    R.zero_()
+    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), B, F, 1.0, 1e300, torch.zeros_like(w), w2, R, off, rev_j,
+                       rev_k, 5, 1)
+    assert abs(np.corrcoef(z, w2.cpu().numpy())[0, 1]) < 5 / np.sqrt(n)
+
+
+@pytest.mark.parametrize("p", [0, 1, 3])
+def test_gibbs_stats(dev, p):
+    from pynngp_amd import _lib
+
+    n = 100003
+    g = torch.Generator(device="cpu").manual_seed(p)
+    mk = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(dev)  # noqa: E731
+    r, Ft, yres, y, w = mk(n), mk(n).abs() + 0.1, mk(n), mk(n), mk(n)
+    X = mk(n, p) if p else None
+    out = _lib.gibbs_stats(r, Ft, yres, y, X, w).cpu().numpy()
+    rh, Fh, yr, yh, wh = (t.cpu().numpy() for t in (r, Ft, yres, y, w))
+    exp = [np.sum(rh ** 2 / Fh), np.sum((yr - wh) ** 2)]
+    if p:
+        exp += list(X.cpu().numpy().T @ (yh - wh))
+    np.testing.assert_allclose(out, exp, rtol=1e-11, atol=1e-9)
+
+
+def _simulate(n, sigma2, phi, tau2, beta, seed):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(size=(n, 2))
+    d = np.sqrt(((c[:, None, :] - c[None, :, :]) ** 2).sum(-1))
+    L = np.linalg.cholesky(sigma2 * np.exp(-phi * d) + 1e-10 * np.eye(n))
+    w = L @ rng.standard_normal(n)
+    X = np.column_stack([np.ones(n), rng.standard_normal(n)])
+    y = X @ beta + w + np.sqrt(tau2) * rng.standard_normal(n)
+    return c, y, X, w
+
+
+def test_seqnngp_determinism(dev):
+    from pynngp_amd import SeqNNGP
+
+    c, y, X, _ = _simulate(600, 1.0, 5.0, 0.2, np.array([1.0, -0.5]), 1)
+    a = SeqNNGP(c, y, X, m=8, seed=11, device=dev).sample(30)
+    b = SeqNNGP(c, y, X, m=8, seed=11, device=dev).sample(30)
+    for k in ("beta", "sigma2", "tau2", "phi"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_seqnngp_recovers_parameters(dev):
+    from pynngp_amd import Priors, SeqNNGP
+
+    truth = dict(sigma2=1.0, phi=6.0, tau2=0.1)
+    beta = np.array([1.0, -0.5])
+    c, y, X, w = _simulate(2500, truth["sigma2"], truth["phi"], truth["tau2"], beta, 2)
+    pri = Priors(sigma2_ig=(2.0, 1.0), tau2_ig=(2.0, 0.1), phi_unif=(0.5, 60.0))
+    s = SeqNNGP(c, y, X, m=10, priors=pri, phi=10.0, tau2=0.5, seed=3, device=dev, phi_tuning=0.1)
+    res = s.sample(2500, burn=1000, keep_w_mean=True)
+    assert 0.1 < res["phi_accept_rate"] < 0.95
+    assert abs(res["beta"][:, 1].mean() - beta[1]) < 0.05
+    assert 0.5 < res["sigma2"].mean() / truth["sigma2"] < 2.0
+    assert 0.5 < res["tau2"].mean() / truth["tau2"] < 2.0
+    assert 0.4 < res["phi"].mean() / truth["phi"] < 2.5
+    # the posterior mean of w tracks the simulated field
+    assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.8
