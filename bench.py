@@ -111,7 +111,7 @@ def main():
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=["exponential", "matern32"])
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
-    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad", "pairb"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
     ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")

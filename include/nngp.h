@@ -43,6 +43,7 @@ extern "C" {
 #define NNGP_ALGO_WAVE 2 /* one wavefront per location (m <= 63)      */
 #define NNGP_ALGO_PAIR 3 /* two lanes per location (10 <= m <= 20)     */
 #define NNGP_ALGO_QUAD 4 /* four lanes per location (m in 15, 16, 20)  */
+#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked elimination (2 <= m <= 20) */
 
 #define NNGP_MAX_M 63
 

@@ -14,7 +14,8 @@ from typing import Optional, Tuple
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libnngp_hip.so")
+# NNGP_LIB overrides the library path (A/B timing of alternative builds only; it must exist)
+LIB_PATH = os.environ.get("NNGP_LIB") or os.path.join(_HERE, "_build", "libnngp_hip.so")
 SYMBOLS = (
     "nngp_version",
     "nngp_last_error",
@@ -36,7 +37,7 @@ SYMBOLS = (
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1}
-ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4}
+ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4, "pairb": 5}
 MAX_M = 63
 
 

@@ -71,6 +71,8 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
                                                 double* __restrict__ bpart) {
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
+    __shared__ double etab[NNGP_EXP_TAB_N];
+    nngp_exp_table_load(etab, Pc.sigma2);
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
     const int64_t tid = blk * blockDim.x + threadIdx.x;
     const int q = (int)(threadIdx.x % P);
@@ -125,9 +127,9 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
             for (int b = 0; b < NR; ++b) {
                 if (b >= P * s + P) continue;  // beyond this local row's width
                 if (b < P * s) {
-                    R[s][b] = nngp_cov_d2<KIND>(Pc, nngp_d2(ox[s], oy[s], X[b], Y[b]));
+                    R[s][b] = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], X[b], Y[b]));
                 } else if (b < P * s + P - 1) {  // diagonal block: lane-dependent
-                    const double c = nngp_cov_d2<KIND>(Pc, nngp_d2(ox[s], oy[s], X[b], Y[b]));
+                    const double c = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], X[b], Y[b]));
                     R[s][b] = b < a ? c : (b == a ? Pc.diag : 0.0);
                 } else {
                     R[s][b] = b == a ? Pc.diag : 0.0;

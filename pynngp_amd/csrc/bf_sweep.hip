@@ -45,6 +45,8 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     constexpr int N1 = M + 1;  // joint block order
+    __shared__ double etab[NNGP_EXP_TAB_N];
+    nngp_exp_table_load(etab, P.sigma2);
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
     const int64_t r = blk * blockDim.x + threadIdx.x;
     const bool live = r < n_rows;
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
 #pragma unroll
     for (int a = 0; a < N1; ++a) {
 #pragma unroll
-        for (int b = 0; b < a; ++b) A[a][b] = nngp_cov_d2<KIND>(P, nngp_d2(px[a], py[a], px[b], py[b]));
+        for (int b = 0; b < a; ++b) A[a][b] = nngp_cov_d2<KIND>(P, etab, nngp_d2(px[a], py[a], px[b], py[b]));
         A[a][a] = P.diag;
     }
 
@@ -248,6 +250,9 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     if (algo == kAlgoLane) {
         ok = a.kind == 1 ? launch_lane_m<1>(a, P, s) : launch_lane_m<0>(a, P, s);
         nb = bf_lane_blocks(a.n_rows);
+    } else if (algo == kAlgoPairB) {
+        ok = bf_pairb_launch(a, P, s);
+        nb = bf_group_blocks(a.n_rows, 2);
     } else if (algo == kAlgoPair || algo == kAlgoQuad) {
         const int lanes = algo == kAlgoPair ? 2 : 4;
         ok = bf_group_launch(a, P, lanes, s);

@@ -23,6 +23,8 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
+    __shared__ double etab[NNGP_EXP_TAB_N];
+    nngp_exp_table_load(etab, P.sigma2);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     double lf_acc = 0.0, q_acc = 0.0;  // lane 0 accumulates this wave's locations in row order
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
         for (int b = 0; b < NR; ++b) {
             const double bx = wave_bcast(xx, b);
             const double by = wave_bcast(xy, b);
-            const double c = nngp_cov_d2<KIND>(P, nngp_d2(xx, xy, bx, by));
+            const double c = nngp_cov_d2<KIND>(P, etab, nngp_d2(xx, xy, bx, by));
             row[b] = b == lane ? P.diag : c;
         }
         bool bad = false;

@@ -40,7 +40,7 @@ int resolve_algo(int32_t algo, int32_t m) {
 
 int64_t bf_blocks(int64_t n_rows, int algo) {
     if (algo == nngp::kAlgoLane) return nngp::bf_lane_blocks(n_rows);
-    if (algo == nngp::kAlgoPair) return nngp::bf_group_blocks(n_rows, 2);
+    if (algo == nngp::kAlgoPair || algo == nngp::kAlgoPairB) return nngp::bf_group_blocks(n_rows, 2);
     if (algo == nngp::kAlgoQuad) return nngp::bf_group_blocks(n_rows, 4);
     return nngp::bf_wave_blocks(n_rows);
 }
@@ -82,11 +82,13 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
     if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
     int a = resolve_algo(algo, m);
-    if (a < nngp::kAlgoLane || a > nngp::kAlgoQuad) return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    if (a < nngp::kAlgoLane || a > nngp::kAlgoPairB) return fail(NNGP_EINVAL, "unknown algo %d", algo);
     if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
         return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
     if ((a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !nngp::bf_group_supported(m, a == nngp::kAlgoPair ? 2 : 4))
         return fail(NNGP_EUNSUP, "no %s-lane kernel instantiated for m=%d", a == nngp::kAlgoPair ? "2" : "4", m);
+    if (a == nngp::kAlgoPairB && !nngp::bf_pairb_supported(m))
+        return fail(NNGP_EUNSUP, "no blocked pair kernel instantiated for m=%d", m);
     const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, algo);
     if (workspace_bytes < need)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);

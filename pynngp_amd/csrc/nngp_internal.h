@@ -24,6 +24,7 @@ constexpr int kAlgoLane = 1;
 constexpr int kAlgoWave = 2;
 constexpr int kAlgoPair = 3;  // bf_group, 2 lanes per location
 constexpr int kAlgoQuad = 4;  // bf_group, 4 lanes per location
+constexpr int kAlgoPairB = 5; // bf_pairb, 2 lanes per location, 2x2-blocked elimination
 constexpr int kLaneMaxM = 16;
 
 struct BfArgs {
@@ -49,6 +50,8 @@ hipError_t combine_partials_launch(const double* gathered, int world, double* ou
 bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s);
 bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t s);
 bool bf_group_supported(int m, int lanes);
+bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
+bool bf_pairb_supported(int m);
 // number of 256-thread blocks (= partial records) each kernel launches for n_rows
 int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);

@@ -18,7 +18,7 @@ import torch
 from . import _lib
 
 _KINDS = ("exponential", "matern32")
-_ALGOS = ("auto", "lane", "wave", "pair", "quad")
+_ALGOS = ("auto", "lane", "wave", "pair", "quad", "pairb")
 
 
 @torch.library.custom_op("nngp::bf_sweep", mutates_args=(), device_types="cuda")

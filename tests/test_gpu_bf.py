@@ -68,12 +68,14 @@ CASES = [
 PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
 QUAD_M = (15, 16, 20)  # and for the 4-lane kernel
 GROUP_M = QUAD_M
+PAIRB_M = tuple(range(2, 21))  # and for the 2x2-blocked 2-lane kernel
 
 
-@pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad"])
+@pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad", "pairb"])
 @pytest.mark.parametrize("kind,theta,m", CASES)
 def test_bf_vs_oracle(lib, dev, c_oracle, kind, theta, m, algo):
-    if (algo == "pair" and m not in PAIR_M) or (algo == "quad" and m not in QUAD_M):
+    if ((algo == "pair" and m not in PAIR_M) or (algo == "quad" and m not in QUAD_M)
+            or (algo == "pairb" and m not in PAIRB_M)):
         pytest.skip("not instantiated")
     coords, y = _field(6000, m)
     nbr = c_oracle.c_knn_prior(coords, m)
@@ -86,8 +88,8 @@ def test_bf_large_m(lib, dev, c_oracle, m):
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 8.0, 0.05), y, "auto")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, "wave")
-    for algo in ("pair", "quad"):
-        if m in (PAIR_M if algo == "pair" else QUAD_M):
+    for algo, ms in (("pair", PAIR_M), ("quad", QUAD_M), ("pairb", PAIRB_M)):
+        if m in ms:
             _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, algo)
             _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 30.0, 0.0), y, algo)
 
@@ -98,6 +100,18 @@ def test_bf_pair_all_m(lib, dev, c_oracle, m):
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.0), y, "pair")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "pair")
+
+
+@pytest.mark.parametrize("m", list(PAIRB_M))
+def test_bf_pairb_all_m(lib, dev, c_oracle, m):
+    """Blocked pair kernel, every instantiated m (odd m ends on a (neighbour, location) pair,
+    even m on (location, padding)); duplicated points exercise coincident coordinates."""
+    coords, y = _field(2500, 300 + m)
+    coords[1000:1010] = coords[500]  # exact duplicates (d2 = 0 -> the 2^-1000 floor)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.3), y, "pairb")
+    _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "pairb")
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (0.8, 30.0, 0.01), None, "pairb")
 
 
 def test_bf_m0_and_no_values(lib, dev, c_oracle):
@@ -156,7 +170,7 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     sing = nbr.copy()
     sing[1234, 1] = sing[1234, 0]  # repeated neighbour: C_N singular, second pivot exactly 0 (sigma2 = 1)
     sing[1500, 1] = sing[1500, 0]
-    for algo in ["lane", "wave", "pair"]:
+    for algo in ["lane", "wave", "pair", "pairb"]:
         B, F, p = lib.bf_sweep(c, torch.from_numpy(sing).to(dev), 0, "exponential", 1.0, 5.0, 0.0, algo=algo)
         _, _, po = c_oracle.c_bf_sweep(coords, sing, "exponential", (1.0, 5.0, 0.0), None)
         assert p[2].item() == 1234 == po[2]
@@ -179,7 +193,7 @@ def test_bf_full_size_properties(lib, dev, c_oracle):
     theta = (1.0, 30.0, 0.0)
     B, F, p = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="lane")
     ll = c_oracle.loglik_from_partials(p.cpu().numpy(), n)
-    for algo in ("wave", "pair", "quad"):
+    for algo in ("wave", "pair", "quad", "pairb"):
         Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo=algo)
         assert torch.allclose(F, Fw, rtol=1e-12, atol=0)
         assert torch.allclose(B, Bw, rtol=0, atol=1e-10)
@@ -211,7 +225,7 @@ def test_bf_op_registered(dev, c_oracle):
     assert abs(p2[0].item() - po[0]) <= 1e-12 * abs(po[0])
 
 
-@pytest.mark.parametrize("algo", ["lane", "pair", "quad", "wave"])
+@pytest.mark.parametrize("algo", ["lane", "pair", "quad", "wave", "pairb"])
 def test_bf_row_order_bit_identical(lib, dev, c_oracle, algo):
     """Visiting rows in Z-order (nngp_row_order) changes nothing per row."""
     coords, y = _field(30000, 12)

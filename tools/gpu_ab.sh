@@ -1,0 +1,16 @@
+# A/B timing of library builds / algos on ONE GPU box (run via gpurun).
+#   VARIANTS="label:libpath:algo ..." bash tools/gpu_ab.sh [bench args...]
+# Each variant runs the bench (no CPU baseline) twice, interleaved, so box-to-box clock
+# differences cancel; prints kernel ms per run.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/ab
+for rep in 1 2; do
+  for v in $VARIANTS; do
+    label=${v%%:*}; rest=${v#*:}; lib=${rest%%:*}; algo=${rest#*:}
+    NNGP_LIB=$lib timeout -k 10 120 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 --algo $algo "$@" \
+      > gpurun_out/ab/$label.$rep.json 2>> gpurun_out/ab/err.log || exit $?
+    python3 -c "import json; d=json.load(open('gpurun_out/ab/$label.$rep.json')); print('$label', $rep, round(d['roofline']['kernel_ms'],4), 'ms', round(d['value']/1e9,3), 'Gloc/s')"
+  done
+done
