@@ -30,7 +30,7 @@ bool bf_group_launch(const BfArgs& a, const CovParams& Pc, int P, hipStream_t s)
     return bf_pair_launch_d(a, Pc, s);
 }
 
-bool bf_pairb_supported(int m) { return m >= 2 && m <= 20; }
+bool bf_pairb_supported(int m) { return m >= 1 && m <= 20; }
 
 bool bf_pairb_launch(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     if (!bf_pairb_supported(a.m)) return false;

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void bf_pairb(const double2* __restrict__ coor
                                                 const double* __restrict__ values, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double* __restrict__ bpart) {
-    static_assert(M >= 2 && M <= 24, "pairb instantiated for 2 <= m <= 24");
+    static_assert(M >= 1 && M <= 24, "pairb instantiated for 1 <= m <= 24");
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps

@@ -10,10 +10,9 @@
 //     one FMA gives f, a degree-4 polynomial gives 2^(f/256), a 256-entry table
 //     (sigma2 2^(j/256), in LDS) and one ldexp finish it.  11 VALU ops + 1 LDS read
 //     instead of the 16 of a degree-11 polynomial on |f| <= 1/2.
-//   * d = sqrt(d2): v_rsq_f64 plus one Newton step (s = x y, r = x - s^2,
-//     d = s + r y/2); d2 carries a 2^-1000 floor from the distance FMA, so no clamp
-//     is needed against d2 == 0 (exp(-phi 2^-500) == 1 in fp64);
-//   * 1/sqrt(pivot): v_rsq_f64 plus two Newton steps.
+//   * d = sqrt(d2) and 1/sqrt(pivot): v_rsq_f64 plus a second-order correction
+//     (below); d2 carries a 2^-1000 floor from the distance FMA, so no clamp is
+//     needed against d2 == 0 (exp(-phi 2^-500) == 1 in fp64).
 // The exponent is bounded by clamping d2 at d2max, where sigma2 2^-1080 has
 // underflowed; far-away padding points (nngp_internal.h) land there.
 // The same source compiles on the host (NNGP_MATH_HOST) so
@@ -29,9 +28,12 @@
 #define NNGP_FN static inline
 #define NNGP_HD static inline
 static inline double nngp_rsq_approx(double x) {
-    // emulate v_rsq_f64's ~2^-29 relative accuracy so the refinement is tested
+    // emulate v_rsq_f64's relative error (measured on gfx950: up to 2^-24.2,
+    // tools/ubench/rsq_acc.hip) with either sign, so the refinement is tested at it
     double y = 1.0 / sqrt(x);
-    return y * (1.0 + 0x1p-29);
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return y * ((u >> 7) & 1 ? 1.0 + 0x1p-24 : 1.0 - 0x1p-24);
 }
 static inline int32_t nngp_lo_dword(double t) {
     uint64_t u;
@@ -102,23 +104,28 @@ NNGP_FN double nngp_exp_tab(const CovParams& P, const double* tab, double d) {
     return ldexp(fma(T, fq, T), ki >> 8);                 // floor(k / 256)
 }
 
-// sqrt(d2) for d2 >= 2^-1000, ~1 ulp
+// v_rsq_f64 is only good to ~2^-24 (measured), so one plain Newton step would leave
+// ~1.5 * 2^-48 relative error.  Both refinements instead use the second-order series
+// in e = 1 - x y^2 (|e| ~ 2^-23; the e^3 term is below 2^-66):
+//   sqrt(x)   = s (1 - e')^(-1/2), s = x y, e' = 1 - s y:  s (1 + e'/2 + 3 e'^2 / 8)
+//   1/sqrt(x) = y (1 - e)^(-1/2)                        :  y (1 + e/2 + 3 e^2 / 8)
+// 5 ops each (one plain Newton step is 4; two are 8), within ~1 ulp.
+
+// sqrt(x) for x >= 2^-1000
 NNGP_FN double nngp_sqrt(double x) {
     const double y = nngp_rsq_approx(x);
     const double s = x * y;
-    const double r = fma(-s, s, x);
-    const double h = 0.5 * y;
-    return fma(r, h, s);
+    const double e = fma(-s, y, 1.0);
+    const double g = e * fma(0.375, e, 0.5);
+    return fma(s, g, s);
 }
 
-// 1/sqrt(x) for a positive pivot: two Newton steps on v_rsq_f64.
+// 1/sqrt(x) for a positive pivot
 NNGP_FN double nngp_rsqrt(double x) {
-    double y = nngp_rsq_approx(x);
-    double t = fma(-(x * y), y, 1.0);
-    y = fma(0.5 * y, t, y);
-    t = fma(-(x * y), y, 1.0);
-    y = fma(0.5 * y, t, y);
-    return y;
+    const double y = nngp_rsq_approx(x);
+    const double e = fma(-(x * y), y, 1.0);
+    const double g = e * fma(0.375, e, 0.5);
+    return fma(y, g, y);
 }
 
 // Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12):

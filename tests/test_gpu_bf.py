@@ -68,7 +68,7 @@ CASES = [
 PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
 QUAD_M = (15, 16, 20)  # and for the 4-lane kernel
 GROUP_M = QUAD_M
-PAIRB_M = tuple(range(2, 21))  # and for the 2x2-blocked 2-lane kernel
+PAIRB_M = tuple(range(1, 21))  # and for the 2x2-blocked 2-lane kernel
 
 
 @pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad", "pairb"])
@@ -254,3 +254,27 @@ def test_combine_partials_rank_order(lib, dev):
     assert out == [(1.5 + 0.25) + 1e-17, (2.0 + 3.0) + 1.0, 5.0, 2.0]
     out = lib.combine_partials(g[:1, :]).cpu().tolist()
     assert out == [1.5, 2.0, -1.0, 7.0]
+
+
+@pytest.mark.parametrize("algo", ["lane", "pairb", "wave"])
+@pytest.mark.parametrize("kind", ["exponential", "matern32"])
+def test_bf_m1_covariance_ulp(lib, dev, c_oracle, kind, algo):
+    """m = 1 isolates the device covariance: B_i = C(d_i) / (sigma2 + tau2) with d_i the
+    nearest-prior distance.  Checked against 80-bit long double at 2e-15 relative, i.e.
+    a few ulp (v_rsq_f64 alone is only good to ~2^-24; one plain Newton step for sqrt
+    would leave ~1e-14 relative error here)."""
+    coords, _ = _field(20000, 77)
+    nbr = c_oracle.c_knn_prior(coords, 1)
+    sigma2, phi, tau2 = 1.3, 9.0, 0.4
+    c = torch.from_numpy(coords).to(dev)
+    B, F, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, kind, sigma2, phi, tau2, algo=algo)
+    j = nbr[1:, 0]
+    dx = coords[1:, 0].astype(np.longdouble) - coords[j, 0]
+    dy = coords[1:, 1].astype(np.longdouble) - coords[j, 1]
+    d = np.sqrt(dx * dx + dy * dy)
+    e = np.exp(-np.longdouble(phi) * d)
+    cov = sigma2 * e * (1 + np.longdouble(phi) * d if kind == "matern32" else 1)
+    Bx = cov / np.longdouble(sigma2 + tau2)
+    Bg = B.cpu().numpy()[1:, 0].astype(np.longdouble)
+    rel = np.abs(Bg - Bx) / Bx
+    assert float(rel.max()) <= 2e-15, float(rel.max())

@@ -1,7 +1,8 @@
 """CPU: accuracy of the kernel's fp64 exp2 / sqrt / rsqrt / covariance (nngp_math.h).
 
 The header compiles on the host (NNGP_MATH_HOST, v_rsq_f64 emulated at its
-~2^-29 accuracy) so the polynomial and the Newton refinements are checked
+measured ~2^-24 accuracy, tools/ubench/rsq_acc.hip) so the table exp and the
+second-order sqrt / rsqrt refinements are checked
 against libm without a GPU.  Bounds: table exp <= 2 ulp, sqrt <= 1 ulp, rsqrt <= 2
 ulp, covariance relative error <= 2e-14 (the exp argument phi*d ~ 20 carries
 its own rounding, amplified by |phi d| in the exponential).

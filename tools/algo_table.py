@@ -35,6 +35,7 @@ for m in range(lo, hi + 1):
     algos = ["lane"] if m <= 16 else []
     algos += ["pair"] if 10 <= m <= 20 else []
     algos += ["quad"] if m in (15, 16, 20) else []
+    algos += ["pairb"] if 2 <= m <= 20 else []
     algos += ["wave"]
     ref = None
     for algo in algos:
