@@ -37,8 +37,15 @@ __device__ __forceinline__ double pr_from0(double v) { return dpp_f64<0xA0>(v); 
 __device__ __forceinline__ double pr_from1(double v) { return dpp_f64<0xF5>(v); }  // lane 1's v
 __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return q1 ? v1 : v0; }
 
+// A/B builds only (make EXTRA=-DNNGP_PAIRB_WAVES_PER_EU=3): ask the compiler for an occupancy
+#ifdef NNGP_PAIRB_WAVES_PER_EU
+#define NNGP_PAIRB_ATTR __attribute__((amdgpu_waves_per_eu(NNGP_PAIRB_WAVES_PER_EU, NNGP_PAIRB_WAVES_PER_EU)))
+#else
+#define NNGP_PAIRB_ATTR
+#endif
+
 template <int M, int KIND>
-__global__ __launch_bounds__(256) void bf_pairb(const double2* __restrict__ coords, int64_t n_points,
+__global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0, const CovParams Pc,
                                                 const double* __restrict__ values, double* __restrict__ Bout,

@@ -144,46 +144,51 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ bpart, int64_t n_blocks,
                                                     double* __restrict__ partials) {
-    __shared__ double s0[1024], s1[1024], s2[1024], s3[1024];
+    // Fixed order: thread t folds records t, t + 1024, t + 2048, ... (each wave reads
+    // contiguous 2 KB per round; up to 8 rounds in flight before the first use), then
+    // a fixed xor-butterfly inside each wave and a fixed fold over the 16 waves.
+    __shared__ double sh[16][4];
     const int t = threadIdx.x;
-    // thread t folds the contiguous chunk [t*C, t*C + C) in order (independent 32-B loads)
-    const int64_t C = (n_blocks + 1023) / 1024;
     const double4* rec = (const double4*)bpart;
     double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
-    for (int64_t k0 = (int64_t)t * C; k0 < (int64_t)(t + 1) * C; k0 += 4) {
-        double4 r[4];
+    for (int64_t k0 = t; k0 < n_blocks; k0 += 8 * 1024) {
+        double4 r[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t k = k0 + u;
-            r[u] = (k < (int64_t)(t + 1) * C && k < n_blocks) ? rec[k] : make_double4(0.0, 0.0, INFINITY, INFINITY);
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + (int64_t)u * 1024;
+            r[u] = k < n_blocks ? rec[k] : make_double4(0.0, 0.0, INFINITY, INFINITY);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
             a += r[u].x;
             b += r[u].y;
             c = fmin(c, r[u].z);
             d = fmin(d, r[u].w);
         }
     }
-    s0[t] = a;
-    s1[t] = b;
-    s2[t] = c;
-    s3[t] = d;
-    __syncthreads();
-    for (int off = 512; off > 0; off >>= 1) {
-        if (t < off) {
-            s0[t] += s0[t + off];
-            s1[t] += s1[t + off];
-            s2[t] = fmin(s2[t], s2[t + off]);
-            s3[t] = fmin(s3[t], s3[t + off]);
-        }
-        __syncthreads();
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_min(c);
+    d = wave_min(d);
+    if ((t & 63) == 0) {
+        sh[t >> 6][0] = a;
+        sh[t >> 6][1] = b;
+        sh[t >> 6][2] = c;
+        sh[t >> 6][3] = d;
     }
+    __syncthreads();
     if (t == 0) {
-        partials[0] = s0[0];
-        partials[1] = s1[0];
-        partials[2] = s2[0] == INFINITY ? -1.0 : s2[0];
-        partials[3] = s3[0] == INFINITY ? -1.0 : s3[0];
+        a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+        for (int w = 0; w < 16; ++w) {
+            a += sh[w][0];
+            b += sh[w][1];
+            c = fmin(c, sh[w][2]);
+            d = fmin(d, sh[w][3]);
+        }
+        partials[0] = a;
+        partials[1] = b;
+        partials[2] = c == INFINITY ? -1.0 : c;
+        partials[3] = d == INFINITY ? -1.0 : d;
     }
 }
 
