@@ -110,6 +110,27 @@ int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, co
                   int32_t algo, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * B/F of query locations t against a reference set S (prediction / kriging at
+ * t not in S).  SURVEY.md 8(f) row 2: the reference builds Nt for refType != 'S=T'
+ * (NNGP._make_t_neighbor_sets, pyNNGP/nngp.py:64-71, KDTree(s).query(t, m)) but
+ * never evaluates B_t / F_t; this is the same fused kernel as nngp_bf_sweep with
+ * the location row taken from `query`:
+ *   C_N = C(S_N) + tau2 I over the neighbours nbr[(q - q0) * m + k] (indices into
+ *   ref; any of them, no prior restriction; -1 = unused slot), c = C(t_q, S_N),
+ *   C_tt = sigma2 + tau2, B_t = c^T C_N^{-1}, F_t = C_tt - c^T C_N^{-1} c.
+ * ref_values (nullable): v on S.  query_values (nullable; needs ref_values): v at t.
+ * R[q] = query_values[q] - B_t v_N(t) (query_values NULL: 0 - B_t v_N(t), i.e. minus
+ * the kriging mean).  partials as nngp_bf_sweep (with query_values: the
+ * conditional log density of v_t given v_S).  Rows q in [q0, q0 + n_rows) of
+ * n_query; order / workspace as nngp_bf_sweep (nngp_row_order on the query
+ * coordinates; nngp_bf_sweep_workspace_bytes).
+ * ------------------------------------------------------------------------- */
+int nngp_bf_cross(const double *ref, int64_t n_ref, const double *query, int64_t n_query, const int32_t *nbr,
+                  const int32_t *order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind, double sigma2,
+                  double phi, double tau2, const double *ref_values, const double *query_values, double *B, double *F,
+                  double *R, double *partials, void *workspace, size_t workspace_bytes, int32_t algo, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Visiting order for nngp_bf_sweep (a speed option; no reference counterpart:
  * the reference visits locations in input order, nngp.py:51).
  * order[t] = the t-th local row (0 .. n_rows-1) of locations i0 .. i0+n_rows-1

@@ -32,6 +32,12 @@ What it restates (reference = ``bwpriest/pyNNGP`` at ``/root/reference``):
   m = N-1 equals the dense-GP log density, m = 0 the independent normal, and the
   result is invariant to permuting a neighbour set.
 
+* ``c_bf_cross`` / ``dense_kriging`` -- B_t, F_t of points t outside the reference set
+  S against their neighbours in S (the reference builds
+  ``Nt = KDTree(s).query(t, m)`` at ``nngp.py:64-71`` but never evaluates B_t/F_t):
+  the same algebra with the location row taken from t; parity unpinned by the
+  reference, anchored by the dense GP conditional (``dense_kriging``) at m = |S|.
+
 Covariance kinds (the reference's ``cov`` plug-in, ``nngp.py:6,12``):
 ``exponential`` C(d) = sigma2 exp(-phi d); ``matern32``
 C(d) = sigma2 (1 + phi d) exp(-phi d); d is Euclidean distance in fp64.
@@ -275,3 +281,29 @@ def c_bf_sweep(coords, nbr, kind, theta, values=None, i0=0, want_bf=True):
     if rc != 0:
         raise RuntimeError(f"oracle_bf_sweep failed: {rc}")
     return B, F, partials
+
+
+def c_bf_cross(ref, query, nbr, kind, theta, ref_values=None, query_values=None, q0=0):
+    """B_t, F_t (and partials) of query rows q0 .. q0+len(nbr) against ``ref``: the C sweep
+    on the stacked coordinates [ref; query] with location rows n_ref + q (neighbour indices
+    already point into ref).  Missing query values are 0 (R = -kriging mean)."""
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    query = np.ascontiguousarray(query, dtype=np.float64)
+    both = np.concatenate([ref, query])
+    vals = None
+    if ref_values is not None:
+        qv = np.zeros(len(query)) if query_values is None else np.asarray(query_values, dtype=np.float64)
+        vals = np.concatenate([np.asarray(ref_values, dtype=np.float64), qv])
+    return c_bf_sweep(both, nbr, kind, theta, vals, i0=len(ref) + q0)
+
+
+def dense_kriging(ref, query, kind, theta, ref_values=None):
+    """Exact GP conditional of the query points given ALL of ref (numpy solve):
+    B = C(t, S) (C(S) + tau2 I)^{-1}, F = sigma2 + tau2 - B C(S, t), mean = B v_S."""
+    sigma2, phi, tau2 = theta
+    Css = cov_fn(kind, _pair_dist(ref[:, None, :], ref[None, :, :]), sigma2, phi) + tau2 * np.eye(len(ref))
+    Cts = cov_fn(kind, _pair_dist(query[:, None, :], ref[None, :, :]), sigma2, phi)
+    B = np.linalg.solve(Css, Cts.T).T
+    F = sigma2 + tau2 - np.einsum("ij,ij->i", B, Cts)
+    mean = None if ref_values is None else B @ np.asarray(ref_values, dtype=np.float64)
+    return B, F, mean

@@ -24,6 +24,7 @@ SYMBOLS = (
     "nngp_knn_query",
     "nngp_bf_sweep_workspace_bytes",
     "nngp_bf_sweep",
+    "nngp_bf_cross",
     "nngp_loglik_from_partials",
     "nngp_row_order_workspace_bytes",
     "nngp_row_order",
@@ -71,6 +72,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
     lib.nngp_bf_sweep_workspace_bytes.restype = SZ
     lib.nngp_bf_sweep.argtypes = [P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_cross.argtypes = [P, I64, P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_cross.restype = ctypes.c_int
     lib.nngp_row_order_workspace_bytes.argtypes = [I64]
     lib.nngp_row_order_workspace_bytes.restype = SZ
     lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
@@ -229,6 +232,55 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
                              float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
+    return B, F, partials
+
+
+def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: str, sigma2: float, phi: float,
+             tau2: float = 0.0, ref_values: Optional[torch.Tensor] = None,
+             query_values: Optional[torch.Tensor] = None, q0: int = 0, algo: str = "auto",
+             B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
+             partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+             order: Optional[torch.Tensor] = None,
+             R: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """B_t, F_t of query rows ``q0 .. q0 + len(nbr)`` against the reference set ``ref``
+    (nngp_bf_cross; prediction at t not in S).
+
+    ``nbr[r]`` lists indices into ``ref`` (e.g. :func:`knn_query` output).  Returns
+    ``(B, F, partials)``; with ``R`` given, ``R = query_values - B_t v_N`` (minus the
+    kriging mean when ``query_values`` is None).
+    """
+    ref, query = _as_coords(ref), _as_coords(query)
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
+    nbr = nbr.contiguous()
+    if ref_values is not None:
+        if ref_values.dtype != torch.float64 or ref_values.shape != (ref.shape[0],):
+            raise ValueError("ref_values must be float64 (n_ref,)")
+        ref_values = ref_values.contiguous()
+    if query_values is not None:
+        if query_values.dtype != torch.float64 or query_values.shape != (query.shape[0],):
+            raise ValueError("query_values must be float64 (n_query,)")
+        query_values = query_values.contiguous()
+    dev = _require_gpu(ref, query, nbr, ref_values, query_values, order)
+    rows, m = nbr.shape
+    if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
+        raise ValueError("order must be int32 (rows,)")
+    if kind not in KIND_CODES:
+        raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
+    lib = load()
+    a = ALGO_CODES[algo]
+    B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
+    F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
+    partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
+    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
+    if workspace is None or workspace.numel() < need:
+        workspace = _workspace(need, dev)
+    if R is not None and (R.dtype != torch.float64 or R.shape != (rows,)):
+        raise ValueError("R must be float64 (rows,)")
+    _check(lib.nngp_bf_cross(_ptr(ref), ref.shape[0], _ptr(query), query.shape[0], _ptr(nbr), _ptr(order), rows, m,
+                             int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(ref_values),
+                             _ptr(query_values), _ptr(B), _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace),
+                             workspace.numel(), a, _stream(dev)), "nngp_bf_cross")
     return B, F, partials
 
 

@@ -66,7 +66,7 @@ template <int M, int KIND, int P>
 __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0,
-                                                const CovParams Pc, const double* __restrict__ values,
+                                                const CovParams Pc, const double* __restrict__ values, const double2* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                 double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double* __restrict__ bpart) {
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
@@ -103,8 +103,9 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
         bad_index |= j >= 0 && !in_range;
         oval[s] = in_range;
         const bool self = a == M;
-        const double2* pc = self ? coords + i : (in_range ? coords + j : kFarPoints + (a & 63));
-        const double* pv = values == nullptr ? kZeroValue : (self ? values + i : (in_range ? values + j : kZeroValue));
+        const double2* pc = self ? qcoords + i : (in_range ? coords + j : kFarPoints + (a & 63));
+        const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
+                                : ((values != nullptr && in_range) ? values + j : kZeroValue);
         const double2 x = *pc;
         ox[s] = x.x;
         oy[s] = x.y;
@@ -219,7 +220,7 @@ template <int M, int KIND, int P>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
     hipLaunchKernelGGL((bf_group<M, KIND, P>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, a.B, a.F, a.R, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
 }
 
 // instantiate both kinds for one (M, P); returns false for other m

@@ -41,7 +41,7 @@ template <int M, int KIND>
 __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coords, int64_t n_points,
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0,
-                                               const CovParams P, const double* __restrict__ values,
+                                               const CovParams P, const double* __restrict__ values, const double2* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     constexpr int N1 = M + 1;  // joint block order
@@ -74,10 +74,10 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
         z[a] = *((values != nullptr && v) ? values + j : kZeroValue);
     }
     {
-        const double2 x = coords[i];
+        const double2 x = qcoords[i];
         px[M] = x.x;
         py[M] = x.y;
-        z[M] = *(values != nullptr ? values + i : kZeroValue);
+        z[M] = *(qvalues != nullptr ? qvalues + i : kZeroValue);
     }
 
     // joint block, lower triangle (A[a][b], b <= a)
@@ -222,7 +222,7 @@ template <int M, int KIND>
 static void launch_lane(const BfArgs& a, const CovParams& P, hipStream_t s) {
     const int64_t blocks = (a.n_rows + 255) / 256;
     hipLaunchKernelGGL((bf_lane<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, a.B, a.F, a.R, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, P, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
 }
 
 int64_t bf_lane_blocks(int64_t n_rows) { return (n_rows + 255) / 256; }

@@ -19,7 +19,7 @@ template <int NR, int KIND>
 __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0, int M,
-                                               const CovParams P, const double* __restrict__ values,
+                                               const CovParams P, const double* __restrict__ values, const double2* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
@@ -39,8 +39,9 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
         const bool is_self = lane == M;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
         const bool bad_index = j >= 0 && !in_range;
-        const double2* pc = is_self ? coords + i : (in_range ? coords + j : kFarPoints + lane);
-        const double* pv = values == nullptr ? kZeroValue : (is_self ? values + i : (in_range ? values + j : kZeroValue));
+        const double2* pc = is_self ? qcoords + i : (in_range ? coords + j : kFarPoints + lane);
+        const double* pv = is_self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
+                                   : ((values != nullptr && in_range) ? values + j : kZeroValue);
         const double2 xg = *pc;
         const double xx = xg.x, xy = xg.y;
         double zv = *pv;
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
 template <int NR, int KIND>
 static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s) {
     hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)n_blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.B, a.F, a.R, a.bpart);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
 }
 
 int64_t bf_wave_blocks(int64_t n_rows) {

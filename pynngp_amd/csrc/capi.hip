@@ -63,17 +63,18 @@ size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
     return align256((size_t)nb * 4 * sizeof(double));
 }
 
-int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
-                  int32_t m, int64_t i0,
-                  int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
-                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
-    if (coords == nullptr || partials == nullptr || workspace == nullptr)
-        return fail(NNGP_EINVAL, "coords, partials and workspace must be non-null");
+static int bf_common(const double* coords, int64_t n_points, const double* qcoords, int64_t n_locs,
+                     const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t i0, int32_t kind,
+                     double sigma2, double phi, double tau2, const double* values, const double* qvalues, double* B,
+                     double* F, double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo,
+                     void* stream) {
+    if (coords == nullptr || qcoords == nullptr || partials == nullptr || workspace == nullptr)
+        return fail(NNGP_EINVAL, "coordinates, partials and workspace must be non-null");
     if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
     if (m > 0 && n_rows > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null for m > 0");
-    if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_points)
+    if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
-                    (long long)n_points);
+                    (long long)n_locs);
     if (kind != NNGP_COV_EXPONENTIAL && kind != NNGP_COV_MATERN32) return fail(NNGP_EINVAL, "unknown kind %d", kind);
     if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
@@ -94,11 +95,29 @@ int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, co
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
 
     hipStream_t s = (hipStream_t)stream;
-    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, B, F, R,
-                      partials, (double*)workspace};
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, qcoords,
+                      qvalues, B, F, R, partials, (double*)workspace};
     hipError_t e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
     return NNGP_OK;
+}
+
+int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
+                  int32_t m, int64_t i0,
+                  int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
+                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
+    return bf_common(coords, n_points, coords, n_points, nbr, order, n_rows, m, i0, kind, sigma2, phi, tau2, values,
+                     values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
+}
+
+int nngp_bf_cross(const double* ref, int64_t n_ref, const double* query, int64_t n_query, const int32_t* nbr,
+                  const int32_t* order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind, double sigma2,
+                  double phi, double tau2, const double* ref_values, const double* query_values, double* B, double* F,
+                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
+    if (query_values != nullptr && ref_values == nullptr)
+        return fail(NNGP_EINVAL, "query_values need ref_values");
+    return bf_common(ref, n_ref, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, ref_values,
+                     query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
 int nngp_combine_partials(const double* gathered, int32_t world, double* partials, void* stream) {

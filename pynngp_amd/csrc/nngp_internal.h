@@ -38,6 +38,8 @@ struct BfArgs {
     double sigma2, phi, tau2;
     const int32_t* order;      // (n_rows,) local row of nbr row t (nngp_row_order layout), or null (identity)
     const double* values;      // (n_points,) or null
+    const double* qcoords;     // coordinates of the locations themselves: coords (sweep) or query points (cross)
+    const double* qvalues;     // values at the locations: values (sweep), query values or null (cross)
     double* B;                 // (n_rows, m) or null
     double* F;                 // (n_rows,) or null
     double* R;                 // (n_rows,) residuals v_i - B_i v_N(i), or null

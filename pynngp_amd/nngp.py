@@ -14,9 +14,15 @@ Differences from the reference, all deliberate:
   bug), but ``_Bsi/_Fsi/loglik`` need a :class:`Covariance` because the kernel
   fuses the covariance.  ``cov=None`` (the reference test) builds neighbour sets only.
 * exact distance ties are ordered by lower index (the reference's is arbitrary).
-* tuple ``refType`` values raise ``NotImplementedError`` (the reference raises
-  ``AttributeError`` at nngp.py:34); an unknown string raises ``ValueError``
-  (the reference silently leaves ``s`` unset, nngp.py:29-31).
+* tuple ``refType`` values work as the reference's comments describe
+  (nngp.py:23-27, with the same ``np.random`` calls as nngp.py:36-40, so a seeded
+  global RNG gives the S the reference meant to draw); the reference itself raises
+  ``AttributeError`` there (``self.typ``, nngp.py:34).  An unknown string raises
+  ``ValueError`` (the reference silently leaves ``s`` unset, nngp.py:29-31).
+* ``Nt`` for refType != 'S=T' is a list of int64 index arrays into ``s`` (the
+  reference appends ``(dist, ind)`` tuples, nngp.py:71, because ``return_distance``
+  defaults to True); ``predict()`` evaluates B_t, F_t and the kriging mean at t
+  (nngp_bf_cross).
 """
 from __future__ import annotations
 
@@ -105,20 +111,17 @@ class NNGP:
 
     # -- construction (nngp.py:21-71) -----------------------------------------
     def _init_s(self):
-        if isinstance(self.refType, str):
-            if self.refType != "S=T":
-                raise ValueError(f"unknown refType {self.refType!r} (only 'S=T' is a string option)")
-            self.s = self.t
-        elif isinstance(self.refType, tuple):
-            raise NotImplementedError(
-                "tuple refType ('subset', n) / ('random', n, bounds) is SURVEY.md 8(f) 'next' "
-                "(the reference raises AttributeError here, nngp.py:34)")
+        """Reference set S (nngp.py:21-40): 'S=T', ('subset', nRef) or ('random', nRef, bounds)."""
+        self.s = reference_set(self.t, self.refType)
+        self._t_dev = torch.as_tensor(np.ascontiguousarray(self.t, dtype=np.float64)).to(self.device)
+        if self._t_dev.dim() != 2 or self._t_dev.shape[1] != 2:
+            raise ValueError(f"ordinates must be (N, 2), got {tuple(self._t_dev.shape)}")
+        if self.s is self.t:
+            self._s_dev = self._t_dev
         else:
-            raise TypeError(f"refType must be 'S=T' or a tuple, got {type(self.refType).__name__}")
-        self._s_dev = torch.as_tensor(np.ascontiguousarray(self.s, dtype=np.float64)).to(self.device)
-        if self._s_dev.dim() != 2 or self._s_dev.shape[1] != 2:
-            raise ValueError(f"ordinates must be (N, 2), got {tuple(self._s_dev.shape)}")
-        self._t_dev = self._s_dev  # S=T
+            self._s_dev = torch.as_tensor(np.ascontiguousarray(self.s, dtype=np.float64)).to(self.device)
+            if self._s_dev.dim() != 2 or self._s_dev.shape[1] != 2 or self._s_dev.shape[0] < 1:
+                raise ValueError(f"reference set must be (nRef >= 1, 2), got {tuple(self._s_dev.shape)}")
 
     def _init_wt(self):
         self.wt = np.copy(self.y)
@@ -148,8 +151,18 @@ class NNGP:
         self._B = self._F = None
 
     def _make_t_neighbor_sets(self):
-        # 'S=T': Nt aliases Ns (nngp.py:65-67)
-        pass
+        """'S=T': Nt aliases Ns (nngp.py:65-67); otherwise the m nearest points of S to
+        every t (nngp.py:68-71), ascending, on the GPU (nngp_knn_query)."""
+        self._Nt = None
+        if self._same_sets():
+            self.nbr_t = None
+            return
+        k = min(self.m, self._s_dev.shape[0])
+        self.nbr_t = _lib.knn_query(self._s_dev, self._t_dev, k) if k > 0 else torch.empty(
+            (self._t_dev.shape[0], 0), dtype=torch.int32, device=self.device)
+
+    def _same_sets(self) -> bool:
+        return isinstance(self.refType, str) and self.refType == "S=T"
 
     @property
     def Ns(self):
@@ -164,7 +177,41 @@ class NNGP:
 
     @property
     def Nt(self):
-        return self.Ns
+        """'S=T': the same object as ``Ns``; otherwise one int64 index array into ``s`` per t."""
+        if self._same_sets():
+            return self.Ns
+        if self._Nt is None:
+            a = self.nbr_t.cpu().numpy().astype(np.int64)
+            self._Nt = [row for row in a]
+        return self._Nt
+
+    # -- prediction at t (SURVEY.md 8(f) row 2) ------------------------------
+    def predict(self, values=None, cov: Optional[Covariance] = None, query=None, algo: str = "auto"):
+        """Kriging of the NNGP at the points ``query`` (default ``t``) from ``values`` on S
+        (default ``ws``): returns numpy ``(mean, var)`` with mean_t = B_t v_N(t) and
+        var_t = F_t (conditional variance; includes tau2 like C_tt = sigma2 + tau2).
+        Neighbours: the m nearest points of S to each query point (for query = t with
+        refType != 'S=T' these are ``Nt``)."""
+        cv = cov if cov is not None else self._covariance()
+        v = self.ws if values is None else values
+        v = torch.as_tensor(np.asarray(v, dtype=np.float64) if not isinstance(v, torch.Tensor) else v,
+                            dtype=torch.float64).to(self.device)
+        if v.shape != (self._s_dev.shape[0],):
+            raise ValueError(f"values must have one entry per reference point ({self._s_dev.shape[0]})")
+        if query is None and not self._same_sets():
+            q, nbr = self._t_dev, self.nbr_t
+        else:
+            q = self._t_dev if query is None else torch.as_tensor(
+                np.ascontiguousarray(query, dtype=np.float64)).to(self.device)
+            k = min(self.m, self._s_dev.shape[0])
+            nbr = _lib.knn_query(self._s_dev, q, k)
+        n = q.shape[0]
+        if nbr.shape[1] == 0:  # m = 0: the marginal
+            return np.zeros(n), np.full(n, cv.sigma2 + cv.tau2)
+        R = torch.empty(n, dtype=torch.float64, device=self.device)
+        _, F, p = _lib.bf_cross(self._s_dev, q, nbr, cv.kind, *cv.theta, ref_values=v, algo=algo, R=R)
+        _raise_on_bad(p.cpu().numpy())
+        return (-R).cpu().numpy(), F.cpu().numpy()
 
     # -- covariance plumbing ---------------------------------------------------
     def _covariance(self) -> Covariance:
@@ -257,6 +304,29 @@ class NNGP:
     def oneSample(self):
         """Gibbs sweep (nngp.py:98-101 calls methods that do not exist): SURVEY.md 8(f) 'next'."""
         raise NotImplementedError("the Gibbs sweep is SURVEY.md 8(f) 'next' (the reference has no implementation)")
+
+
+def reference_set(t, refType):
+    """S for a refType (nngp.py:21-40).  The tuple forms draw from numpy's global RNG with
+    the reference's own calls: ('subset', nRef) -> t[np.random.choice(len(t), size=nRef)]
+    (with replacement, as nngp.py:36); ('random', nRef, bounds) -> one
+    np.random.uniform(lo, hi, nRef) column per (lo, hi) in bounds (nngp.py:39-40)."""
+    if isinstance(refType, str):
+        if refType != "S=T":
+            raise ValueError(f"unknown refType {refType!r} (only 'S=T' is a string option)")
+        return t
+    if isinstance(refType, tuple) and len(refType) >= 2:
+        typ = refType[0]
+        if typ == "subset":
+            choice = np.random.choice(len(t), size=int(refType[1]))
+            return np.asarray(t)[choice]
+        if typ == "random":
+            if len(refType) < 3:
+                raise ValueError("('random', nRef, bounds) needs bounds")
+            nRef, bounds = int(refType[1]), refType[2]
+            return np.vstack([np.random.uniform(lo, hi, nRef) for lo, hi in bounds]).T
+        raise ValueError(f"unknown refType kind {typ!r} (expected 'subset' or 'random')")
+    raise TypeError(f"refType must be 'S=T' or a tuple, got {refType!r}")
 
 
 class NNGPNumericalError(ArithmeticError):

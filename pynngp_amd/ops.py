@@ -8,6 +8,7 @@ Fake (meta) kernels give shapes for tracing.
         -> (B, F, partials)
     torch.ops.nngp.knn_prior(coords, m, q0, q1) -> nbr
     torch.ops.nngp.knn_query(ref, query, k) -> nbr
+    torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo) -> (B, F, mean)
 """
 from __future__ import annotations
 
@@ -58,6 +59,24 @@ def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
 @knn_query.register_fake
 def _(ref, query, k):
     return query.new_empty((query.shape[0], k), dtype=torch.int32)
+
+
+@torch.library.custom_op("nngp::bf_cross", mutates_args=(), device_types="cuda")
+def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: int, sigma2: float, phi: float,
+             tau2: float, ref_values: Optional[torch.Tensor], algo: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """B_t, F_t against the reference set and the kriging mean B_t v_N(t) (zeros without ref_values)."""
+    rows = nbr.shape[0]
+    R = torch.empty((rows,), dtype=torch.float64, device=query.device) if ref_values is not None else None
+    B, F, _ = _lib.bf_cross(ref, query, nbr, _KINDS[kind], sigma2, phi, tau2, ref_values=ref_values,
+                            algo=_ALGOS[algo], R=R)
+    mean = -R if R is not None else torch.zeros((rows,), dtype=torch.float64, device=query.device)
+    return B, F, mean
+
+
+@bf_cross.register_fake
+def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo):
+    rows, m = nbr.shape
+    return query.new_empty((rows, m)), query.new_empty((rows,)), query.new_empty((rows,))
 
 
 def kind_code(kind: str) -> int:

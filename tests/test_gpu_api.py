@@ -89,8 +89,8 @@ def test_callable_cov_and_errors(dev):
         model._Bsi(10)
     with pytest.raises(NotImplementedError):
         model.oneSample()
-    with pytest.raises(NotImplementedError):
-        NNGP(t, y, None, ("subset", 10), 4, None)
+    with pytest.raises(ValueError):
+        NNGP(t, y, None, ("grid", 10), 4, None)
     with pytest.raises(ValueError):
         NNGP(t, y, None, "S=X", 4, None)
     dup = t.copy()
