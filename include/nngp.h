@@ -167,11 +167,17 @@ int nngp_combine_partials(const double *gathered, int32_t world, double *partial
  * nngp_color_moral_graph (HOST pointers, host computation): greedy colouring
  *   of the moral graph (i ~ N(i); co-parents of a child ~ each other) in index
  *   order; returns the number of colours (or a negative NNGP_E* code).
+ * nngp_gibbs_prepare: fold the factors of the unit-variance field (sigma2 = 1,
+ *   tau2 = 0; B (n, m) and Ft (n,) from nngp_bf_sweep) into reverse-list order for
+ *   the w sweeps: B_{j,i} and B_{j,i}/F_j per reverse entry, sum_e B_{j,i}^2/F_j and
+ *   1/F_i per location, into `prep` (device, nngp_gibbs_prep_bytes(n, m) bytes,
+ *   256-B aligned).  Call it again whenever B / Ft change (a new phi accepted).
+ *   order: NULL or a permutation of 0..n-1 to visit the locations in (speed only;
+ *   nngp_row_order's Z-order keeps the gathers in L2).
  * nngp_gibbs_w_sweep: one sweep of w_i | rest over the colours in order;
  *   `members` (device) lists the locations grouped by colour, color_off_host
- *   (host, n_colors + 1) delimits them.  B (n, m) and Ft (n,) are the factors of
- *   the unit-variance field (sigma2 = 1, tau2 = 0) from nngp_bf_sweep; r (n,) the
- *   residuals w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
+ *   (host, n_colors + 1) delimits them.  r (n,) holds the residuals
+ *   w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
  *   yres = y - X beta.  z: NULL (Philox4x32-10 normals keyed by seed, counter
  *   (location, sweep)) or n given standard normals (for testing).
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum (yres_i - w_i)^2,
@@ -182,10 +188,14 @@ int nngp_reverse_neighbors(const int32_t *nbr, int64_t n, int32_t m, int32_t *of
                            void *workspace, size_t workspace_bytes, void *stream);
 int64_t nngp_color_moral_graph(const int32_t *nbr_host, const int32_t *off_host, const int32_t *rev_j_host,
                                int64_t n, int32_t m, int32_t *color_host);
-int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, int32_t n_colors, const double *B,
-                       const double *Ft, double sigma2, double tau2, const double *yres, double *w, double *r,
-                       const int32_t *off, const int32_t *rev_j, const int32_t *rev_k, int32_t m, const double *z,
-                       uint64_t seed, uint64_t sweep, void *stream);
+size_t nngp_gibbs_prep_bytes(int64_t n, int32_t m);
+int nngp_gibbs_prepare(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
+                       const int32_t *rev_k, const int32_t *order, int64_t n, int32_t m, void *prep,
+                       size_t prep_bytes, void *stream);
+int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, int32_t n_colors, const void *prep,
+                       int64_t n, int32_t m, double sigma2, double tau2, const double *yres, double *w, double *r,
+                       const int32_t *off, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
+                       void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
                      const double *X, int32_t p, const double *w, double *out, void *workspace,

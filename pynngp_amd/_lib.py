@@ -32,6 +32,8 @@ SYMBOLS = (
     "nngp_reverse_workspace_bytes",
     "nngp_reverse_neighbors",
     "nngp_color_moral_graph",
+    "nngp_gibbs_prep_bytes",
+    "nngp_gibbs_prepare",
     "nngp_gibbs_w_sweep",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
@@ -87,7 +89,11 @@ def load() -> ctypes.CDLL:
     lib.nngp_reverse_neighbors.restype = ctypes.c_int
     lib.nngp_color_moral_graph.argtypes = [P, P, P, I64, I32, P]
     lib.nngp_color_moral_graph.restype = I64
-    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, P, D, D, P, P, P, P, P, P, I32, P, U64, U64, P]
+    lib.nngp_gibbs_prep_bytes.argtypes = [I64, I32]
+    lib.nngp_gibbs_prep_bytes.restype = SZ
+    lib.nngp_gibbs_prepare.argtypes = [P, P, P, P, P, P, I64, I32, P, SZ, P]
+    lib.nngp_gibbs_prepare.restype = ctypes.c_int
+    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P]
     lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
     lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]
     lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
@@ -367,19 +373,36 @@ def color_moral_graph(nbr_host, off_host, rev_j_host):
     return colors, int(nc)
 
 
-def gibbs_w_sweep(members: torch.Tensor, color_off_host, B: torch.Tensor, Ft: torch.Tensor, sigma2: float,
+def gibbs_prepare(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor, rev_k: torch.Tensor,
+                  prep: Optional[torch.Tensor] = None, order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fold the unit-variance factors (B, Ft) into the reverse-list layout the w sweeps read
+    (nngp_gibbs_prepare); returns the device buffer to pass to :func:`gibbs_w_sweep`."""
+    dev = _require_gpu(B, Ft, off, rev_j, rev_k, prep, order)
+    n, m = B.shape
+    if order is not None and (order.dtype != torch.int32 or order.shape != (n,)):
+        raise ValueError("order must be int32 (n,)")
+    lib = load()
+    need = lib.nngp_gibbs_prep_bytes(n, m)
+    if prep is None or prep.numel() < need:
+        prep = _workspace(need, dev)
+    _check(lib.nngp_gibbs_prepare(_ptr(B), _ptr(Ft), _ptr(off), _ptr(rev_j), _ptr(rev_k), _ptr(order), n, m, _ptr(prep),
+                                  prep.numel(), _stream(dev)), "nngp_gibbs_prepare")
+    return prep
+
+
+def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: int, sigma2: float,
                   tau2: float, yres: torch.Tensor, w: torch.Tensor, r: torch.Tensor, off: torch.Tensor,
-                  rev_j: torch.Tensor, rev_k: torch.Tensor, seed: int, sweep: int,
-                  z: Optional[torch.Tensor] = None) -> None:
-    """One colour-ordered sweep of w_i | rest, in place on w and r (see include/nngp.h)."""
+                  rev_j: torch.Tensor, seed: int, sweep: int, z: Optional[torch.Tensor] = None) -> None:
+    """One colour-ordered sweep of w_i | rest, in place on w and r (see include/nngp.h);
+    ``prep`` from :func:`gibbs_prepare` for the current B / Ft."""
     import numpy as np
 
-    dev = _require_gpu(members, B, Ft, yres, w, r, off, rev_j, rev_k, z)
+    dev = _require_gpu(members, prep, yres, w, r, off, rev_j, z)
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
-    m = B.shape[1]
-    _check(load().nngp_gibbs_w_sweep(_ptr(members), co.ctypes.data, len(co) - 1, _ptr(B), _ptr(Ft), float(sigma2),
-                                     float(tau2), _ptr(yres), _ptr(w), _ptr(r), _ptr(off), _ptr(rev_j), _ptr(rev_k),
-                                     m, _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
+    n = w.shape[0]
+    _check(load().nngp_gibbs_w_sweep(_ptr(members), co.ctypes.data, len(co) - 1, _ptr(prep), n, int(m),
+                                     float(sigma2), float(tau2), _ptr(yres), _ptr(w), _ptr(r), _ptr(off), _ptr(rev_j),
+                                     _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
 
 

@@ -157,18 +157,39 @@ int64_t nngp_color_moral_graph(const int32_t* nbr, const int32_t* off, const int
     return nngp::color_moral_graph_host(nbr, off, rev_j, n, m, color);
 }
 
-int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, int32_t n_colors, const double* B,
-                       const double* Ft, double sigma2, double tau2, const double* yres, double* w, double* r,
-                       const int32_t* off, const int32_t* rev_j, const int32_t* rev_k, int32_t m, const double* z,
-                       uint64_t seed, uint64_t sweep, void* stream) {
-    if (members == nullptr || color_off_host == nullptr || Ft == nullptr || yres == nullptr || w == nullptr ||
-        r == nullptr || off == nullptr || (m > 0 && (B == nullptr || rev_j == nullptr || rev_k == nullptr)))
+size_t nngp_gibbs_prep_bytes(int64_t n, int32_t m) {
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return 0;
+    return nngp::gibbs_prep_bytes(n, m);
+}
+
+int nngp_gibbs_prepare(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                       const int32_t* rev_k, const int32_t* order, int64_t n, int32_t m, void* prep,
+                       size_t prep_bytes, void* stream) {
+    if (Ft == nullptr || off == nullptr || prep == nullptr || (m > 0 && (B == nullptr || rev_j == nullptr ||
+                                                                          rev_k == nullptr)))
         return fail(NNGP_EINVAL, "null pointer argument");
-    if (n_colors < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors or m");
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n or m");
+    if (((uintptr_t)prep & 255) != 0) return fail(NNGP_EINVAL, "prep must be 256-byte aligned");
+    if (prep_bytes < nngp::gibbs_prep_bytes(n, m))
+        return fail(NNGP_EINVAL, "prep too small: %zu < %zu bytes", prep_bytes, nngp::gibbs_prep_bytes(n, m));
+    hipError_t e = nngp::gibbs_prepare_launch(B, Ft, off, rev_j, rev_k, order, n, m, prep, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_prepare launch");
+    return NNGP_OK;
+}
+
+int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, int32_t n_colors, const void* prep,
+                       int64_t n, int32_t m, double sigma2, double tau2, const double* yres, double* w, double* r,
+                       const int32_t* off, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
+                       void* stream) {
+    if (members == nullptr || color_off_host == nullptr || prep == nullptr || yres == nullptr || w == nullptr ||
+        r == nullptr || off == nullptr || (m > 0 && rev_j == nullptr))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
+    if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
     if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
-    hipError_t e = nngp::gibbs_w_sweep_launch(nullptr, members, n_colors, color_off_host, B, Ft, sigma2, tau2, yres,
-                                              w, r, off, rev_j, rev_k, m, z, seed, sweep, (hipStream_t)stream);
+    hipError_t e = nngp::gibbs_w_sweep_launch(members, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres, w, r,
+                                              off, rev_j, z, seed, sweep, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
     return NNGP_OK;
 }

@@ -148,7 +148,9 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
     std::vector<int64_t> stamp(1024, -1);
     int32_t n_colors = 0;
     for (int64_t i = 0; i < n; ++i) {
-        // mark colours of already-coloured moral neighbours: parents N(i), and co-parents k < i of children j
+        // mark colours of already-coloured (index < i) moral neighbours: parents N(i), children j
+        // (earlier than i only when the locations were relabelled, e.g. into a spatial storage
+        // order) and co-parents of children
         auto mark = [&](int32_t k) {
             if (k >= 0 && k < i) {
                 const int32_t c = color[k];
@@ -160,6 +162,7 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
         for (int s = 0; s < m; ++s) mark(row[s]);
         for (int32_t e = off[i]; e < off[i + 1]; ++e) {
             const int64_t j = rev_j[e];
+            mark((int32_t)j);
             const int32_t* rj = nbr + j * m;
             for (int s = 0; s < m; ++s)
                 if (rj[s] != i) mark(rj[s]);
@@ -173,55 +176,137 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
     return n_colors;
 }
 
+// ---------------------------------------------------------------- per-phi preparation
+// Everything of the w full conditionals that depends on B / F only (i.e. changes only
+// when a new phi is accepted) is folded once into reverse-list order:
+//   Brev[e] = B_{j,i},  Grev[e] = B_{j,i} / F_j   (e in [off[i], off[i+1]), j = rev_j[e])
+//   P[i]    = sum_e B_{j,i}^2 / F_j,  invF[i] = 1 / F_i
+// so that, with s2 = sigma2 (F here is the unit-variance field's),
+//   prec_i = 1/tau2 + (invF_i + P_i) / s2
+//   lin_i  = yres_i / tau2 + [(w_i - r_i) invF_i + w_i P_i + sum_e Grev[e] r_j] / s2
+// and a colour step reads one streamed double and one gathered r_j per child.
+// kGroup lanes per location (as the colour kernel): the lanes split the reverse entries
+// (contiguous stores per round), a fixed xor-butterfly sums P_i.
+constexpr int kGroup = 8;
+
+__global__ __launch_bounds__(256) void gibbs_prepare_kernel(const double* __restrict__ B, const double* __restrict__ Ft,
+                                                            const int32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ rev_j,
+                                                            const int32_t* __restrict__ rev_k,
+                                                            const int32_t* __restrict__ order, int64_t n, int m,
+                                                            double* __restrict__ Brev, double* __restrict__ Grev,
+                                                            double* __restrict__ P, double* __restrict__ invF) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = t / kGroup;
+    const int l = (int)(t % kGroup);
+    const bool live = g < n;
+    const int64_t gc = live ? g : n - 1;
+    // visiting order (speed only): with a spatial order, consecutive locations share
+    // children, so the B / Ft gathers of a block hit L2
+    const int64_t i = order != nullptr ? (int64_t)order[gc] : gc;
+    const int32_t e0 = off[i], e1 = live ? off[i + 1] : off[i];
+    double acc = 0.0;
+    for (int32_t e = e0 + l; e < e1; e += kGroup) {
+        const int64_t j = rev_j[e];
+        const double b = B[j * m + rev_k[e]];
+        const double g = b / Ft[j];
+        Brev[e] = b;
+        Grev[e] = g;
+        acc = fma(b, g, acc);
+    }
+#pragma unroll
+    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (live && l == 0) {
+        P[i] = acc;
+        invF[i] = 1.0 / Ft[i];
+    }
+}
+
+struct GibbsPrep {
+    double *Brev, *Grev, *P, *invF;
+};
+
+static GibbsPrep prep_layout(void* prep, int64_t n, int m) {
+    char* w = (char*)prep;
+    GibbsPrep g;
+    g.Brev = (double*)w;
+    w += align256((size_t)(n * m) * 8);
+    g.Grev = (double*)w;
+    w += align256((size_t)(n * m) * 8);
+    g.P = (double*)w;
+    w += align256((size_t)n * 8);
+    g.invF = (double*)w;
+    return g;
+}
+
+size_t gibbs_prep_bytes(int64_t n, int m) {
+    return 2 * align256((size_t)(n * m) * 8) + 2 * align256((size_t)n * 8);
+}
+
+hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                                const int32_t* rev_k, const int32_t* order, int64_t n, int m, void* prep,
+                                hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const GibbsPrep g = prep_layout(prep, n, m);
+    hipLaunchKernelGGL(gibbs_prepare_kernel, dim3((unsigned)((n * kGroup + 255) / 256)), dim3(256), 0, s, B, Ft,
+                       off, rev_j, rev_k, order, n, m, g.Brev, g.Grev, g.P, g.invF);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- colour update
+// kGroup lanes per location: the lanes split its children (reverse entries), a
+// fixed xor-butterfly sums their sum_e Grev[e] r_j, and every lane of the group then
+// evaluates the same full conditional and the same Philox normal (no broadcast
+// needed; lane 0 writes w_i, r_i), and the lanes scatter r_j -= B_{j,i} dw to their
+// children.  Race-free within a colour (moral-graph colouring: no two members share a
+// child, and no member is another's child).
+
 __global__ __launch_bounds__(256) void gibbs_w_color(const int32_t* __restrict__ members, int64_t n_members,
-                                                     const double* __restrict__ B, const double* __restrict__ Ft,
-                                                     double sigma2, double tau2, const double* __restrict__ yres,
+                                                     const double* __restrict__ Brev, const double* __restrict__ Grev,
+                                                     const double* __restrict__ P, const double* __restrict__ invF,
+                                                     double it2, double is2, const double* __restrict__ yres,
                                                      double* __restrict__ w, double* __restrict__ r,
                                                      const int32_t* __restrict__ off, const int32_t* __restrict__ rev_j,
-                                                     const int32_t* __restrict__ rev_k, int m,
                                                      const double* __restrict__ z, uint64_t seed, uint64_t sweep) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_members) return;
-    const int64_t i = members[t];
-    const double wi = w[i], ri = r[i];
-    const double it2 = 1.0 / tau2, is2 = 1.0 / sigma2;
-    const double iFi = is2 / Ft[i];
-    double prec = it2 + iFi;
-    double lin = fma(yres[i], it2, (wi - ri) * iFi);
-    const int32_t e0 = off[i], e1 = off[i + 1];
-    for (int32_t e = e0; e < e1; ++e) {
-        const int64_t j = rev_j[e];
-        const double bji = B[j * m + rev_k[e]];
-        const double iFj = is2 / Ft[j];
-        const double sj = fma(bji, wi, r[j]);
-        prec = fma(bji * bji, iFj, prec);
-        lin = fma(bji * sj, iFj, lin);
-    }
+    const int64_t g = t / kGroup;
+    const int l = (int)(t % kGroup);
+    const bool live = g < n_members;
+    const int64_t i = members[live ? g : n_members - 1];
+    const int32_t e0 = off[i], e1 = live ? off[i + 1] : off[i];
+    double acc = 0.0;
+    for (int32_t e = e0 + l; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
+#pragma unroll
+    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i];
+    const double prec = fma(iF + Pi, is2, it2);
+    const double lin = fma(yres[i], it2, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
     const double zi = z != nullptr ? z[i] : philox_normal(seed, (uint64_t)i, sweep);
     const double sd = nngp_rsqrt(prec);
     const double wn = fma(zi, sd, lin / prec);
     const double dw = wn - wi;
-    w[i] = wn;
-    r[i] = ri + dw;
-    for (int32_t e = e0; e < e1; ++e) {
+    if (live && l == 0) {
+        w[i] = wn;
+        r[i] = ri + dw;
+    }
+    for (int32_t e = e0 + l; e < e1; e += kGroup) {
         const int64_t j = rev_j[e];
-        const double bji = B[j * m + rev_k[e]];
-        r[j] = fma(-bji, dw, r[j]);
+        r[j] = fma(-Brev[e], dw, r[j]);
     }
 }
 
-hipError_t gibbs_w_sweep_launch(const int32_t* color_off, const int32_t* members_all, int n_colors,
-                                const int32_t* color_off_host, const double* B, const double* Ft, double sigma2,
-                                double tau2, const double* yres, double* w, double* r, const int32_t* off,
-                                const int32_t* rev_j, const int32_t* rev_k, int m, const double* z, uint64_t seed,
-                                uint64_t sweep, hipStream_t s) {
-    (void)color_off;
+hipError_t gibbs_w_sweep_launch(const int32_t* members_all, int n_colors, const int32_t* color_off_host,
+                                const void* prep, int64_t n, int m, double sigma2, double tau2,
+                                const double* yres, double* w, double* r, const int32_t* off, const int32_t* rev_j,
+                                const double* z, uint64_t seed, uint64_t sweep, hipStream_t s) {
+    const GibbsPrep g = prep_layout((void*)prep, n, m);
     for (int c = 0; c < n_colors; ++c) {
         const int64_t a = color_off_host[c], b = color_off_host[c + 1];
         if (b <= a) continue;
-        hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((b - a + 255) / 256)), dim3(256), 0, s, members_all + a,
-                           b - a, B, Ft, sigma2, tau2, yres, w, r, off, rev_j, rev_k, m, z, seed, sweep);
+        const int64_t threads = (b - a) * kGroup;
+        hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, members_all + a,
+                           b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres, w, r, off, rev_j, z,
+                           seed, sweep);
     }
     return hipGetLastError();
 }
@@ -261,13 +346,24 @@ __global__ __launch_bounds__(256) void gibbs_stats_blocks(int64_t n, const doubl
     }
 }
 
-__global__ __launch_bounds__(64) void gibbs_stats_fold(const double* __restrict__ rec, int64_t nb, int nv,
-                                                       double* __restrict__ out) {
-    const int v = threadIdx.x;
-    if (v >= nv) return;
-    double a = 0.0;
-    for (int64_t b = 0; b < nb; ++b) a += rec[b * nv + v];
-    out[v] = a;
+__global__ __launch_bounds__(1024) void gibbs_stats_fold(const double* __restrict__ rec, int64_t nb, int nv,
+                                                         double* __restrict__ out) {
+    // fixed order: thread t folds records t, t + 1024, ...; xor-butterfly per wave; 16 waves in order
+    __shared__ double sh[16];
+    const int t = threadIdx.x;
+    for (int v = 0; v < nv; ++v) {
+        double a = 0.0;
+        for (int64_t b = t; b < nb; b += 1024) a += rec[b * nv + v];
+        a = wave_sum(a);
+        if ((t & 63) == 0) sh[t >> 6] = a;
+        __syncthreads();
+        if (t == 0) {
+            double x = 0.0;
+            for (int k = 0; k < 16; ++k) x += sh[k];
+            out[v] = x;
+        }
+        __syncthreads();
+    }
 }
 
 size_t gibbs_stats_workspace_bytes(int64_t n, int p) { return align256((size_t)((n + 255) / 256) * (2 + p) * 8); }
@@ -278,7 +374,7 @@ hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, cons
     if (nb == 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gibbs_stats_blocks, dim3((unsigned)nb), dim3(256), 0, s, n, r, Ft, yres, y, X, p, w,
                        (double*)workspace);
-    hipLaunchKernelGGL(gibbs_stats_fold, dim3(1), dim3(64), 0, s, (const double*)workspace, nb, 2 + p, out);
+    hipLaunchKernelGGL(gibbs_stats_fold, dim3(1), dim3(1024), 0, s, (const double*)workspace, nb, 2 + p, out);
     return hipGetLastError();
 }
 

@@ -80,11 +80,14 @@ hipError_t reverse_launch(const int32_t* nbr, int64_t n, int m, int32_t* off, in
                           void* workspace, hipStream_t s);
 int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
                                int32_t* color);
-hipError_t gibbs_w_sweep_launch(const int32_t* color_off, const int32_t* members_all, int n_colors,
-                                const int32_t* color_off_host, const double* B, const double* Ft, double sigma2,
-                                double tau2, const double* yres, double* w, double* r, const int32_t* off,
-                                const int32_t* rev_j, const int32_t* rev_k, int m, const double* z, uint64_t seed,
-                                uint64_t sweep, hipStream_t s);
+size_t gibbs_prep_bytes(int64_t n, int m);
+hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                                const int32_t* rev_k, const int32_t* order, int64_t n, int m, void* prep,
+                                hipStream_t s);
+hipError_t gibbs_w_sweep_launch(const int32_t* members_all, int n_colors, const int32_t* color_off_host,
+                                const void* prep, int64_t n, int m, double sigma2, double tau2,
+                                const double* yres, double* w, double* r, const int32_t* off, const int32_t* rev_j,
+                                const double* z, uint64_t seed, uint64_t sweep, hipStream_t s);
 size_t gibbs_stats_workspace_bytes(int64_t n, int p);
 hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
                               const double* X, int p, const double* w, double* out, void* workspace, hipStream_t s);

@@ -54,3 +54,21 @@ def test_colour_sweep_invariant_law():
     C = np.stack([G.color_sweep(P, b, np.zeros(n), colors, e) - d for e in np.eye(n)], 1)
     np.testing.assert_allclose(A @ mu + d, mu, rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(A @ S @ A.T + C @ C.T, S, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,m", [(300, 4), (2000, 10)])
+def test_colouring_after_relabelling(c_oracle, n, m):
+    """SeqNNGP relabels locations into a spatial storage order, after which a child can
+    precede its parents: the greedy colouring must still be proper."""
+    from pynngp_amd import _lib
+
+    rng = np.random.default_rng(7 + n)
+    nbr0 = c_oracle.c_knn_prior(rng.uniform(size=(n, 2)), m)
+    perm = rng.permutation(n)
+    pos = np.empty(n, np.int64)
+    pos[perm] = np.arange(n)
+    nb = nbr0[perm]
+    nbr = np.where(nb >= 0, pos[np.maximum(nb, 0)], -1).astype(np.int32)
+    off, rev_j = _reverse(nbr)
+    colors, nc = _lib.color_moral_graph(nbr, off, rev_j)
+    assert G.coloring_is_valid(nbr, colors)

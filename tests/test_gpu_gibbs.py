@@ -75,8 +75,9 @@ def test_w_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2):
     b = yres.cpu().numpy() / tau2
     w_ref = G.color_sweep(P, b, w0, s["colors"], z.cpu().numpy())
     w, r = s["w"].clone(), s["R"].clone()
-    _lib.gibbs_w_sweep(s["members"], s["color_off"], s["B"], s["F"], sigma2, tau2, yres, w, r, s["off"],
-                       s["rev_j"], s["rev_k"], 123, 0, z=z)
+    prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
+    _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, sigma2, tau2, yres, w, r, s["off"], s["rev_j"], 123, 0,
+                       z=z)
     wh = w.cpu().numpy()
     np.testing.assert_allclose(wh, w_ref, rtol=1e-9, atol=1e-9 * np.abs(w_ref).max())
     # maintained residuals equal the recomputed ones
@@ -98,9 +99,9 @@ def test_w_sweep_stationary_law(dev):
     w, r = s["w"].clone(), s["R"].clone()
     draws = []
     n_sweeps = 20000
+    prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
     for t in range(n_sweeps):
-        _lib.gibbs_w_sweep(s["members"], s["color_off"], s["B"], s["F"], sigma2, tau2, yres, w, r, s["off"],
-                           s["rev_j"], s["rev_k"], 99, t)
+        _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, sigma2, tau2, yres, w, r, s["off"], s["rev_j"], 99, t)
         if t >= 100:
             draws.append(w.clone())
     W = torch.stack(draws).cpu().numpy()
@@ -130,8 +131,9 @@ def test_philox_normals_moments(dev):
     B, F, _ = _lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 3.0, 0.0, values=w, R=R)
     off, rev_j, rev_k = _lib.reverse_neighbors(nbr)
     members = torch.arange(n, dtype=torch.int32, device=dev)
-    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), B, F, 1.0, 1e300, torch.zeros_like(w), w, R, off, rev_j,
-                       rev_k, 5, 0)
+    prep = _lib.gibbs_prepare(B, F, off, rev_j, rev_k)
+    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), prep, 0, 1.0, 1e300, torch.zeros_like(w), w, R, off,
+                       rev_j, 5, 0)
     z = w.cpu().numpy()
     assert abs(z.mean()) < 5 / np.sqrt(n)
     assert abs(z.var() - 1) < 5 * np.sqrt(2 / n)
@@ -140,8 +142,8 @@ def test_philox_normals_moments(dev):
     # different sweep counter -> independent stream (r back to w - B w_N = 0)
     w2 = torch.zeros_like(w)
     R.zero_()
-    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), B, F, 1.0, 1e300, torch.zeros_like(w), w2, R, off, rev_j,
-                       rev_k, 5, 1)
+    _lib.gibbs_w_sweep(members, np.array([0, n], np.int32), prep, 0, 1.0, 1e300, torch.zeros_like(w), w2, R, off,
+                       rev_j, 5, 1)
     assert abs(np.corrcoef(z, w2.cpu().numpy())[0, 1]) < 5 / np.sqrt(n)
 
 

@@ -1,0 +1,46 @@
+"""Gibbs sampler timing (BASELINE.json configs[4]: 1,000 sweeps at N=1M, m=15; here one GPU).
+
+One iteration = SeqNNGP.step(): MH proposal for phi (one fused B/F sweep + residuals),
+conjugate sigma2, the colour-ordered w sweep, tau2 and beta draws (host scalars).
+Synthetic response data y = 1 + w + eps from the seed; prints one JSON line.
+    python tools/bench_gibbs.py [--n 1000000 --m 15 --iters 50 --warmup 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pynngp_amd import SeqNNGP  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=1_000_000)
+ap.add_argument("--m", type=int, default=15)
+ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--warmup", type=int, default=5)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+rng = np.random.default_rng(2)
+coords = rng.uniform(0, 1, (args.n, 2))
+y = 1.0 + rng.standard_normal(args.n) * 0.5 + 0.3 * rng.standard_normal(args.n)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev)
+torch.cuda.synchronize()
+setup_s = time.perf_counter() - t0
+for _ in range(args.warmup):
+    g.step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(args.iters):
+    g.step()
+torch.cuda.synchronize()
+el = time.perf_counter() - t0
+print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, 1 GPU",
+                  "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
+                  "locations_per_s": args.n * args.iters / el, "setup_s": setup_s, "n_colors": int(g.n_colors),
+                  "phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "accept": g.n_accept / max(1, g.iteration)}))
