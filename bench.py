@@ -113,7 +113,9 @@ def main():
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
     ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad", "pairb"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
-    ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order)")
+    ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order; natural layout)")
+    ap.add_argument("--layout", default="storage", choices=["storage", "natural"],
+                    help="storage: per-location arrays relabelled into Z-order storage (default); natural: input rows")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
@@ -139,14 +141,21 @@ def main():
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order)
+    sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order,
+                          layout=args.layout)
+    if args.layout == "storage":
+        # the synthetic field lives in the engine's storage order (an MCMC state would);
+        # same iid N(0,1) values, assigned to locations in storage order
+        v_sweep, v_layout = v, "storage"
+    else:
+        v_sweep, v_layout = v, "input"
     torch.cuda.synchronize()
     knn_s = time.perf_counter() - t0
     want_bf = not args.loglik_only
     rows = sweep.hi - sweep.lo
 
     for _ in range(args.warmup):
-        sweep.partials(cov, v, want_bf)
+        sweep.partials(cov, v_sweep, want_bf, v_layout)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -155,7 +164,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        local = sweep.local_partials(cov, v, want_bf)
+        local = sweep.local_partials(cov, v_sweep, want_bf, v_layout)
         ev[k][1].record(stream)
         combine_partials(local, world)
     torch.cuda.synchronize()
@@ -167,7 +176,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    p = sweep.partials(cov, v, want_bf).cpu().numpy()
+    p = sweep.partials(cov, v_sweep, want_bf, v_layout).cpu().numpy()
     ll = -0.5 * (n_total * np.log(2 * np.pi) + p[0] + p[1])
 
     if rank == 0:
@@ -188,7 +197,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: uniform [0,1]^2 coords + N(0,1) values, numpy default_rng(0)",
+            "data": "synthetic: uniform [0,1]^2 coords + N(0,1) values, numpy default_rng(0)" + (
+                "; values resident in the engine's Z-order storage layout" if args.layout == "storage" else ""),
             "config": {
                 "workload": "BASELINE config 3: fused B/F + log-lik sweep, N=1,000,000 locations per GPU, m=15, "
                             "exponential covariance" if (args.n == 1_000_000 and args.m == 15
@@ -201,6 +211,7 @@ def main():
                 "theta": [sigma2, phi, tau2],
                 "algo": args.algo,
                 "row_order": "index" if args.no_order else "z-order",
+                "layout": args.layout,
                 "write_BF": want_bf,
                 "global_batch": n_total,
                 "parallelism": f"dp{world} (contiguous location shards, all-gather of 4 partials per sweep)",
@@ -230,10 +241,11 @@ def main():
         }
         if world == 1 and args.cpu_seconds > 0:
             F_gpu = sweep.F.cpu().numpy() if want_bf else None
+            c_sw = sweep._coords_sweep  # storage- or input-order coordinates the rows / nbr refer to
             if F_gpu is None:
-                _, F_t, _ = _lib.bf_sweep(c, sweep.nbr, 0, cov.kind, *cov.theta)
+                _, F_t, _ = _lib.bf_sweep(c_sw, sweep.nbr, 0, cov.kind, *cov.theta)
                 F_gpu = F_t.cpu().numpy()
-            out["cpu_baseline"] = cpu_baseline(coords, values, sweep.nbr.cpu().numpy(), args.kind,
+            out["cpu_baseline"] = cpu_baseline(c_sw.cpu().numpy(), values, sweep.nbr.cpu().numpy(), args.kind,
                                                (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

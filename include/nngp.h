@@ -67,6 +67,13 @@ size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m);
 int nngp_knn_prior(const double *coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t *nbr,
                    void *workspace, size_t workspace_bytes, void *stream);
 
+/* Same neighbour sets for an arbitrary list of locations: query row t is point rows[t]
+ * (its min(m, rows[t]) nearest among coords[0:rows[t]]), written to nbr[t * m + s].
+ * Used to build a shard's sets when the shard is a range of a spatial storage order
+ * (pynngp_amd.sweep.ShardedLogLik, layout "storage").  Workspace as nngp_knn_prior. */
+int nngp_knn_prior_rows(const double *coords, int64_t n_points, int32_t m, const int32_t *rows, int64_t n_rows,
+                        int32_t *nbr, void *workspace, size_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Unrestricted k-nearest neighbours of query points among a reference set.
  * Replaces the sklearn searches behind NNGP._init_ws (pyNNGP/nngp.py:45-47,

@@ -21,6 +21,7 @@ SYMBOLS = (
     "nngp_last_error",
     "nngp_knn_workspace_bytes",
     "nngp_knn_prior",
+    "nngp_knn_prior_rows",
     "nngp_knn_query",
     "nngp_bf_sweep_workspace_bytes",
     "nngp_bf_sweep",
@@ -69,6 +70,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_knn_workspace_bytes.restype = SZ
     lib.nngp_knn_prior.argtypes = [P, I64, I32, I64, I64, P, P, SZ, P]
     lib.nngp_knn_prior.restype = ctypes.c_int
+    lib.nngp_knn_prior_rows.argtypes = [P, I64, I32, P, I64, P, P, SZ, P]
+    lib.nngp_knn_prior_rows.restype = ctypes.c_int
     lib.nngp_knn_query.argtypes = [P, I64, P, I64, I32, P, P, SZ, P]
     lib.nngp_knn_query.restype = ctypes.c_int
     lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
@@ -171,6 +174,25 @@ def knn_prior(coords: torch.Tensor, m: int, q0: int = 0, q1: Optional[int] = Non
     ws = _workspace(lib.nngp_knn_workspace_bytes(n, m), dev)
     _check(lib.nngp_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out), _ptr(ws), ws.numel(), _stream(dev)),
            "nngp_knn_prior")
+    return out
+
+
+def knn_prior_rows(coords: torch.Tensor, m: int, rows: torch.Tensor,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Prior neighbour sets of the locations ``rows`` (int32 point indices, any order):
+    row t of the result is the set of point ``rows[t]`` (nngp_knn_prior_rows)."""
+    coords = _as_coords(coords)
+    if rows.dtype != torch.int32 or rows.dim() != 1:
+        raise ValueError("rows must be int32 (n_rows,)")
+    rows = rows.contiguous()
+    dev = _require_gpu(coords, rows)
+    n = coords.shape[0]
+    if out is None:
+        out = torch.empty((rows.shape[0], m), dtype=torch.int32, device=dev)
+    lib = load()
+    ws = _workspace(lib.nngp_knn_workspace_bytes(n, m), dev)
+    _check(lib.nngp_knn_prior_rows(_ptr(coords), n, m, _ptr(rows), rows.shape[0], _ptr(out), _ptr(ws), ws.numel(),
+                                   _stream(dev)), "nngp_knn_prior_rows")
     return out
 
 

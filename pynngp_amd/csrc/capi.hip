@@ -257,8 +257,27 @@ int nngp_knn_prior(const double* coords, int64_t n_points, int32_t m, int64_t q0
     if (workspace_bytes < plan.total_bytes)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
     if (q1 == q0 || m == 0) return NNGP_OK;
-    e = nngp::knn_launch(true, coords, n_points, m, coords, q0, q1, nbr, workspace, plan, (hipStream_t)stream);
+    e = nngp::knn_launch(true, coords, n_points, m, coords, q0, q1, nullptr, nbr, workspace, plan, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "knn_prior launch");
+    return NNGP_OK;
+}
+
+int nngp_knn_prior_rows(const double* coords, int64_t n_points, int32_t m, const int32_t* rows, int64_t n_rows,
+                        int32_t* nbr, void* workspace, size_t workspace_bytes, void* stream) {
+    if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
+    if (n_points < 1 || n_points > INT32_MAX) return fail(NNGP_EINVAL, "n_points=%lld outside [1, 2^31)", (long long)n_points);
+    if (m < 0 || m > 64) return fail(NNGP_EUNSUP, "m=%d outside [0, 64]", m);
+    if (n_rows < 0) return fail(NNGP_EINVAL, "n_rows < 0");
+    if (n_rows > 0 && m > 0 && (nbr == nullptr || rows == nullptr)) return fail(NNGP_EINVAL, "rows and nbr must be non-null");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    nngp::KnnPlan plan;
+    hipError_t e = nngp::knn_plan(n_points, &plan);
+    if (e != hipSuccess) return hip_fail(e, "knn plan");
+    if (workspace_bytes < plan.total_bytes)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
+    if (n_rows == 0 || m == 0) return NNGP_OK;
+    e = nngp::knn_launch(true, coords, n_points, m, coords, 0, n_rows, rows, nbr, workspace, plan, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "knn_prior_rows launch");
     return NNGP_OK;
 }
 
@@ -277,7 +296,7 @@ int nngp_knn_query(const double* ref, int64_t n_ref, const double* query, int64_
     if (workspace_bytes < plan.total_bytes)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
     if (n_query == 0 || k == 0) return NNGP_OK;
-    e = nngp::knn_launch(false, ref, n_ref, k, query, 0, n_query, nbr, workspace, plan, (hipStream_t)stream);
+    e = nngp::knn_launch(false, ref, n_ref, k, query, 0, n_query, nullptr, nbr, workspace, plan, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "knn_query launch");
     return NNGP_OK;
 }

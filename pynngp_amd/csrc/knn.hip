@@ -179,14 +179,15 @@ struct TopK {
 template <int KMAX, bool PRIOR>
 __global__ __launch_bounds__(256) void knn_query_kernel(const double2* __restrict__ coords, int64_t n, int m,
                                                         const double2* __restrict__ query, int64_t q0, int64_t q1,
+                                                        const int32_t* __restrict__ rows,
                                                         int64_t brute_below, const Bbox* __restrict__ box, int gx,
                                                         int gy, const int32_t* __restrict__ cell_start,
                                                         const int32_t* __restrict__ idx_sorted,
                                                         const double2* __restrict__ pts_sorted,
                                                         int32_t* __restrict__ nbr) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t i = q0 + t;
-    if (i >= q1) return;
+    if (q0 + t >= q1) return;
+    const int64_t i = rows != nullptr ? (int64_t)rows[t] : q0 + t;  // PRIOR with a row list: query row t is point rows[t]
     const int64_t limit = PRIOR ? i : n;  // candidates are reference points j < limit
     const int k = (int)(limit < m ? limit : m);
     int32_t* out = nbr + t * m;
@@ -297,22 +298,22 @@ hipError_t knn_plan(int64_t n_points, KnnPlan* plan) {
 
 template <int KMAX>
 static void launch_query(bool prior, const double* coords, int64_t n, int m, const double* query, int64_t q0,
-                         int64_t q1, int64_t brute_below, const Bbox* box, const KnnPlan& pl,
+                         int64_t q1, const int32_t* rows, int64_t brute_below, const Bbox* box, const KnnPlan& pl,
                          const int32_t* cell_start, const int32_t* idx_sorted, const double2* pts_sorted, int32_t* nbr,
                          hipStream_t s) {
     const dim3 grid((unsigned)((q1 - q0 + 255) / 256)), block(256);
     if (prior)
         hipLaunchKernelGGL((knn_query_kernel<KMAX, true>), grid, block, 0, s, (const double2*)coords, n, m,
-                           (const double2*)query, q0, q1, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
+                           (const double2*)query, q0, q1, rows, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
                            pts_sorted, nbr);
     else
         hipLaunchKernelGGL((knn_query_kernel<KMAX, false>), grid, block, 0, s, (const double2*)coords, n, m,
-                           (const double2*)query, q0, q1, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
+                           (const double2*)query, q0, q1, rows, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
                            pts_sorted, nbr);
 }
 
 hipError_t knn_launch(bool prior, const double* coords, int64_t n, int m, const double* query, int64_t q0, int64_t q1,
-                      int32_t* nbr, void* workspace, const KnnPlan& pl, hipStream_t s) {
+                      const int32_t* rows, int32_t* nbr, void* workspace, const KnnPlan& pl, hipStream_t s) {
     char* w = (char*)workspace;
     double* bpart = (double*)(w + pl.off_bbox);
     Bbox* box = (Bbox*)(bpart + 4 * 256);
@@ -340,7 +341,7 @@ hipError_t knn_launch(bool prior, const double* coords, int64_t n, int m, const 
     // brute force where scanning s[0:i] is cheaper than the grid rings it would need
     int64_t brute_below = (int64_t)sqrt((double)m * (double)n / kPointsPerCell);
     if (brute_below < 1024) brute_below = 1024;
-#define NNGP_Q(KM) launch_query<KM>(prior, coords, n, m, query, q0, q1, brute_below, box, pl, cell_start, idx_sorted, pts_sorted, nbr, s)
+#define NNGP_Q(KM) launch_query<KM>(prior, coords, n, m, query, q0, q1, rows, brute_below, box, pl, cell_start, idx_sorted, pts_sorted, nbr, s)
     if (m <= 8)
         NNGP_Q(8);
     else if (m <= 16)

