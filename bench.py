@@ -54,6 +54,21 @@ def synth(n_total, seed=0):
     return coords, values
 
 
+def committed_traffic(args, want_bf):
+    """HBM bytes per launch measured for this exact kernel config by a committed rocprofv3
+    --pmc pass (profiles/traffic.json), or (None, None)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            entries = json.load(f)["entries"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for e in entries:
+        if (e["n_per_gpu"] == args.n and e["m"] == args.m and e["kind"] == args.kind and e["layout"] == args.layout
+                and e["write_BF"] == want_bf and args.algo == "auto"):
+            return e["bytes_per_launch"], f'{e["source"]} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {e["kernel"]})'
+    return None, None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -183,7 +198,9 @@ def main():
         bpl = bytes_per_location(args.m) if want_bf else bytes_per_location(args.m) - 8 * args.m - 8
         achieved = bpl * rows / (kern_ms * 1e-3)
         fpl = flops_per_location(args.m)
-        traffic = args.pmc_traffic
+        traffic, traffic_src = args.pmc_traffic, "--pmc-traffic" if args.pmc_traffic is not None else None
+        if traffic is None:
+            traffic, traffic_src = committed_traffic(args, want_bf)
         out = {
             "metric": METRIC,
             "value": n_total * args.steps / elapsed,
@@ -223,6 +240,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_location": bpl,
                 "kernel_ms": kern_ms,
                 "kernel_rows": rows,
