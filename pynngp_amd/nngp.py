@@ -301,9 +301,30 @@ class NNGP:
         n = self.nbr.shape[0]
         return -0.5 * (n * LOG_2PI + ph[0] + ph[1])
 
-    def oneSample(self):
-        """Gibbs sweep (nngp.py:98-101 calls methods that do not exist): SURVEY.md 8(f) 'next'."""
-        raise NotImplementedError("the Gibbs sweep is SURVEY.md 8(f) 'next' (the reference has no implementation)")
+    def oneSample(self, seed: int = 0, X=None, **sampler_kw):
+        """One Gibbs iteration (nngp.py:98-101, whose update_wt / update_ws /
+        update_y_unobserved do not exist in the reference) of the response model
+        y = X beta + w + eps on S = T: delegates to :class:`pynngp_amd.SeqNNGP`, created on
+        the first call with w initialised to ``ws`` and (sigma2, phi, tau2) from ``cov``
+        (``X`` defaults to an intercept).  Afterwards ``ws`` and ``wt`` hold the current w.
+        Returns the sampler (its ``beta, sigma2, tau2, phi`` are the other draws)."""
+        if not self._same_sets():
+            raise NotImplementedError("oneSample needs refType 'S=T' (w lives on the observed locations)")
+        y = np.asarray(self.y, dtype=np.float64)
+        if y.ndim != 1:
+            raise ValueError("oneSample needs one response per location (1-D y)")
+        if getattr(self, "_sampler", None) is None:
+            from .gibbs import SeqNNGP
+
+            cv = self._covariance()
+            tau2 = cv.tau2 if cv.tau2 > 0 else 0.1 * cv.sigma2
+            self._sampler = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi,
+                                    seed=seed, device=self.device, w_init=np.asarray(self.ws, dtype=np.float64),
+                                    **sampler_kw)
+        self._sampler.step()
+        self.ws = self._sampler.w_input_order.cpu().numpy()
+        self.wt = self.ws
+        return self._sampler
 
 
 def reference_set(t, refType):

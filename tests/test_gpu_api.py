@@ -87,7 +87,7 @@ def test_callable_cov_and_errors(dev):
     assert model._CNs(10).shape == (4, 4)
     with pytest.raises(TypeError):
         model._Bsi(10)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(TypeError):  # the sampler needs a Covariance (fused kernel)
         model.oneSample()
     with pytest.raises(ValueError):
         NNGP(t, y, None, ("grid", 10), 4, None)
@@ -145,3 +145,23 @@ def test_sharded_storage_layout_equals_natural(dev, kind, theta):
         assert torch.equal(sh.F, nat.F[sh.rows_input])
     assert torch.equal(torch.sort(torch.cat(seen)).values, torch.arange(n, device=dev))
     assert torch.allclose(tot, pn[:2], rtol=1e-12, atol=0)
+
+
+def test_one_sample_drop_in(dev):
+    """NNGP.oneSample (nngp.py:98-101) runs the Gibbs iteration and updates ws / wt."""
+    from pynngp_amd import NNGP, Covariance
+
+    rng = np.random.default_rng(12)
+    t = rng.uniform(size=(3000, 2))
+    y = np.sin(5 * t[:, 0]) + 0.2 * rng.standard_normal(3000)
+    runs = []
+    for _ in range(2):
+        g = NNGP(t, y, None, "S=T", 10, Covariance("exponential", 1.0, 8.0, 0.05), device=dev)
+        ws0 = g.ws.copy()
+        for _ in range(5):
+            s = g.oneSample(seed=4)
+        assert g.ws.shape == (3000,) and g.wt is g.ws and not np.array_equal(g.ws, ws0)
+        assert s.iteration == 5 and np.isfinite(s.sigma2) and np.isfinite(s.tau2)
+        runs.append(g.ws)
+    np.testing.assert_array_equal(runs[0], runs[1])  # bit-reproducible chain
+    assert np.corrcoef(runs[0], y)[0, 1] > 0.5
