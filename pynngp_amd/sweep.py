@@ -73,11 +73,9 @@ class ShardedLogLik:
 
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
                  algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
-                 spatial_order: bool = True, layout: str = "natural"):
+                 spatial_order: bool = True, layout: str = "natural", build_perm: Optional[Callable] = None):
         if layout not in ("natural", "storage"):
             raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
-        if layout == "storage" and (compute is not None or build_nbr is not None):
-            raise ValueError("layout='storage' uses the device kernels (no injected compute / build_nbr)")
         self.layout = layout
         self.coords = coords
         self.n = coords.shape[0]
@@ -91,12 +89,14 @@ class ShardedLogLik:
         self.order = None
         self.perm = self.pos = None
         if layout == "storage":
-            perm, _ = _lib.row_order(coords)
+            # global Z-order storage order (identical on every rank); injectable for the CPU tests
+            perm = _lib.row_order(coords)[0] if build_perm is None else build_perm(coords)
             self.perm = perm
             self.pos = torch.empty(self.n, dtype=torch.int32, device=coords.device)
             self.pos[perm.long()] = torch.arange(self.n, dtype=torch.int32, device=coords.device)
             self._coords_sweep = coords[perm.long()].contiguous()
-            nbr0 = _lib.knn_prior_rows(coords, self.m, perm[self.lo:self.hi])
+            rows = perm[self.lo:self.hi].contiguous()
+            nbr0 = _lib.knn_prior_rows(coords, self.m, rows) if build_nbr is None else build_nbr(coords, self.m, rows)
             nb = nbr0.long()
             self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
             self._nbr_sweep = self.nbr
@@ -123,10 +123,10 @@ class ShardedLogLik:
     def local_partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
                        values_layout: str = "input") -> torch.Tensor:
         """Stream-ordered partials of this shard (no host sync)."""
-        if self._compute is not None:
-            return self._compute(self, cov, values, want_bf)
         if self.layout == "storage" and values is not None and values_layout == "input":
             values = self.to_storage(values, out=self._vstore)
+        if self._compute is not None:
+            return self._compute(self, cov, values, want_bf)
         B, F = (self._B, self._F) if want_bf else (None, None)
         _, _, p = _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
                                 want_bf=want_bf, algo=self.algo, B=B, F=F, partials=self._partials,

@@ -47,6 +47,63 @@ def _oracle_compute(sweep, cov, values, want_bf):
     return torch.tensor([p[0], p[1], p[2], -1.0], dtype=torch.float64)
 
 
+def _oracle_build_rows(coords, m, rows):
+    from oracle import nngp_oracle as O
+
+    full = O.c_knn_prior(coords.numpy(), m)
+    return torch.from_numpy(full[rows.numpy()])
+
+
+def _random_perm(coords):
+    return torch.from_numpy(np.random.default_rng(99).permutation(coords.shape[0]).astype(np.int32))
+
+
+def _oracle_compute_storage(sweep, cov, values, want_bf):
+    """The C oracle on the relabelled (storage-order) arrays the device kernel would see."""
+    from oracle import nngp_oracle as O
+
+    _, _, p = O.c_bf_sweep(sweep._coords_sweep.numpy(), sweep._nbr_sweep.numpy(), cov.kind, cov.theta,
+                           None if values is None else values.numpy(), i0=sweep.lo)
+    return torch.tensor([p[0], p[1], p[2], -1.0], dtype=torch.float64)
+
+
+def _worker_storage(rank, world, port, n, m, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pynngp_amd import Covariance
+
+    rng = np.random.default_rng(0)
+    coords = torch.from_numpy(rng.uniform(size=(n, 2)))
+    values = torch.from_numpy(rng.standard_normal(n))
+    sweep = ShardedLogLik(coords, m, rank, world, layout="storage", build_perm=_random_perm,
+                          build_nbr=_oracle_build_rows, compute=_oracle_compute_storage)
+    cov = Covariance("exponential", 1.3, 9.0, 0.05)
+    out[rank] = (sweep.loglik(cov, values), sweep.rows_input.tolist())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_storage_layout_matches_single(world):
+    """Relabelled storage shards (any global permutation, identical on every rank) give
+    the input-order log-likelihood, and the shards' rows cover every location once."""
+    from oracle import nngp_oracle as O
+
+    n, m = 2500, 8
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_storage, args=(world, _free_port(), n, m, out), nprocs=world, join=True)
+    rng = np.random.default_rng(0)
+    coords = rng.uniform(size=(n, 2))
+    values = rng.standard_normal(n)
+    _, _, p = O.c_bf_sweep(coords, O.c_knn_prior(coords, m), "exponential", (1.3, 9.0, 0.05), values)
+    want = O.loglik_from_partials(p, n)
+    lls = [out[r][0] for r in range(world)]
+    assert all(v == lls[0] for v in lls)
+    assert abs(lls[0] - want) <= 1e-11 * abs(want)
+    assert sorted(sum((out[r][1] for r in range(world)), [])) == list(range(n))
+
+
 def _worker(rank, world, port, n, m, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
