@@ -35,20 +35,14 @@ def combine_partials(local: torch.Tensor, world: int, group=None) -> torch.Tenso
 
     [0], [1] are summed; [2], [3] (first bad row or -1) take the smallest non-negative.
     """
-    if world == 1 and not (dist.is_available() and dist.is_initialized()):
+    if world == 1:
         return local
     gathered = torch.empty((world, 4), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(gathered, local.reshape(1, 4), group=group)
     if gathered.device.type == "cuda":
         return _lib.combine_partials(gathered)  # one tiny HIP kernel, rank order
     # CPU (gloo) path: the same fold on the host, for the multi-process tests
-    g = gathered.tolist()
-    flags = [[r[2] for r in g if r[2] >= 0], [r[3] for r in g if r[3] >= 0]]
-    out = [0.0, 0.0] + [min(f) if f else -1.0 for f in flags]
-    for r in g:
-        out[0] += r[0]
-        out[1] += r[1]
-    return torch.tensor(out, dtype=local.dtype)
+    return combine_partials_host(gathered)
 
 
 class ShardedLogLik:
@@ -121,16 +115,18 @@ class ShardedLogLik:
         return torch.index_select(values, 0, self.perm, out=out)
 
     def local_partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
-                       values_layout: str = "input") -> torch.Tensor:
-        """Stream-ordered partials of this shard (no host sync)."""
+                       values_layout: str = "input", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Stream-ordered partials of this shard (no host sync); into ``out`` (4,) if given."""
         if self.layout == "storage" and values is not None and values_layout == "input":
             values = self.to_storage(values, out=self._vstore)
         if self._compute is not None:
-            return self._compute(self, cov, values, want_bf)
+            p = self._compute(self, cov, values, want_bf)
+            return p if out is None else out.copy_(p)
         B, F = (self._B, self._F) if want_bf else (None, None)
         _, _, p = _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
-                                want_bf=want_bf, algo=self.algo, B=B, F=F, partials=self._partials,
-                                workspace=self._ws, order=self.order)
+                                want_bf=want_bf, algo=self.algo, B=B, F=F,
+                                partials=self._partials if out is None else out, workspace=self._ws,
+                                order=self.order)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
@@ -163,8 +159,65 @@ class ShardedLogLik:
         return self._F
 
 
+class PipelinedCombine:
+    """Throughput mode for independent sweeps (a theta scan, a batch of MH proposals,
+    the benchmark): sweep k writes its partials to slot k, its all-gather runs
+    asynchronously on the RCCL stream and the rank-order fold on a side stream, so
+    the next sweep starts while the collective of the previous one is in flight.
+    Every sweep's global partials end up in row k of :meth:`finish`.
+
+        pipe = PipelinedCombine(sweep, K)
+        for k in range(K):
+            sweep.local_partials(cov_k, v, out=pipe.local[k])
+            pipe.exchange(k)
+        res = pipe.finish()      # (K, 4), stream-ordered
+    """
+
+    def __init__(self, sweep: "ShardedLogLik", slots: int):
+        dev = sweep.coords.device
+        self.sweep = sweep
+        self.world = sweep.world
+        self.local = torch.empty((slots, 4), dtype=torch.float64, device=dev)
+        self.gathered = torch.empty((slots, self.world, 4), dtype=torch.float64, device=dev)
+        self.results = torch.empty((slots, 4), dtype=torch.float64, device=dev)
+        self.side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.k = 0
+
+    def exchange(self, k: int) -> None:
+        self.k = max(self.k, k + 1)
+        if self.world == 1:
+            return
+        work = dist.all_gather_into_tensor(self.gathered[k], self.local[k].reshape(1, 4),
+                                           group=self.sweep.group, async_op=True)
+        if self.side is None:
+            work.wait()
+            self.results[k].copy_(combine_partials_host(self.gathered[k]))
+            return
+        with torch.cuda.stream(self.side):
+            work.wait()  # the side stream waits for the collective, the compute stream does not
+            _lib.combine_partials(self.gathered[k], out=self.results[k])
+
+    def finish(self) -> torch.Tensor:
+        if self.world == 1:
+            return self.local[: self.k]
+        if self.side is not None:
+            torch.cuda.current_stream(self.side.device).wait_stream(self.side)
+        return self.results[: self.k]
+
+
+def combine_partials_host(g: torch.Tensor) -> torch.Tensor:
+    """Rank-order fold of gathered (world, 4) partials on the host (CPU / gloo path)."""
+    rows = g.tolist()
+    flags = [[r[2] for r in rows if r[2] >= 0], [r[3] for r in rows if r[3] >= 0]]
+    out = [0.0, 0.0] + [min(f) if f else -1.0 for f in flags]
+    for r in rows:
+        out[0] += r[0]
+        out[1] += r[1]
+    return torch.tensor(out, dtype=g.dtype)
+
+
 def loglik_from_partials(p, n: int) -> float:
     return -0.5 * (n * LOG_2PI + float(p[0]) + float(p[1]))
 
 
-__all__ = ["shard_range", "combine_partials", "ShardedLogLik", "loglik_from_partials", "math"]
+__all__ = ["shard_range", "combine_partials", "ShardedLogLik", "PipelinedCombine", "loglik_from_partials", "math"]

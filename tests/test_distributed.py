@@ -79,7 +79,16 @@ def _worker_storage(rank, world, port, n, m, out):
     sweep = ShardedLogLik(coords, m, rank, world, layout="storage", build_perm=_random_perm,
                           build_nbr=_oracle_build_rows, compute=_oracle_compute_storage)
     cov = Covariance("exponential", 1.3, 9.0, 0.05)
-    out[rank] = (sweep.loglik(cov, values), sweep.rows_input.tolist())
+    # pipelined exchange (throughput mode): three independent sweeps, each fully combined
+    from pynngp_amd.sweep import PipelinedCombine
+
+    pipe = PipelinedCombine(sweep, 3)
+    for k, c in enumerate([cov, cov.replace(phi=4.0), cov]):
+        sweep.local_partials(c, values, out=pipe.local[k])
+        pipe.exchange(k)
+    res = pipe.finish()
+    assert torch.equal(res[0], res[2]) and not torch.equal(res[0], res[1])
+    out[rank] = (sweep.loglik(cov, values), sweep.rows_input.tolist(), res[0].tolist())
     dist.destroy_process_group()
 
 
@@ -102,6 +111,7 @@ def test_gloo_storage_layout_matches_single(world):
     assert all(v == lls[0] for v in lls)
     assert abs(lls[0] - want) <= 1e-11 * abs(want)
     assert sorted(sum((out[r][1] for r in range(world)), [])) == list(range(n))
+    assert abs(O.loglik_from_partials(out[0][2], n) - lls[0]) <= 1e-12 * abs(lls[0])
 
 
 def _worker(rank, world, port, n, m, out):
