@@ -37,12 +37,13 @@ __device__ __forceinline__ double pr_from0(double v) { return dpp_f64<0xA0>(v); 
 __device__ __forceinline__ double pr_from1(double v) { return dpp_f64<0xF5>(v); }  // lane 1's v
 __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return q1 ? v1 : v0; }
 
-// A/B builds only (make EXTRA=-DNNGP_PAIRB_WAVES_PER_EU=3): ask the compiler for an occupancy
-#ifdef NNGP_PAIRB_WAVES_PER_EU
-#define NNGP_PAIRB_ATTR __attribute__((amdgpu_waves_per_eu(NNGP_PAIRB_WAVES_PER_EU, NNGP_PAIRB_WAVES_PER_EU)))
-#else
-#define NNGP_PAIRB_ATTR
+// Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
+// (<= 256 VGPRs): m = 16 / 17 then fit in 248 / 252 VGPRs without spills instead of
+// 264 / 266 (one wave per SIMD).  Beyond it the block needs more registers than that.
+#ifndef NNGP_PAIRB_TWO_WAVES_MAX
+#define NNGP_PAIRB_TWO_WAVES_MAX 17
 #endif
+#define NNGP_PAIRB_ATTR __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), 2)))
 
 template <int M, int KIND>
 __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* __restrict__ coords, int64_t n_points,

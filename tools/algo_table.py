@@ -19,7 +19,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1_000_000)
 ap.add_argument("--ms", default="1-20")
 ap.add_argument("--kind", default="exponential")
-ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--rounds", type=int, default=6)
 args = ap.parse_args()
 lo, hi = (int(x) for x in args.ms.split("-"))
 dev = torch.device("cuda", 0)
@@ -27,6 +28,7 @@ rng = np.random.default_rng(0)
 c = torch.from_numpy(rng.uniform(0, 1, (args.n, 2))).to(dev)
 v = torch.from_numpy(rng.standard_normal(args.n)).to(dev)
 theta = (1.0, 30.0, 0.0) if args.kind == "exponential" else (1.0, 17.320508075688772, 0.1)
+ap2 = None
 for m in range(lo, hi + 1):
     nb = _lib.knn_prior(c, m)
     order, srt = _lib.row_order(c, 0, args.n, nb)
@@ -35,24 +37,37 @@ for m in range(lo, hi + 1):
     algos = ["lane"] if m <= 16 else []
     algos += ["pair"] if 10 <= m <= 20 else []
     algos += ["quad"] if m in (15, 16, 20) else []
-    algos += ["pairb"] if 2 <= m <= 20 else []
+    algos += ["pairb"] if 1 <= m <= 20 else []
     algos += ["wave"]
-    ref = None
-    for algo in algos:
-        ws = _lib.bf_workspace(args.n, m, algo, dev)
+    wss = {a: _lib.bf_workspace(args.n, m, a, dev) for a in algos}
+
+    def run(algo):
+        _lib.bf_sweep(c, srt, 0, args.kind, *theta, values=v, algo=algo, B=B, F=F, workspace=wss[algo], order=order)
+
+    for a in algos:
         for _ in range(2):
-            _, _, p = _lib.bf_sweep(c, srt, 0, args.kind, *theta, values=v, algo=algo, B=B, F=F, workspace=ws,
-                                    order=order)
-        reps = 2 if algo == "wave" else args.reps
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-        for a, b in ev:
-            a.record()
-            _lib.bf_sweep(c, srt, 0, args.kind, *theta, values=v, algo=algo, B=B, F=F, workspace=ws, order=order)
-            b.record()
+            run(a)
+    times = {a: [] for a in algos}
+    # interleaved rounds (clock / thermal drift hits every algo alike); median per algo
+    for rnd in range(args.rounds):
+        for a in algos:
+            reps = 1 if a == "wave" else args.reps
+            if a == "wave" and rnd > 0:
+                continue
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                run(a)
+            e1.record()
+            torch.cuda.synchronize()
+            times[a].append(e0.elapsed_time(e1) / reps)
+    ref = None
+    for a in algos:
+        run(a)
         torch.cuda.synchronize()
-        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         Fh = F.cpu().numpy()
-        if ref is None:
-            ref = Fh
-        print(json.dumps({"m": m, "algo": algo, "kernel_ms": round(ms, 5), "gloc_s": round(args.n / ms / 1e6, 4),
+        ref = Fh if ref is None else ref
+        ms = float(np.median(times[a]))
+        print(json.dumps({"m": m, "algo": a, "kernel_ms": round(ms, 5), "gloc_s": round(args.n / ms / 1e6, 4),
+                          "rounds_ms": [round(t, 5) for t in times[a]],
                           "max_rel_dF_vs_first": float(np.max(np.abs(Fh - ref) / ref))}), flush=True)
