@@ -54,6 +54,21 @@ def synth(n_total, seed=0):
     return coords, values
 
 
+def knn_cpu_baseline(coords, m, n_full):
+    """Neighbour-set build on the host: the C oracle (exact brute force over s[0:i],
+    OpenMP) on the first 20,000 locations, extrapolated quadratically to n_full (the
+    reference rebuilds a KDTree per i, SURVEY.md 6: 12.7 s at N=1e4, single thread)."""
+    from oracle import nngp_oracle as O
+
+    n = min(20_000, coords.shape[0])
+    t = time.perf_counter()
+    O.c_knn_prior(coords[:n], m)
+    el = time.perf_counter() - t
+    return {"seconds_measured": el, "n_measured": n, "seconds_extrapolated": el * (n_full / n) ** 2,
+            "n_extrapolated": n_full, "cores": int(O.load_c_oracle().oracle_num_threads()),
+            "kind": "port (exact brute force, C oracle; extrapolated as N^2)"}
+
+
 def committed_traffic(args, want_bf):
     """HBM bytes per launch measured for this exact kernel config by a committed rocprofv3
     --pmc pass (profiles/traffic.json), or (None, None)."""
@@ -269,6 +284,7 @@ def main():
             if F_gpu is None:
                 _, F_t, _ = _lib.bf_sweep(c_sw, sweep.nbr, 0, cov.kind, *cov.theta)
                 F_gpu = F_t.cpu().numpy()
+            out["neighbor_build_cpu"] = knn_cpu_baseline(coords, args.m, n_total)
             out["cpu_baseline"] = cpu_baseline(c_sw.cpu().numpy(), values, sweep.nbr.cpu().numpy(), args.kind,
                                                (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
         sys.stdout.flush()

@@ -278,3 +278,27 @@ def test_bf_m1_covariance_ulp(lib, dev, c_oracle, kind, algo):
     Bg = B.cpu().numpy()[1:, 0].astype(np.longdouble)
     rel = np.abs(Bg - Bx) / Bx
     assert float(rel.max()) <= 2e-15, float(rel.max())
+
+
+@pytest.mark.parametrize("algo", ["lane", "pairb", "wave"])
+def test_bf_extreme_inputs(lib, dev, c_oracle, algo):
+    """UTM-like coordinates (offset 1e6, spread ~1e3), tiny and huge phi, exact duplicates:
+    the kernel's clamps (d2 floor, exp underflow bound) and far-point padding hold."""
+    rng = np.random.default_rng(8)
+    n, m = 4000, 12
+    coords = 1e6 + rng.uniform(0, 1000.0, (n, 2))
+    coords[2000:2010] = coords[100]
+    y = rng.standard_normal(n)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    for kind, theta in [("exponential", (2.0, 1e-2, 0.3)), ("matern32", (1.0, 3e-3, 0.2)),
+                        ("exponential", (1.0, 50.0, 0.1)), ("exponential", (1e6, 0.5, 1e5))]:
+        _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, algo if m <= 16 or algo != "lane" else "auto")
+
+
+def test_bf_tiny_fields(lib, dev, c_oracle):
+    """N <= m (every row padded), N = 1 and N = 2."""
+    for n, m in [(1, 4), (2, 4), (5, 15), (16, 15), (3, 20)]:
+        coords, y = _field(n, 40 + n)
+        nbr = c_oracle.c_knn_prior(coords, m)
+        for algo in ("auto", "wave") + (("pairb",) if m <= 20 else ()):
+            _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 5.0, 0.1), y, algo)

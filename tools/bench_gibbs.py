@@ -23,24 +23,43 @@ ap.add_argument("--m", type=int, default=15)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--warmup", type=int, default=5)
 args = ap.parse_args()
-dev = torch.device("cuda", 0)
+# several GPUs (torchrun): independent chains, one per GPU ("replicas only")
+world = int(os.environ.get("WORLD_SIZE", "1"))
+rank = int(os.environ.get("RANK", "0"))
+dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+torch.cuda.set_device(dev)
+if world > 1:
+    import torch.distributed as dist
+
+    dist.init_process_group("nccl", device_id=dev)
 rng = np.random.default_rng(2)
 coords = rng.uniform(0, 1, (args.n, 2))
 y = 1.0 + rng.standard_normal(args.n) * 0.5 + 0.3 * rng.standard_normal(args.n)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev)
+g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
 torch.cuda.synchronize()
 setup_s = time.perf_counter() - t0
 for _ in range(args.warmup):
     g.step()
 torch.cuda.synchronize()
+if world > 1:
+    dist.barrier()
 t0 = time.perf_counter()
 for _ in range(args.iters):
     g.step()
 torch.cuda.synchronize()
+if world > 1:
+    dist.barrier()
 el = time.perf_counter() - t0
-print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, 1 GPU",
-                  "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
+if world > 1:
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+if rank == 0:
+    print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, one chain per GPU",
+                      "chains": world, "chain_iters_per_s": world * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
                   "locations_per_s": args.n * args.iters / el, "setup_s": setup_s, "n_colors": int(g.n_colors),
                   "phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "accept": g.n_accept / max(1, g.iteration)}))
+if world > 1:
+    dist.destroy_process_group()
