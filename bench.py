@@ -69,19 +69,45 @@ def knn_cpu_baseline(coords, m, n_full):
             "kind": "port (exact brute force, C oracle; extrapolated as N^2)"}
 
 
-def committed_traffic(args, want_bf):
-    """HBM bytes per launch measured for this exact kernel config by a committed rocprofv3
-    --pmc pass (profiles/traffic.json), or (None, None)."""
+def committed_profile(args, want_bf):
+    """The committed rocprofv3 --pmc measurement (profiles/traffic.json) of this exact kernel
+    config, or None."""
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
-        return None, None
+        return None
     for e in entries:
         if (e["n_per_gpu"] == args.n and e["m"] == args.m and e["kind"] == args.kind and e["layout"] == args.layout
                 and e["write_BF"] == want_bf and args.algo == "auto"):
-            return e["bytes_per_launch"], f'{e["source"]} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {e["kernel"]})'
-    return None, None
+            return e
+    return None
+
+
+def committed_traffic(args, want_bf):
+    """HBM bytes per launch measured for this exact kernel config by a committed rocprofv3
+    --pmc pass (profiles/traffic.json), or (None, None)."""
+    e = committed_profile(args, want_bf)
+    if e is None:
+        return None, None
+    return e["bytes_per_launch"], f'{e["source"]} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {e["kernel"]})'
+
+
+# VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes per clock x 2.4 GHz (a 64-lane wave-instruction
+# issues in 4 clocks; fp64 FMA / add / mul and 32-bit ops alike, MI355X_MICROARCH.md)
+VALU_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def valu_roofline(prof, rows, kern_ms):
+    """Vector-issue roofline: lane-operations per second (VALU instructions per wave from the
+    committed PMC profile x 64 lanes / locations per wave x locations/s) vs the issue peak."""
+    if prof is None or "valu_per_wave" not in prof:
+        return None
+    per_loc = prof["valu_per_wave"] * 64 / prof["locations_per_wave"]
+    achieved = per_loc * rows / (kern_ms * 1e-3)
+    return {"achieved": achieved / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s",
+            "frac": achieved / VALU_LANE_OPS_PEAK, "valu_lane_ops_per_location": per_loc,
+            "source": prof["source"] + " (SQ_INSTS_VALU / SQ_WAVES)"}
 
 
 def cpu_model():
@@ -266,6 +292,7 @@ def main():
                 "kernel_ms": kern_ms,
                 "kernel_rows": rows,
             },
+            "roofline_valu": valu_roofline(committed_profile(args, want_bf), rows, kern_ms),
             "roofline_fp64": {
                 "achieved": fpl * rows / (kern_ms * 1e-3) / 1e12,
                 "peak": FP64_PEAK / 1e12,

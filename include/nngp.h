@@ -187,6 +187,9 @@ int nngp_combine_partials(const double *gathered, int32_t world, double *partial
  *   w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
  *   yres = y - X beta.  z: NULL (Philox4x32-10 normals keyed by seed, counter
  *   (location, sweep)) or n given standard normals (for testing).
+ * nngp_gibbs_normals: z[i] = the Philox4x32-10 normal the sweep would draw for
+ *   (seed, location i, sweep), for all n locations in one parallel pass; passing it
+ *   as nngp_gibbs_w_sweep's z gives the bit-identical chain with shorter colour steps.
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum (yres_i - w_i)^2,
  *   out[2 + c] = sum_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p)).
  * ------------------------------------------------------------------------- */
@@ -203,6 +206,7 @@ int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, in
                        int64_t n, int32_t m, double sigma2, double tau2, const double *yres, double *w, double *r,
                        const int32_t *off, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
                        void *stream);
+int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
                      const double *X, int32_t p, const double *w, double *out, void *workspace,

@@ -36,6 +36,7 @@ SYMBOLS = (
     "nngp_gibbs_prep_bytes",
     "nngp_gibbs_prepare",
     "nngp_gibbs_w_sweep",
+    "nngp_gibbs_normals",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
 )
@@ -98,6 +99,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_prepare.restype = ctypes.c_int
     lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P]
     lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
+    lib.nngp_gibbs_normals.argtypes = [I64, U64, U64, P, P]
+    lib.nngp_gibbs_normals.restype = ctypes.c_int
     lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]
     lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, SZ, P]
@@ -426,6 +429,16 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
                                      float(sigma2), float(tau2), _ptr(yres), _ptr(w), _ptr(r), _ptr(off), _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
+
+
+def gibbs_normals(z: torch.Tensor, seed: int, sweep: int) -> torch.Tensor:
+    """Fill z (float64 (n,)) with the sweep's Philox normals (nngp_gibbs_normals)."""
+    dev = _require_gpu(z)
+    if z.dtype != torch.float64 or z.dim() != 1:
+        raise ValueError("z must be float64 (n,)")
+    _check(load().nngp_gibbs_normals(z.shape[0], int(seed) & (2 ** 64 - 1), int(sweep), _ptr(z), _stream(dev)),
+           "nngp_gibbs_normals")
+    return z
 
 
 def gibbs_stats(r: torch.Tensor, Ft: torch.Tensor, yres: torch.Tensor, y: torch.Tensor, X: Optional[torch.Tensor],

@@ -194,6 +194,13 @@ int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, in
     return NNGP_OK;
 }
 
+int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double* z, void* stream) {
+    if (n < 0 || (n > 0 && z == nullptr)) return fail(NNGP_EINVAL, "bad n or null z");
+    hipError_t e = nngp::philox_normals_launch(n, seed, sweep, z, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_normals launch");
+    return NNGP_OK;
+}
+
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p) {
     if (n < 1 || p < 0 || p > 62) return 0;
     return nngp::gibbs_stats_workspace_bytes(n, p);

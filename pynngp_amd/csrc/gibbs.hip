@@ -63,6 +63,21 @@ __host__ __device__ __forceinline__ double philox_normal(uint64_t seed, uint64_t
     return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
+// n standard normals z[i] = philox_normal(seed, i, sweep): the same stream the w sweep draws
+// inline when it gets no z, precomputed in one fully parallel pass so the colour kernels'
+// critical path carries no Philox rounds / log / cos.
+__global__ __launch_bounds__(256) void philox_normals_kernel(int64_t n, uint64_t seed, uint64_t sweep,
+                                                             double* __restrict__ z) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) z[i] = philox_normal(seed, (uint64_t)i, sweep);
+}
+
+hipError_t philox_normals_launch(int64_t n, uint64_t seed, uint64_t sweep, double* z, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(philox_normals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, seed, sweep, z);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- reverse neighbour lists
 __global__ __launch_bounds__(256) void rev_keys(const int32_t* __restrict__ nbr, int64_t n_entries, int64_t n,
                                                 uint32_t* __restrict__ key, int32_t* __restrict__ val) {

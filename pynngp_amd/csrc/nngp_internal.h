@@ -83,6 +83,7 @@ hipError_t reverse_launch(const int32_t* nbr, int64_t n, int m, int32_t* off, in
 int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
                                int32_t* color);
 size_t gibbs_prep_bytes(int64_t n, int m);
+hipError_t philox_normals_launch(int64_t n, uint64_t seed, uint64_t sweep, double* z, hipStream_t s);
 hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
                                 const int32_t* rev_k, const int32_t* order, int64_t n, int m, void* prep,
                                 hipStream_t s);

@@ -117,6 +117,7 @@ class SeqNNGP:
         self.B, self.Ft, self.r = z(n, self.m), z(n), z(n)
         self._B2, self._Ft2, self._r2 = z(n, self.m), z(n), z(n)
         self._part = z(4)
+        self._z = z(n)
         self._ws = _lib.bf_workspace(n, self.m, algo, dev)
         self._stats = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
@@ -174,8 +175,9 @@ class SeqNNGP:
         a, b = self.priors.sigma2_ig
         self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
         # 3. w | rest (colour sweep, in place on w and r)
+        _lib.gibbs_normals(self._z, self.seed, self.iteration)  # the sweep's normals, one parallel pass
         _lib.gibbs_w_sweep(self.members, self.color_off, self._prep, self.m, self.sigma2, self.tau2, self.yres, self.w,
-                           self.r, self.off, self.rev_j, self.seed, self.iteration)
+                           self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z)
         st = _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats).cpu().numpy()
         self.quad = float(st[0])
         # 4. tau2 | y, beta, w

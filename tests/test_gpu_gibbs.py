@@ -201,3 +201,23 @@ def test_seqnngp_recovers_parameters(dev):
     assert 0.4 < res["phi"].mean() / truth["phi"] < 2.5
     # the posterior mean of w tracks the simulated field
     assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.8
+
+
+def test_precomputed_normals_same_chain(dev):
+    """nngp_gibbs_normals gives exactly the normals the sweep draws inline."""
+    from pynngp_amd import _lib
+
+    n, m = 3000, 10
+    s = _setup(dev, n, m, seed=5)
+    yres = torch.from_numpy(s["rng"].standard_normal(n)).to(dev)
+    prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
+    w1, r1 = s["w"].clone(), s["R"].clone()
+    w2, r2 = s["w"].clone(), s["R"].clone()
+    z = torch.empty(n, dtype=torch.float64, device=dev)
+    for sweep in range(3):
+        _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, 1.3, 0.4, yres, w1, r1, s["off"], s["rev_j"], 77,
+                           sweep)
+        _lib.gibbs_normals(z, 77, sweep)
+        _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, 1.3, 0.4, yres, w2, r2, s["off"], s["rev_j"], 77,
+                           sweep, z=z)
+    assert torch.equal(w1, w2) and torch.equal(r1, r2)
