@@ -301,6 +301,72 @@ class NNGP:
         n = self.nbr.shape[0]
         return -0.5 * (n * LOG_2PI + ph[0] + ph[1])
 
+    def profile_loglik(self, cov: Covariance, values=None, mean: str = "constant", algo: str = "auto"):
+        """NNGP log-likelihood of ``values`` (default y) at ``cov`` with a constant mean
+        profiled out by GLS under the NNGP precision (I - B)^T F^-1 (I - B):
+        mu = sum(r1 ry / F) / sum(r1^2 / F), r1 = (I - B) 1, ry = (I - B) y (two fused
+        sweeps with residual output).  ``mean="zero"`` is :meth:`loglik`.  Returns
+        ``(loglik, mu)``."""
+        v = self.y if values is None else values
+        v = torch.as_tensor(np.asarray(v, dtype=np.float64) if not isinstance(v, torch.Tensor) else v,
+                            dtype=torch.float64).to(self.device)
+        if mean == "zero":
+            return self.loglik(v, cov, algo), 0.0
+        if mean != "constant":
+            raise ValueError("mean must be 'constant' or 'zero'")
+        n = v.shape[0]
+        ry = torch.empty(n, dtype=torch.float64, device=self.device)
+        r1 = torch.empty_like(ry)
+        kw = dict(algo=algo, order=self._order)
+        _, F, py = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=v, R=ry, **kw)
+        ones = torch.ones_like(v)
+        _, _, p1 = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=ones, R=r1, **kw)
+        s_y1 = torch.sum(ry * r1 / F)
+        sums = torch.stack([py[0], py[1], p1[1], s_y1, py[2], py[3]]).cpu().numpy()
+        _raise_on_bad(np.array([0.0, 0.0, sums[4], sums[5]]))
+        logF, qyy, q11, qy1 = sums[:4]
+        mu = qy1 / q11
+        quad = qyy - 2.0 * mu * qy1 + mu * mu * q11
+        return -0.5 * (n * LOG_2PI + logF + quad), float(mu)
+
+    def fit(self, kind: Optional[str] = None, x0=None, mean: str = "constant", fix_tau2: Optional[float] = None,
+            method: str = "Nelder-Mead", maxiter: int = 400, algo: str = "auto"):
+        """Maximum-likelihood (sigma2, phi, tau2) of the NNGP response model on S = T, each
+        objective evaluation one or two fused GPU sweeps (scipy.optimize on log-parameters).
+        ``x0`` defaults to ``cov``'s theta; ``fix_tau2`` holds the nugget fixed (e.g. 0 for the
+        latent model).  Sets ``cov`` to the estimate and returns a dict with theta, mu,
+        loglik and the optimizer's evaluation count."""
+        from scipy.optimize import minimize
+
+        base = self.cov if isinstance(self.cov, Covariance) else None
+        kind = kind or (base.kind if base is not None else "exponential")
+        th0 = tuple(x0) if x0 is not None else (base.theta if base is not None else (1.0, 10.0, 0.1))
+        free_tau = fix_tau2 is None
+        z0 = [math.log(th0[0]), math.log(th0[1])] + ([math.log(max(th0[2], 1e-6))] if free_tau else [])
+
+        def theta_of(z):
+            return (math.exp(z[0]), math.exp(z[1]), math.exp(z[2]) if free_tau else float(fix_tau2))
+
+        best = {"ll": -math.inf}
+
+        def obj(z):
+            th = theta_of(z)
+            try:
+                ll, mu = self.profile_loglik(Covariance(kind, *th), mean=mean, algo=algo)
+            except NNGPNumericalError:
+                return 1e300
+            if ll > best["ll"]:
+                best.update(ll=ll, mu=mu, theta=th)
+            return -ll
+
+        res = minimize(obj, np.array(z0), method=method, options={"maxiter": maxiter, "xatol": 1e-6,
+                                                                  "fatol": 1e-9} if method == "Nelder-Mead"
+                       else {"maxiter": maxiter})
+        self.cov = Covariance(kind, *best["theta"])
+        self._B = self._F = None
+        return {"theta": best["theta"], "mu": best["mu"], "loglik": best["ll"], "n_evals": int(res.nfev),
+                "converged": bool(res.success)}
+
     def oneSample(self, seed: int = 0, X=None, **sampler_kw):
         """One Gibbs iteration (nngp.py:98-101, whose update_wt / update_ws /
         update_y_unobserved do not exist in the reference) of the response model

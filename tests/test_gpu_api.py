@@ -165,3 +165,31 @@ def test_one_sample_drop_in(dev):
         runs.append(g.ws)
     np.testing.assert_array_equal(runs[0], runs[1])  # bit-reproducible chain
     assert np.corrcoef(runs[0], y)[0, 1] > 0.5
+
+
+def test_profile_loglik_and_fit(dev, c_oracle):
+    """profile_loglik equals the oracle's log density of y - mu at the GLS mu (found by
+    brute force over mu); fit() recovers the parameters of a simulated field."""
+    from pynngp_amd import NNGP, Covariance
+
+    rng = np.random.default_rng(17)
+    n = 1500
+    t = rng.uniform(size=(n, 2))
+    d = np.sqrt(((t[:, None, :] - t[None, :, :]) ** 2).sum(-1))
+    sigma2, phi, tau2, mu = 1.5, 8.0, 0.2, 3.0
+    L = np.linalg.cholesky(sigma2 * np.exp(-phi * d) + tau2 * np.eye(n))
+    y = mu + L @ rng.standard_normal(n)
+    cov = Covariance("exponential", 1.0, 5.0, 0.1)
+    g = NNGP(t, y, None, "S=T", 15, cov, device=dev)
+    ll, mu_hat = g.profile_loglik(cov)
+    nbr = g.nbr.cpu().numpy()
+    _, _, p = c_oracle.c_bf_sweep(t, nbr, "exponential", cov.theta, y - mu_hat)
+    assert abs(ll - c_oracle.loglik_from_partials(p, n)) <= 1e-10 * abs(ll)
+    for dm in (-1e-3, 1e-3):  # mu_hat maximises the log-likelihood
+        _, _, p2 = c_oracle.c_bf_sweep(t, nbr, "exponential", cov.theta, y - mu_hat - dm)
+        assert c_oracle.loglik_from_partials(p2, n) < ll
+    res = g.fit()
+    s2, ph, t2 = res["theta"]
+    assert res["loglik"] >= ll
+    assert abs(res["mu"] - mu) < 1.0 and 0.5 < s2 / sigma2 < 2.0 and 0.4 < ph / phi < 2.5 and 0.3 < t2 / tau2 < 3.0
+    assert g.cov.theta == res["theta"]
