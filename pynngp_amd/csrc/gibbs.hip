@@ -201,8 +201,13 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
 //   lin_i  = yres_i / tau2 + [(w_i - r_i) invF_i + w_i P_i + sum_e Grev[e] r_j] / s2
 // and a colour step reads one streamed double and one gathered r_j per child.
 // kGroup lanes per location (as the colour kernel): the lanes split the reverse entries
-// (contiguous stores per round), a fixed xor-butterfly sums P_i.
-constexpr int kGroup = 8;
+// (contiguous stores per round), a fixed xor-butterfly sums P_i.  32 measured best for
+// m = 15 (~15 children per location): 8 lanes 1.30, 16 lanes 1.07, 32 lanes 1.05 ms per
+// Gibbs iteration at N = 1e6 -- the colour steps are latency bound.
+#ifndef NNGP_GIBBS_GROUP
+#define NNGP_GIBBS_GROUP 32
+#endif
+constexpr int kGroup = NNGP_GIBBS_GROUP;
 
 __global__ __launch_bounds__(256) void gibbs_prepare_kernel(const double* __restrict__ B, const double* __restrict__ Ft,
                                                             const int32_t* __restrict__ off,
