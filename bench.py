@@ -163,7 +163,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=1_000_000, help="locations per GPU")
+    ap.add_argument("--n", "--n-per-gpu", dest="n", type=int, default=1_000_000, help="locations per GPU")
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=["exponential", "matern32"])
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
@@ -173,6 +173,8 @@ def main():
     ap.add_argument("--layout", default="storage", choices=["storage", "natural"],
                     help="storage: per-location arrays relabelled into Z-order storage (default); natural: input rows")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="testing only: every rank on cuda:0 with gloo collectives (the N-rank flow on one GPU)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
@@ -182,11 +184,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse_on_one_gpu:
+        local_rank = 0  # rehearsal of the N-rank flow on a one-GPU box (gloo collectives)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ  # launched by torch.distributed.run
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_on_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     sigma2, phi, tau2 = (float(x) for x in args.theta.split(","))
     cov = Covariance(args.kind, sigma2, phi, tau2)
