@@ -193,3 +193,41 @@ def test_profile_loglik_and_fit(dev, c_oracle):
     assert res["loglik"] >= ll
     assert abs(res["mu"] - mu) < 1.0 and 0.5 < s2 / sigma2 < 2.0 and 0.4 < ph / phi < 2.5 and 0.3 < t2 / tau2 < 3.0
     assert g.cov.theta == res["theta"]
+
+
+def _splitmix_uniforms(seed, count):
+    """The SplitMix64 stream of examples/capi_demo.c as numpy uniforms in [0, 1)."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, count + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def test_capi_demo_plain_c_caller(dev, c_oracle):
+    """A plain C program (examples/capi_demo.c, built by build()) drives the C ABI with
+    hipMalloc'd buffers -- no Python, no torch -- and gets the oracle's log-likelihood."""
+    import os
+    import subprocess
+
+    from pynngp_amd import _lib
+
+    exe = os.path.join(os.path.dirname(_lib.LIB_PATH), "capi_demo")
+    assert os.path.exists(exe), "capi_demo not built (make -C pynngp_amd/csrc)"
+    n, m, seed = 20000, 15, 5
+    out = subprocess.run([exe, str(n), str(m), str(seed)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    f = out.stdout.split()
+    ll, first_bad, F_last = float(f[1]), int(f[3]), float(f[5])
+    u = _splitmix_uniforms(seed, 2 * n + 2 * n)
+    coords = u[: 2 * n].reshape(n, 2)
+    u1, u2 = u[2 * n::2] + 2.0 ** -54, u[2 * n + 1::2]
+    v = np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586 * u2)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _, Fo, po = c_oracle.c_bf_sweep(coords, nbr, "exponential", (1.0, 30.0, 0.1), v)
+    llo = c_oracle.loglik_from_partials(po, n)
+    assert first_bad == -1
+    assert abs(F_last - Fo[-1]) <= 1e-10 * Fo[-1]
+    assert abs(ll - llo) <= 1e-9 * abs(llo), (ll, llo)
