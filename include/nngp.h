@@ -32,6 +32,7 @@ extern "C" {
 
 #define NNGP_OK 0
 #define NNGP_EINVAL (-1)    /* bad argument (shape, range, null pointer, small workspace) */
+#define NNGP_ENOTPD (-2)    /* a location's C_N / F was not positive definite (nngp_check_partials) */
 #define NNGP_EHIP (-3)      /* a HIP runtime call or kernel launch failed */
 #define NNGP_EUNSUP (-4)    /* unsupported configuration (e.g. m > 63) */
 
@@ -211,6 +212,14 @@ size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
                      const double *X, int32_t p, const double *w, double *out, void *workspace,
                      size_t workspace_bytes, void *stream);
+
+/* Host helper for callers that synchronise ("-2 means a non-positive
+ * pivot; report the first bad index through an out-param"): given host-resident
+ * partials of a finished sweep, returns NNGP_OK, NNGP_ENOTPD with *first_bad_row = the
+ * first location whose pivot / F was not > 0, or NNGP_EINVAL with *first_bad_index = the
+ * first location with an out-of-range neighbour index (either out-param may be NULL;
+ * -1 when not applicable). */
+int nngp_check_partials(const double *partials_host, int64_t *first_bad_row, int64_t *first_bad_index);
 
 /* Host helper: -1/2 (n_rows log 2 pi + p[0] + p[1]) from host-resident partials. */
 double nngp_loglik_from_partials(const double *partials_host, int64_t n_rows);

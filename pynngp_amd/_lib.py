@@ -27,6 +27,7 @@ SYMBOLS = (
     "nngp_bf_sweep",
     "nngp_bf_cross",
     "nngp_loglik_from_partials",
+    "nngp_check_partials",
     "nngp_row_order_workspace_bytes",
     "nngp_row_order",
     "nngp_combine_partials",
@@ -106,6 +107,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
+    lib.nngp_check_partials.argtypes = [P, P, P]
+    lib.nngp_check_partials.restype = ctypes.c_int
     lib.nngp_loglik_from_partials.argtypes = [P, I64]
     lib.nngp_loglik_from_partials.restype = D
     _lib = lib

@@ -52,6 +52,15 @@ const char* nngp_version(void) { return "pynngp_amd 0.1.0 gfx950"; }
 
 const char* nngp_last_error(void) { return g_err; }
 
+int nngp_check_partials(const double* p, int64_t* first_bad_row, int64_t* first_bad_index) {
+    if (p == nullptr) return fail(NNGP_EINVAL, "partials must be non-null");
+    if (first_bad_row != nullptr) *first_bad_row = p[2] >= 0.0 ? (int64_t)p[2] : -1;
+    if (first_bad_index != nullptr) *first_bad_index = p[3] >= 0.0 ? (int64_t)p[3] : -1;
+    if (p[3] >= 0.0) return fail(NNGP_EINVAL, "neighbour index out of range at location %lld", (long long)p[3]);
+    if (p[2] >= 0.0) return fail(NNGP_ENOTPD, "C_N or F not positive definite at location %lld", (long long)p[2]);
+    return NNGP_OK;
+}
+
 double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
     return -0.5 * ((double)n_rows * 1.8378770664093453 + p[0] + p[1]);
 }

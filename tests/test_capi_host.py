@@ -114,3 +114,21 @@ def test_no_cpu_fallback():
         _lib.knn_prior(c, 3)
     with pytest.raises(_lib.NNGPExtensionError, match="no CPU fallback"):
         _lib.bf_sweep(c, torch.zeros((4, 3), dtype=torch.int32), 0, "exponential", 1.0, 1.0)
+
+
+def test_check_partials_codes(lib):
+    """-2 for a non-positive pivot with the first bad location reported."""
+    import ctypes
+
+    import numpy as np
+
+    def run(p):
+        a = np.asarray(p, dtype=np.float64)
+        r, i = ctypes.c_int64(7), ctypes.c_int64(7)
+        rc = lib.nngp_check_partials(a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(r), ctypes.byref(i))
+        return rc, r.value, i.value
+
+    assert run([1.0, 2.0, -1.0, -1.0]) == (0, -1, -1)
+    assert run([1.0, 2.0, 1234.0, -1.0]) == (-2, 1234, -1)
+    assert b"1234" in lib.nngp_last_error()
+    assert run([1.0, 2.0, 5.0, 99.0]) == (-1, 5, 99)
