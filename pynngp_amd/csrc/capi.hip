@@ -30,11 +30,12 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // (tools/algo_table.py; DESIGN.md 4, profiles/r01d/algo_table.jsonl): one lane per
 // location while the joint block still leaves room for latency hiding (m <= 10; the
 // blocked pair kernel is within 2-7 % there), the 2x2-blocked two-lane kernel for
-// 11 <= m <= 20, one wavefront per location above.
+// 11 <= m <= 24 (~10x the wavefront kernel even at one wave per SIMD), one wavefront
+// per location above.
 int resolve_algo(int32_t algo, int32_t m) {
     if (algo != NNGP_ALGO_AUTO) return algo;
     if (m >= 1 && m <= 10) return nngp::kAlgoLane;
-    if (m >= 11 && m <= 20) return nngp::kAlgoPairB;
+    if (m >= 11 && m <= 24) return nngp::kAlgoPairB;
     return nngp::kAlgoWave;
 }
 

@@ -68,7 +68,7 @@ CASES = [
 PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
 QUAD_M = (15, 16, 20)  # and for the 4-lane kernel
 GROUP_M = QUAD_M
-PAIRB_M = tuple(range(1, 21))  # and for the 2x2-blocked 2-lane kernel
+PAIRB_M = tuple(range(1, 25))  # and for the 2x2-blocked 2-lane kernel
 
 
 @pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad", "pairb"])

@@ -37,7 +37,7 @@ for m in range(lo, hi + 1):
     algos = ["lane"] if m <= 16 else []
     algos += ["pair"] if 10 <= m <= 20 else []
     algos += ["quad"] if m in (15, 16, 20) else []
-    algos += ["pairb"] if 1 <= m <= 20 else []
+    algos += ["pairb"] if 1 <= m <= 24 else []
     algos += ["wave"]
     wss = {a: _lib.bf_workspace(args.n, m, a, dev) for a in algos}
 
