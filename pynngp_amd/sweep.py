@@ -141,6 +141,25 @@ class ShardedLogLik:
         _raise_on_bad(p)
         return -0.5 * (self.n * LOG_2PI + p[0] + p[1])
 
+    def loglik_scan(self, covs, values: torch.Tensor, values_layout: str = "input") -> list:
+        """Global log-likelihoods at many covariances (a grid / profile-likelihood scan, a
+        batch of MH proposals) with ONE host synchronisation: the sweeps run back to back
+        and each sweep's all-gather overlaps the next sweep (:class:`PipelinedCombine`)."""
+        covs = list(covs)
+        if self.layout == "storage" and values is not None and values_layout == "input":
+            values = self.to_storage(values, out=self._vstore)
+            values_layout = "storage"
+        pipe = PipelinedCombine(self, len(covs))
+        for k, cov in enumerate(covs):
+            self.local_partials(cov, values, False, values_layout, out=pipe.local[k])
+            pipe.exchange(k)
+        res = pipe.finish().cpu().numpy()
+        out = []
+        for p in res:
+            _raise_on_bad(p)
+            out.append(-0.5 * (self.n * LOG_2PI + p[0] + p[1]))
+        return out
+
     @property
     def rows_input(self) -> torch.Tensor:
         """Input-order location index of each local row of B / F (int64)."""

@@ -231,3 +231,19 @@ def test_capi_demo_plain_c_caller(dev, c_oracle):
     assert first_bad == -1
     assert abs(F_last - Fo[-1]) <= 1e-10 * Fo[-1]
     assert abs(ll - llo) <= 1e-9 * abs(llo), (ll, llo)
+
+
+def test_loglik_scan_matches_single_calls(dev):
+    """ShardedLogLik.loglik_scan (pipelined sweeps, one host sync) equals one loglik call per theta."""
+    from pynngp_amd import Covariance, ShardedLogLik
+
+    rng = np.random.default_rng(23)
+    n = 50000
+    c = torch.from_numpy(rng.uniform(size=(n, 2))).to(dev)
+    v = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    for layout in ("natural", "storage"):
+        sh = ShardedLogLik(c, 15, layout=layout)
+        covs = [Covariance("exponential", 1.0, phi, 0.1) for phi in (5.0, 10.0, 20.0, 40.0)]
+        scan = sh.loglik_scan(covs, v)
+        single = [sh.loglik(cv, v) for cv in covs]
+        assert scan == single
