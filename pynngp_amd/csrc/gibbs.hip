@@ -294,8 +294,16 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int32_t* __restrict__
     const bool live = g < n_members;
     const int64_t i = members[live ? g : n_members - 1];
     const int32_t e0 = off[i], e1 = live ? off[i + 1] : off[i];
-    double acc = 0.0;
-    for (int32_t e = e0 + l; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
+    // first kGroup children in registers (child index, B, r_j): the scatter below reuses
+    // them without reloading (no other member of this colour touches r_j); more children
+    // than lanes (rare) take the generic loops
+    const int32_t ef = e0 + l;
+    const bool has = ef < e1;
+    const int64_t jf = has ? (int64_t)rev_j[ef] : 0;
+    const double bf = has ? Brev[ef] : 0.0;
+    const double rf = has ? r[jf] : 0.0;
+    double acc = has ? Grev[ef] * rf : 0.0;
+    for (int32_t e = ef + kGroup; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
 #pragma unroll
     for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i];
@@ -309,7 +317,8 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int32_t* __restrict__
         w[i] = wn;
         r[i] = ri + dw;
     }
-    for (int32_t e = e0 + l; e < e1; e += kGroup) {
+    if (has) r[jf] = fma(-bf, dw, rf);
+    for (int32_t e = ef + kGroup; e < e1; e += kGroup) {
         const int64_t j = rev_j[e];
         r[j] = fma(-Brev[e], dw, r[j]);
     }
