@@ -201,3 +201,25 @@ int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t
     free(quad);
     return 0;
 }
+
+/* Draw w ~ NNGP(0, C~) by forward substitution through the DAG the neighbour sets
+ * define: w_i = sum_k B_ik w_{N(i)_k} + sqrt(F_i) eps_i, in location order (every
+ * neighbour of i precedes i).  This is the density the B/F sweep evaluates
+ * (the factorisation behind _Bsi/_Fsi nngp.py:73-90); the
+ * reference has no simulator.  Used by the tests to draw large fields whose law is
+ * exactly the NNGP (a dense GP draw is out of reach at N = 1e6). */
+int oracle_nngp_simulate(const int32_t *nbr, const double *B, const double *F, int64_t n, int32_t m,
+                         const double *eps, double *w) {
+    for (int64_t i = 0; i < n; ++i) {
+        double acc = 0.0;
+        for (int32_t k = 0; k < m; ++k) {
+            int32_t j = nbr[i * m + k];
+            if (j < 0) continue;
+            if (j >= i) return -1;
+            acc += B[i * m + k] * w[j];
+        }
+        if (!(F[i] > 0.0)) return -2;
+        w[i] = acc + sqrt(F[i]) * eps[i];
+    }
+    return 0;
+}

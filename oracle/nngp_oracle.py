@@ -245,6 +245,8 @@ def load_c_oracle():
                                     ctypes.c_int64, ctypes.c_int64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
     lib.oracle_num_threads.restype = ctypes.c_int
+    lib.oracle_nngp_simulate.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int32, P, P]
+    lib.oracle_nngp_simulate.restype = ctypes.c_int
     _C = lib
     return lib
 
@@ -281,6 +283,21 @@ def c_bf_sweep(coords, nbr, kind, theta, values=None, i0=0, want_bf=True):
     if rc != 0:
         raise RuntimeError(f"oracle_bf_sweep failed: {rc}")
     return B, F, partials
+
+
+def c_nngp_simulate(nbr, B, F, eps):
+    """w ~ NNGP by forward substitution (oracle_nngp_simulate): w_i = B_i w_N(i) + sqrt(F_i) eps_i."""
+    lib = load_c_oracle()
+    nbr = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, m = nbr.shape
+    B = np.ascontiguousarray(B, dtype=np.float64)
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    eps = np.ascontiguousarray(eps, dtype=np.float64)
+    w = np.zeros(n)
+    rc = lib.oracle_nngp_simulate(_ptr(nbr), _ptr(B), _ptr(F), n, m, _ptr(eps), _ptr(w))
+    if rc != 0:
+        raise RuntimeError(f"oracle_nngp_simulate failed: {rc}")
+    return w
 
 
 def c_bf_cross(ref, query, nbr, kind, theta, ref_values=None, query_values=None, q0=0):

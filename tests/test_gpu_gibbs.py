@@ -221,3 +221,36 @@ def test_precomputed_normals_same_chain(dev):
         _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, 1.3, 0.4, yres, w2, r2, s["off"], s["rev_j"], 77,
                            sweep, z=z)
     assert torch.equal(w1, w2) and torch.equal(r1, r2)
+
+
+@pytest.mark.timeout(300)
+def test_seqnngp_config5_scale_stationary(dev):
+    """Config 5's size (N = 1e6, m = 15): a field drawn exactly from the NNGP (forward
+    simulation through B/F at the true parameters, oracle_nngp_simulate) and a chain
+    started at the truth stays at the truth: at this N the posterior is tight, so the
+    posterior means must sit within a few percent of the generating values."""
+    from oracle import nngp_oracle as O
+    from pynngp_amd import Priors, SeqNNGP, _lib
+
+    n, m = 1_000_000, 15
+    sigma2, phi, tau2, beta = 1.0, 30.0, 0.1, np.array([1.0, -0.5])
+    rng = np.random.default_rng(55)
+    c = rng.uniform(size=(n, 2))
+    ct = torch.from_numpy(c).to(dev)
+    nbr = _lib.knn_prior(ct, m)
+    B, F, _ = _lib.bf_sweep(ct, nbr, 0, "exponential", sigma2, phi, 0.0)
+    w = O.c_nngp_simulate(nbr.cpu().numpy(), B.cpu().numpy(), F.cpu().numpy(), rng.standard_normal(n))
+    X = np.column_stack([np.ones(n), rng.standard_normal(n)])
+    y = X @ beta + w + np.sqrt(tau2) * rng.standard_normal(n)
+    pri = Priors(sigma2_ig=(2.0, 1.0), tau2_ig=(2.0, 0.1), phi_unif=(1.0, 100.0))
+    s = SeqNNGP(c, y, X, m=m, priors=pri, sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.004, seed=9,
+                device=dev, w_init=w)
+    res = s.sample(600, burn=200, keep_w_mean=True)
+    assert 0.05 < res["phi_accept_rate"] < 0.95
+    assert abs(res["sigma2"].mean() / sigma2 - 1) < 0.05
+    assert abs(res["tau2"].mean() / tau2 - 1) < 0.05
+    assert abs(res["phi"].mean() / phi - 1) < 0.1
+    assert abs(res["beta"][:, 1].mean() - beta[1]) < 0.01
+    assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.9
+    print(f"N=1e6 chain: sigma2 {res['sigma2'].mean():.4f} tau2 {res['tau2'].mean():.4f} "
+          f"phi {res['phi'].mean():.3f} beta {res['beta'].mean(0)} accept {res['phi_accept_rate']:.2f}")
