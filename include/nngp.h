@@ -186,13 +186,17 @@ int nngp_combine_partials(const double *gathered, int32_t world, double *partial
  *   `members` (device) lists the locations grouped by colour, color_off_host
  *   (host, n_colors + 1) delimits them.  r (n,) holds the residuals
  *   w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
- *   yres = y - X beta.  z: NULL (Philox4x32-10 normals keyed by seed, counter
+ *   yres = y - X beta.  noise_w: NULL (homoscedastic noise, variance tau2) or n
+ *   positive weights h_i, the noise variance of location i being tau2 / h_i (e.g.
+ *   h_i = 1 / eps_i^2 for the reference's per-point measurement sigmas, nngp.py:9).
+ *   z: NULL (Philox4x32-10 normals keyed by seed, counter
  *   (location, sweep)) or n given standard normals (for testing).
  * nngp_gibbs_normals: z[i] = the Philox4x32-10 normal the sweep would draw for
  *   (seed, location i, sweep), for all n locations in one parallel pass; passing it
  *   as nngp_gibbs_w_sweep's z gives the bit-identical chain with shorter colour steps.
- * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum (yres_i - w_i)^2,
- *   out[2 + c] = sum_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p)).
+ * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,
+ *   out[2 + c] = sum_i h_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p));
+ *   h_i = noise_w[i], or 1 when noise_w is NULL.
  * ------------------------------------------------------------------------- */
 size_t nngp_reverse_workspace_bytes(int64_t n, int32_t m);
 int nngp_reverse_neighbors(const int32_t *nbr, int64_t n, int32_t m, int32_t *off, int32_t *rev_j, int32_t *rev_k,
@@ -204,14 +208,14 @@ int nngp_gibbs_prepare(const double *B, const double *Ft, const int32_t *off, co
                        const int32_t *rev_k, const int32_t *order, int64_t n, int32_t m, void *prep,
                        size_t prep_bytes, void *stream);
 int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, int32_t n_colors, const void *prep,
-                       int64_t n, int32_t m, double sigma2, double tau2, const double *yres, double *w, double *r,
-                       const int32_t *off, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
-                       void *stream);
+                       int64_t n, int32_t m, double sigma2, double tau2, const double *yres, const double *noise_w,
+                       double *w, double *r, const int32_t *off, const int32_t *rev_j, const double *z, uint64_t seed,
+                       uint64_t sweep, void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
-                     const double *X, int32_t p, const double *w, double *out, void *workspace,
-                     size_t workspace_bytes, void *stream);
+                     const double *X, int32_t p, const double *w, const double *noise_w, double *out,
+                     void *workspace, size_t workspace_bytes, void *stream);
 
 /* Host helper for callers that synchronise ("-2 means a non-positive
  * pivot; report the first bad index through an out-param"): given host-resident

@@ -98,13 +98,13 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_prep_bytes.restype = SZ
     lib.nngp_gibbs_prepare.argtypes = [P, P, P, P, P, P, I64, I32, P, SZ, P]
     lib.nngp_gibbs_prepare.restype = ctypes.c_int
-    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P]
+    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, P, U64, U64, P]
     lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
     lib.nngp_gibbs_normals.argtypes = [I64, U64, U64, P, P]
     lib.nngp_gibbs_normals.restype = ctypes.c_int
     lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]
     lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
-    lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, SZ, P]
+    lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_check_partials.argtypes = [P, P, P]
@@ -418,18 +418,28 @@ def gibbs_prepare(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: t
     return prep
 
 
+def _check_noise_w(noise_w: Optional[torch.Tensor], n: int) -> None:
+    if noise_w is not None and (noise_w.dtype != torch.float64 or noise_w.shape != (n,)
+                                or not noise_w.is_contiguous()):
+        raise ValueError(f"noise_w must be a contiguous float64 ({n},) tensor")
+
+
 def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: int, sigma2: float,
                   tau2: float, yres: torch.Tensor, w: torch.Tensor, r: torch.Tensor, off: torch.Tensor,
-                  rev_j: torch.Tensor, seed: int, sweep: int, z: Optional[torch.Tensor] = None) -> None:
+                  rev_j: torch.Tensor, seed: int, sweep: int, z: Optional[torch.Tensor] = None,
+                  noise_w: Optional[torch.Tensor] = None) -> None:
     """One colour-ordered sweep of w_i | rest, in place on w and r (see include/nngp.h);
-    ``prep`` from :func:`gibbs_prepare` for the current B / Ft."""
+    ``prep`` from :func:`gibbs_prepare` for the current B / Ft; ``noise_w`` (n,) optional
+    weights h_i (noise variance tau2 / h_i)."""
     import numpy as np
 
-    dev = _require_gpu(members, prep, yres, w, r, off, rev_j, z)
+    dev = _require_gpu(members, prep, yres, w, r, off, rev_j, z, noise_w)
+    _check_noise_w(noise_w, w.shape[0])
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
     n = w.shape[0]
     _check(load().nngp_gibbs_w_sweep(_ptr(members), co.ctypes.data, len(co) - 1, _ptr(prep), n, int(m),
-                                     float(sigma2), float(tau2), _ptr(yres), _ptr(w), _ptr(r), _ptr(off), _ptr(rev_j),
+                                     float(sigma2), float(tau2), _ptr(yres), _ptr(noise_w), _ptr(w), _ptr(r), _ptr(off),
+                                     _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
 
@@ -446,9 +456,11 @@ def gibbs_normals(z: torch.Tensor, seed: int, sweep: int) -> torch.Tensor:
 
 def gibbs_stats(r: torch.Tensor, Ft: torch.Tensor, yres: torch.Tensor, y: torch.Tensor, X: Optional[torch.Tensor],
                 w: torch.Tensor, out: Optional[torch.Tensor] = None,
-                workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[sum r^2/Ft, sum (yres - w)^2, X^T (y - w)...] as a float64 device tensor (2 + p,)."""
-    dev = _require_gpu(r, Ft, yres, y, X, w)
+                workspace: Optional[torch.Tensor] = None, noise_w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[sum r^2/Ft, sum h (yres - w)^2, X^T H (y - w)...] as a float64 device tensor (2 + p,);
+    h = ``noise_w`` (n,) or 1."""
+    dev = _require_gpu(r, Ft, yres, y, X, w, noise_w)
+    _check_noise_w(noise_w, r.shape[0])
     n = r.shape[0]
     p = 0 if X is None else X.shape[1]
     lib = load()
@@ -456,6 +468,6 @@ def gibbs_stats(r: torch.Tensor, Ft: torch.Tensor, yres: torch.Tensor, y: torch.
     need = lib.nngp_gibbs_stats_workspace_bytes(n, p)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
-    _check(lib.nngp_gibbs_stats(n, _ptr(r), _ptr(Ft), _ptr(yres), _ptr(y), _ptr(X), p, _ptr(w), _ptr(out),
+    _check(lib.nngp_gibbs_stats(n, _ptr(r), _ptr(Ft), _ptr(yres), _ptr(y), _ptr(X), p, _ptr(w), _ptr(noise_w), _ptr(out),
                                 _ptr(workspace), workspace.numel(), _stream(dev)), "nngp_gibbs_stats")
     return out

@@ -188,9 +188,9 @@ int nngp_gibbs_prepare(const double* B, const double* Ft, const int32_t* off, co
 }
 
 int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, int32_t n_colors, const void* prep,
-                       int64_t n, int32_t m, double sigma2, double tau2, const double* yres, double* w, double* r,
-                       const int32_t* off, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
-                       void* stream) {
+                       int64_t n, int32_t m, double sigma2, double tau2, const double* yres, const double* noise_w,
+                       double* w, double* r, const int32_t* off, const int32_t* rev_j, const double* z, uint64_t seed,
+                       uint64_t sweep, void* stream) {
     if (members == nullptr || color_off_host == nullptr || prep == nullptr || yres == nullptr || w == nullptr ||
         r == nullptr || off == nullptr || (m > 0 && rev_j == nullptr))
         return fail(NNGP_EINVAL, "null pointer argument");
@@ -198,8 +198,8 @@ int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, in
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
     if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
-    hipError_t e = nngp::gibbs_w_sweep_launch(members, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres, w, r,
-                                              off, rev_j, z, seed, sweep, (hipStream_t)stream);
+    hipError_t e = nngp::gibbs_w_sweep_launch(members, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres, noise_w,
+                                              w, r, off, rev_j, z, seed, sweep, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
     return NNGP_OK;
 }
@@ -217,14 +217,16 @@ size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p) {
 }
 
 int nngp_gibbs_stats(int64_t n, const double* r, const double* Ft, const double* yres, const double* y, const double* X,
-                     int32_t p, const double* w, double* out, void* workspace, size_t workspace_bytes, void* stream) {
+                     int32_t p, const double* w, const double* noise_w, double* out, void* workspace,
+                     size_t workspace_bytes, void* stream) {
     if (r == nullptr || Ft == nullptr || yres == nullptr || w == nullptr || out == nullptr || workspace == nullptr ||
         (p > 0 && (X == nullptr || y == nullptr)))
         return fail(NNGP_EINVAL, "null pointer argument");
     if (n < 1 || p < 0 || p > 62) return fail(NNGP_EINVAL, "bad n or p");
     const size_t need = nngp::gibbs_stats_workspace_bytes(n, p);
     if (workspace_bytes < need) return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
-    hipError_t e = nngp::gibbs_stats_launch(n, r, Ft, yres, y, X, p, w, out, workspace, (hipStream_t)stream);
+    hipError_t e = nngp::gibbs_stats_launch(n, r, Ft, yres, y, X, p, w, noise_w, out, workspace,
+                                              (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_stats launch");
     return NNGP_OK;
 }

@@ -89,11 +89,12 @@ hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t
                                 hipStream_t s);
 hipError_t gibbs_w_sweep_launch(const int32_t* members_all, int n_colors, const int32_t* color_off_host,
                                 const void* prep, int64_t n, int m, double sigma2, double tau2,
-                                const double* yres, double* w, double* r, const int32_t* off, const int32_t* rev_j,
-                                const double* z, uint64_t seed, uint64_t sweep, hipStream_t s);
+                                const double* yres, const double* noise_w, double* w, double* r, const int32_t* off,
+                                const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep, hipStream_t s);
 size_t gibbs_stats_workspace_bytes(int64_t n, int p);
 hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
-                              const double* X, int p, const double* w, double* out, void* workspace, hipStream_t s);
+                              const double* X, int p, const double* w, const double* noise_w, double* out,
+                              void* workspace, hipStream_t s);
 
 // row-order plan (nngp_row_order): Morton-sorted local rows for cache locality
 size_t row_order_workspace_bytes(int64_t n_rows);

@@ -5,7 +5,7 @@ which calls ``update_wt`` / ``update_ws`` / ``update_y_unobserved`` -- none of t
 exist.  This is the sampler those names describe, for the model of Datta et al.
 (2016) that the reference's B/F docstrings (nngp.py:73-96) come from:
 
-    y = X beta + w + eps,   eps ~ N(0, tau2 I),   w ~ NNGP(0, sigma2 R(phi))
+    y = X beta + w + e,   e_i ~ N(0, tau2 v_i),   w ~ NNGP(0, sigma2 R(phi))
     beta ~ flat,  sigma2 ~ IG(a_s, b_s),  tau2 ~ IG(a_t, b_t),  phi ~ U(phi_lo, phi_hi)
 
 One iteration (``step``):
@@ -18,6 +18,11 @@ One iteration (``step``):
                           (nngp_gibbs_w_sweep; moral-graph colouring, Philox normals);
   4. tau2 | ...          -- IG(a_t + N/2, b_t + |y - X beta - w|^2 / 2);
   5. beta | ...          -- N((X'X)^-1 X'(y - w), tau2 (X'X)^-1).
+v_i = 1 (homoscedastic) unless ``eps`` is given: then v_i = eps_i^2, the reference's
+per-point measurement uncertainties (nngp.py:9, "measurement uncertainties in y",
+stored and never used there); with ``fix_tau2=True`` and tau2 = 1 the noise variances
+are exactly eps_i^2, otherwise tau2 scales them.  Steps 4-5 then use the weights
+h_i = 1/v_i (weighted sums and X' H X).
 Scalars (MH decision, conjugate draws) are drawn on the host from a numpy
 Generator seeded with ``seed``; every per-location operation runs in
 ``libnngp_hip.so``.  Parity: the reference has no sampler ("parity unpinned");
@@ -50,7 +55,7 @@ class SeqNNGP:
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
-                 seed: int = 0, device=None, algo: str = "auto", w_init=None):
+                 seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False):
         self.device = _default_device(device)
         dev = self.device
         self.kind = kind
@@ -67,7 +72,17 @@ class SeqNNGP:
         X0 = to(np.ones((n, 1)) if X is None else np.asarray(X, dtype=np.float64).reshape(n, -1))
         self.p = X0.shape[1]
         Xh = X0.cpu().numpy()
-        self._XtX_inv = np.linalg.inv(Xh.T @ Xh)
+        self.fix_tau2 = bool(fix_tau2)
+        if eps is None:
+            hh = np.ones(n)
+            h0 = None
+        else:
+            ev = np.asarray(eps, dtype=np.float64).reshape(-1)
+            if ev.shape != (n,) or not np.all(np.isfinite(ev)) or not np.all(ev > 0):
+                raise ValueError(f"eps must hold {n} positive finite measurement sigmas")
+            hh = 1.0 / ev ** 2
+            h0 = to(hh)
+        self._XtX_inv = np.linalg.inv((Xh * hh[:, None]).T @ Xh)
         self._XtX_inv_chol = np.linalg.cholesky(self._XtX_inv)
 
         # neighbour sets in the model's (input) order; then every per-location array is
@@ -83,6 +98,7 @@ class SeqNNGP:
         self.coords = coords0[self.perm].contiguous()
         self.y = y0[self.perm].contiguous()
         self.X = X0[self.perm].contiguous()
+        self.noise_w = None if h0 is None else h0[self.perm].contiguous()  # h_i = 1 / eps_i^2, storage order
         nb = nbr0[self.perm].long()
         self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
         self.off, self.rev_j, self.rev_k = _lib.reverse_neighbors(self.nbr)
@@ -100,8 +116,8 @@ class SeqNNGP:
             np.int32)
 
         # state
-        yh = self.y.cpu().numpy()
-        self.beta = self._XtX_inv @ (Xh.T @ yh)
+        # (weighted) least squares start; X, y and the weights in the caller's order
+        self.beta = self._XtX_inv @ ((Xh * hh[:, None]).T @ y0.cpu().numpy())
         self.sigma2 = float(sigma2)
         self.tau2 = float(tau2)
         lo, hi = self.priors.phi_unif
@@ -177,13 +193,15 @@ class SeqNNGP:
         # 3. w | rest (colour sweep, in place on w and r)
         _lib.gibbs_normals(self._z, self.seed, self.iteration)  # the sweep's normals, one parallel pass
         _lib.gibbs_w_sweep(self.members, self.color_off, self._prep, self.m, self.sigma2, self.tau2, self.yres, self.w,
-                           self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z)
-        st = _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats).cpu().numpy()
+                           self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z, noise_w=self.noise_w)
+        st = _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats,
+                              noise_w=self.noise_w).cpu().numpy()
         self.quad = float(st[0])
-        # 4. tau2 | y, beta, w
-        a, b = self.priors.tau2_ig
-        self.tau2 = self._ig(a + 0.5 * n, b + 0.5 * float(st[1]))
-        # 5. beta | y, w, tau2 (flat prior)
+        # 4. tau2 | y, beta, w (weighted residual sum of squares; held fixed on request)
+        if not self.fix_tau2:
+            a, b = self.priors.tau2_ig
+            self.tau2 = self._ig(a + 0.5 * n, b + 0.5 * float(st[1]))
+        # 5. beta | y, w, tau2 (flat prior; weighted least squares)
         mean = self._XtX_inv @ st[2:]
         self.beta = mean + math.sqrt(self.tau2) * (self._XtX_inv_chol @ self.rng.standard_normal(self.p))
         self.yres = self._residual_y(self.beta)

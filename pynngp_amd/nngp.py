@@ -372,7 +372,10 @@ class NNGP:
         update_y_unobserved do not exist in the reference) of the response model
         y = X beta + w + eps on S = T: delegates to :class:`pynngp_amd.SeqNNGP`, created on
         the first call with w initialised to ``ws`` and (sigma2, phi, tau2) from ``cov``
-        (``X`` defaults to an intercept).  Afterwards ``ws`` and ``wt`` hold the current w.
+        (``X`` defaults to an intercept).  ``eps`` (nngp.py:9, "measurement uncertainties in
+        y"), when it is one positive sigma per location, makes the noise heteroscedastic:
+        variance tau2 eps_i^2 (see SeqNNGP; pass ``fix_tau2=True`` with tau2 = 1 for exactly
+        eps_i^2).  Afterwards ``ws`` and ``wt`` hold the current w.
         Returns the sampler (its ``beta, sigma2, tau2, phi`` are the other draws)."""
         if not self._same_sets():
             raise NotImplementedError("oneSample needs refType 'S=T' (w lives on the observed locations)")
@@ -384,6 +387,10 @@ class NNGP:
 
             cv = self._covariance()
             tau2 = cv.tau2 if cv.tau2 > 0 else 0.1 * cv.sigma2
+            if "eps" not in sampler_kw and self.eps is not None:
+                ev = np.asarray(self.eps, dtype=np.float64)
+                if ev.shape == y.shape and np.all(np.isfinite(ev)) and np.all(ev > 0):
+                    sampler_kw["eps"] = ev
             self._sampler = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi,
                                     seed=seed, device=self.device, w_init=np.asarray(self.ws, dtype=np.float64),
                                     **sampler_kw)

@@ -61,23 +61,28 @@ def test_residual_output(dev, m):
     assert abs(q - float(s["p"][1])) <= 1e-10 * abs(q)
 
 
-@pytest.mark.parametrize("n,m,sigma2,tau2", [(400, 5, 1.3, 0.2), (1500, 10, 0.7, 0.05), (3000, 15, 2.0, 1.0)])
-def test_w_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2):
+@pytest.mark.parametrize("n,m,sigma2,tau2,weighted", [(400, 5, 1.3, 0.2, False), (1500, 10, 0.7, 0.05, False),
+                                                      (3000, 15, 2.0, 1.0, False), (1500, 10, 0.7, 0.05, True),
+                                                      (3000, 15, 2.0, 1.0, True)])
+def test_w_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted):
+    """One colour sweep with given normals equals the dense full-conditional sweep;
+    weighted: heteroscedastic noise, variance tau2 / h_i (h = 1 / eps^2)."""
     from pynngp_amd import _lib
 
     s = _setup(dev, n, m, seed=n)
     rng = s["rng"]
     yres = torch.from_numpy(rng.standard_normal(n) * 1.5).to(dev)
     z = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    h = rng.uniform(0.2, 5.0, n) if weighted else np.ones(n)
     nbr, B, F = s["nbr"].cpu().numpy(), s["B"].cpu().numpy(), s["F"].cpu().numpy()
     w0 = s["w"].cpu().numpy().copy()
-    P = G.precision(nbr, B, F * sigma2) + np.eye(n) / tau2
-    b = yres.cpu().numpy() / tau2
+    P = G.precision(nbr, B, F * sigma2) + np.diag(h / tau2)
+    b = yres.cpu().numpy() * h / tau2
     w_ref = G.color_sweep(P, b, w0, s["colors"], z.cpu().numpy())
     w, r = s["w"].clone(), s["R"].clone()
     prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
     _lib.gibbs_w_sweep(s["members"], s["color_off"], prep, m, sigma2, tau2, yres, w, r, s["off"], s["rev_j"], 123, 0,
-                       z=z)
+                       z=z, noise_w=torch.from_numpy(h).to(dev) if weighted else None)
     wh = w.cpu().numpy()
     np.testing.assert_allclose(wh, w_ref, rtol=1e-9, atol=1e-9 * np.abs(w_ref).max())
     # maintained residuals equal the recomputed ones
@@ -147,8 +152,8 @@ def test_philox_normals_moments(dev):
     assert abs(np.corrcoef(z, w2.cpu().numpy())[0, 1]) < 5 / np.sqrt(n)
 
 
-@pytest.mark.parametrize("p", [0, 1, 3])
-def test_gibbs_stats(dev, p):
+@pytest.mark.parametrize("p,weighted", [(0, False), (1, False), (3, False), (0, True), (3, True)])
+def test_gibbs_stats(dev, p, weighted):
     from pynngp_amd import _lib
 
     n = 100003
@@ -156,11 +161,13 @@ def test_gibbs_stats(dev, p):
     mk = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64).to(dev)  # noqa: E731
     r, Ft, yres, y, w = mk(n), mk(n).abs() + 0.1, mk(n), mk(n), mk(n)
     X = mk(n, p) if p else None
-    out = _lib.gibbs_stats(r, Ft, yres, y, X, w).cpu().numpy()
+    hw = mk(n).abs() + 0.05 if weighted else None
+    out = _lib.gibbs_stats(r, Ft, yres, y, X, w, noise_w=hw).cpu().numpy()
     rh, Fh, yr, yh, wh = (t.cpu().numpy() for t in (r, Ft, yres, y, w))
-    exp = [np.sum(rh ** 2 / Fh), np.sum((yr - wh) ** 2)]
+    hh = hw.cpu().numpy() if weighted else np.ones(n)
+    exp = [np.sum(rh ** 2 / Fh), np.sum(hh * (yr - wh) ** 2)]
     if p:
-        exp += list(X.cpu().numpy().T @ (yh - wh))
+        exp += list(X.cpu().numpy().T @ (hh * (yh - wh)))
     np.testing.assert_allclose(out, exp, rtol=1e-11, atol=1e-9)
 
 
@@ -201,6 +208,32 @@ def test_seqnngp_recovers_parameters(dev):
     assert 0.4 < res["phi"].mean() / truth["phi"] < 2.5
     # the posterior mean of w tracks the simulated field
     assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.8
+
+
+def test_seqnngp_heteroscedastic_eps(dev):
+    """Known per-point measurement sigmas (the reference's eps, nngp.py:9) with
+    fix_tau2: the chain recovers the field parameters, and weighting by 1/eps^2 tracks
+    the simulated field better than treating the noise as homoscedastic."""
+    from pynngp_amd import Priors, SeqNNGP
+
+    n = 2500
+    beta = np.array([1.0, -0.5])
+    c, _, X, w = _simulate(n, 1.0, 6.0, 0.0, beta, 4)
+    rng = np.random.default_rng(8)
+    eps = np.where(rng.random(n) < 0.5, 0.05, 1.0)  # half precise, half noisy
+    y = X @ beta + w + eps * rng.standard_normal(n)
+    pri = Priors(sigma2_ig=(2.0, 1.0), tau2_ig=(2.0, 0.1), phi_unif=(0.5, 60.0))
+    het = SeqNNGP(c, y, X, m=10, priors=pri, phi=10.0, tau2=1.0, seed=3, device=dev, phi_tuning=0.1, eps=eps,
+                  fix_tau2=True).sample(2000, burn=800, keep_w_mean=True)
+    assert np.all(het["tau2"] == 1.0)
+    assert 0.5 < het["sigma2"].mean() < 2.0
+    assert 0.4 < het["phi"].mean() / 6.0 < 2.5
+    assert abs(het["beta"][:, 1].mean() - beta[1]) < 0.05
+    hom = SeqNNGP(c, y, X, m=10, priors=pri, phi=10.0, tau2=0.5, seed=3, device=dev,
+                  phi_tuning=0.1).sample(2000, burn=800, keep_w_mean=True)
+    err_het = np.sqrt(np.mean((het["w_mean"] - w) ** 2))
+    err_hom = np.sqrt(np.mean((hom["w_mean"] - w) ** 2))
+    assert err_het < 0.8 * err_hom, (err_het, err_hom)
 
 
 def test_precomputed_normals_same_chain(dev):
