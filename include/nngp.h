@@ -39,11 +39,11 @@ extern "C" {
 #define NNGP_COV_EXPONENTIAL 0 /* sigma2 * exp(-phi d)                  */
 #define NNGP_COV_MATERN32 1    /* sigma2 * (1 + phi d) * exp(-phi d)      */
 
-#define NNGP_ALGO_AUTO 0 /* fastest measured kernel for m (lane m <= 10, pairb 11..24, wave) */
+#define NNGP_ALGO_AUTO 0 /* fastest measured kernel for m (lane m <= 10, pairb 11..24, quad 25..32, wave) */
 #define NNGP_ALGO_LANE 1 /* one lane per location (m <= 16)           */
 #define NNGP_ALGO_WAVE 2 /* one wavefront per location (m <= 63)      */
 #define NNGP_ALGO_PAIR 3 /* two lanes per location (10 <= m <= 20)     */
-#define NNGP_ALGO_QUAD 4 /* four lanes per location (m in 15, 16, 20)  */
+#define NNGP_ALGO_QUAD 4 /* four lanes per location (m in 15, 16, 20, 25..32) */
 #define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked elimination (1 <= m <= 24) */
 
 #define NNGP_MAX_M 63

@@ -36,6 +36,7 @@ int resolve_algo(int32_t algo, int32_t m) {
     if (algo != NNGP_ALGO_AUTO) return algo;
     if (m >= 1 && m <= 10) return nngp::kAlgoLane;
     if (m >= 11 && m <= 24) return nngp::kAlgoPairB;
+    if (m >= 25 && m <= 32) return nngp::kAlgoQuad;  // ~10x bf_wave (tools/algo_table.py)
     return nngp::kAlgoWave;
 }
 

@@ -66,7 +66,7 @@ CASES = [
 
 
 PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
-QUAD_M = (15, 16, 20)  # and for the 4-lane kernel
+QUAD_M = (15, 16, 20) + tuple(range(25, 33))  # and for the 4-lane kernel
 GROUP_M = QUAD_M
 PAIRB_M = tuple(range(1, 25))  # and for the 2x2-blocked 2-lane kernel
 
@@ -100,6 +100,17 @@ def test_bf_pair_all_m(lib, dev, c_oracle, m):
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.0), y, "pair")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "pair")
+
+
+@pytest.mark.parametrize("m", list(range(25, 33)))
+def test_bf_quad_all_m(lib, dev, c_oracle, m):
+    """4-lane kernel at every m it serves by default (25..32), duplicates included."""
+    coords, y = _field(2500, 400 + m)
+    coords[1000:1010] = coords[500]
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.3), y, "quad")
+    _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "quad")
+    _check(dev, lib, c_oracle, coords, nbr, "exponential", (0.8, 30.0, 0.01), None, "auto")
 
 
 @pytest.mark.parametrize("m", list(PAIRB_M))

@@ -36,7 +36,7 @@ for m in range(lo, hi + 1):
     F = torch.empty((args.n,), dtype=torch.float64, device=dev)
     algos = ["lane"] if m <= 16 else []
     algos += ["pair"] if 10 <= m <= 20 else []
-    algos += ["quad"] if m in (15, 16, 20) else []
+    algos += ["quad"] if m in (15, 16, 20) or 25 <= m <= 32 else []
     algos += ["pairb"] if 1 <= m <= 24 else []
     algos += ["wave"]
     wss = {a: _lib.bf_workspace(args.n, m, a, dev) for a in algos}
