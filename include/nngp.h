@@ -180,8 +180,8 @@ int nngp_combine_partials(const double *gathered, int32_t world, double *partial
  *   the w sweeps: B_{j,i} and B_{j,i}/F_j per reverse entry, sum_e B_{j,i}^2/F_j and
  *   1/F_i per location, into `prep` (device, nngp_gibbs_prep_bytes(n, m) bytes,
  *   256-B aligned).  Call it again whenever B / Ft change (a new phi accepted).
- *   order: NULL or a permutation of 0..n-1 to visit the locations in (speed only;
- *   nngp_row_order's Z-order keeps the gathers in L2).
+ *   order: unused (accepted for compatibility; the preparation streams the reverse
+ *   lists in their own order).
  * nngp_gibbs_w_sweep: one sweep of w_i | rest over the colours in order;
  *   `members` (device) lists the locations grouped by colour, color_off_host
  *   (host, n_colors + 1) delimits them.  r (n,) holds the residuals

@@ -203,42 +203,55 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
 // Workgroups are dealt round-robin over the 8 XCDs (private L2s): xcd_logical_block gives
 // each XCD a contiguous chunk of the grid, so spatially adjacent locations (sharing
 // children and reverse-list lines) meet in one L2 (speed only; -4 % per Gibbs iteration).
-// kGroup lanes per location (as the colour kernel): the lanes split the reverse entries
-// (contiguous stores per round), a fixed xor-butterfly sums P_i.  32 measured best for
-// m = 15 (~15 children per location): 8 lanes 1.30, 16 lanes 1.07, 32 lanes 1.05 ms per
-// Gibbs iteration at N = 1e6 -- the colour steps are latency bound.
+// The colour kernel gives kGroup lanes to a location: the lanes split its children, a
+// fixed xor-butterfly sums their terms.  32 measured best for m = 15 (~15 children per
+// location): 8 lanes 1.30, 16 lanes 1.07, 32 lanes 1.05 ms per Gibbs iteration at
+// N = 1e6 -- the colour steps are latency bound.
 #ifndef NNGP_GIBBS_GROUP
 #define NNGP_GIBBS_GROUP 32
 #endif
 constexpr int kGroup = NNGP_GIBBS_GROUP;
 
-__global__ __launch_bounds__(256) void gibbs_prepare_kernel(const double* __restrict__ B, const double* __restrict__ Ft,
-                                                            const int32_t* __restrict__ off,
-                                                            const int32_t* __restrict__ rev_j,
-                                                            const int32_t* __restrict__ rev_k,
-                                                            const int32_t* __restrict__ order, int64_t n, int m,
-                                                            double* __restrict__ Brev, double* __restrict__ Grev,
-                                                            double* __restrict__ P, double* __restrict__ invF) {
+// Two passes, both streaming:
+//   entries: one thread per reverse entry e: Brev[e] = B[j, k], Grev[e] = Brev[e] / Ft[j]
+//            (coalesced rev_j / rev_k reads and Brev / Grev writes, B / Ft gathered from
+//            rows near j's parents in the storage order);
+//   rows:    kRowLanes lanes per location fold P_i over its contiguous reverse range
+//            (fixed order: lane-strided partial sums + a fixed xor-butterfly), 1 / Ft_i.
+// (The first version, kGroup lanes per location doing both, took 267 us at N = 1e6, m = 15:
+// half the lanes idle and every lane's chain rev_j -> B -> divide -> store serial.)
+__global__ __launch_bounds__(256) void gibbs_prepare_entries(const double* __restrict__ B,
+                                                             const double* __restrict__ Ft,
+                                                             const int32_t* __restrict__ rev_j,
+                                                             const int32_t* __restrict__ rev_k,
+                                                             const int32_t* __restrict__ off, int64_t n, int m,
+                                                             double* __restrict__ Brev,
+                                                             double* __restrict__ Grev) {
+    const int64_t e = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (e >= n * (int64_t)m || e >= (int64_t)off[n]) return;  // entries past off[n] are padding
+    const int64_t j = rev_j[e];
+    const double b = B[j * m + rev_k[e]];
+    Brev[e] = b;
+    Grev[e] = b / Ft[j];
+}
+
+constexpr int kRowLanes = 4;
+
+__global__ __launch_bounds__(256) void gibbs_prepare_rows(const double* __restrict__ Ft,
+                                                          const int32_t* __restrict__ off, int64_t n,
+                                                          const double* __restrict__ Brev,
+                                                          const double* __restrict__ Grev, double* __restrict__ P,
+                                                          double* __restrict__ invF) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int64_t g = t / kGroup;
-    const int l = (int)(t % kGroup);
-    const bool live = g < n;
-    const int64_t gc = live ? g : n - 1;
-    // visiting order (speed only): with a spatial order, consecutive locations share
-    // children, so the B / Ft gathers of a block hit L2
-    const int64_t i = order != nullptr ? (int64_t)order[gc] : gc;
-    const int32_t e0 = off[i], e1 = live ? off[i + 1] : off[i];
+    const int64_t i = t / kRowLanes;
+    const int l = (int)(t % kRowLanes);
+    const bool live = i < n;
+    const int64_t ic = live ? i : n - 1;
+    const int32_t e0 = off[ic], e1 = live ? off[ic + 1] : e0;
     double acc = 0.0;
-    for (int32_t e = e0 + l; e < e1; e += kGroup) {
-        const int64_t j = rev_j[e];
-        const double b = B[j * m + rev_k[e]];
-        const double g = b / Ft[j];
-        Brev[e] = b;
-        Grev[e] = g;
-        acc = fma(b, g, acc);
-    }
+    for (int32_t e = e0 + l; e < e1; e += kRowLanes) acc = fma(Brev[e], Grev[e], acc);
 #pragma unroll
-    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    for (int o = kRowLanes / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (live && l == 0) {
         P[i] = acc;
         invF[i] = 1.0 / Ft[i];
@@ -271,8 +284,13 @@ hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t
                                 hipStream_t s) {
     if (n == 0) return hipSuccess;
     const GibbsPrep g = prep_layout(prep, n, m);
-    hipLaunchKernelGGL(gibbs_prepare_kernel, dim3((unsigned)((n * kGroup + 255) / 256)), dim3(256), 0, s, B, Ft,
-                       off, rev_j, rev_k, order, n, m, g.Brev, g.Grev, g.P, g.invF);
+    (void)order;  // both passes stream the reverse lists in storage order; no visiting order needed
+    const int64_t ne = n * (int64_t)m;
+    if (ne > 0)
+        hipLaunchKernelGGL(gibbs_prepare_entries, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
+                           rev_k, off, n, m, g.Brev, g.Grev);
+    hipLaunchKernelGGL(gibbs_prepare_rows, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, Ft, off, n,
+                       g.Brev, g.Grev, g.P, g.invF);
     return hipGetLastError();
 }
 
