@@ -13,8 +13,16 @@
 // query i scans square rings of cells around its own cell, keeping the k best
 // (rdist, j) in a register-resident sorted list, and stops when the k-th best
 // rdist is below the squared distance to the unscanned region (minus a slack
-// that covers cell-assignment rounding).  Queries with small i (few prior points,
-// large search radius) use a brute-force scan of s[0:i] instead.
+// that covers cell-assignment rounding).  Levels: grid L covers only the prefix
+// s[0:n/4^L] (2 points per cell of ITS prefix), and query i scans the grid of the
+// smallest prefix holding all of s[0:i] -- its prior points fill >= 1/4 of that
+// prefix, so ~30 cells suffice at every i (one full-density grid made early, sparse-
+// prior queries scan thousands of cells: 7.2 ms at N = 1e6, m = 15, all of it the
+// slowest waves).  Queries with i < kBruteBelow scan s[0:i] directly.
+// Query order (prior mode): lanes of a wave take queries sorted by (floor(log2 i),
+// Morton code of the cell), so they have similar prior densities (similar ring counts,
+// little divergence) AND neighbouring cells (shared cell-list and point lines in L1/L2);
+// each query still writes its own output row.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <math.h>
@@ -25,6 +33,17 @@
 namespace nngp {
 
 constexpr double kPointsPerCell = 2.0;
+constexpr int64_t kBruteBelow = 1024;      // prior queries i < this: brute force over s[0:i]
+constexpr int64_t kLevelMinPoints = 4096;  // no grid level over fewer points than this
+
+struct KnnLevels {  // kernel-argument view of the plan's grids
+    int n;
+    int64_t np[kKnnMaxLevels];
+    int g[kKnnMaxLevels];
+    const int32_t* cell_start[kKnnMaxLevels];
+    const int32_t* idx_sorted[kKnnMaxLevels];
+    const double2* pts_sorted[kKnnMaxLevels];
+};
 
 struct Bbox {
     double minx, miny, maxx, maxy;
@@ -130,6 +149,33 @@ __global__ __launch_bounds__(256) void gather_sorted(const double2* __restrict__
     if (k < n) pts_sorted[k] = p[idx_sorted[k]];
 }
 
+// bits of x spread to the even positions (x < 2^16)
+__device__ __forceinline__ uint32_t spread_bits(uint32_t x) {
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+// sort key of query position t (prior mode): log2 band of the point index, then the
+// Morton code of its cell coarsened to `cbits` bits per axis (band in the top 5 bits)
+__global__ __launch_bounds__(256) void query_keys(const double2* __restrict__ p, int64_t q0, int64_t nq,
+                                                  const int32_t* __restrict__ rows, const Bbox* __restrict__ box,
+                                                  int gx, int gy, int shift, uint32_t* __restrict__ key,
+                                                  int32_t* __restrict__ pos) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const int64_t i = rows != nullptr ? (int64_t)rows[t] : q0 + t;
+    const Grid g = make_grid(*box, gx, gy);
+    const double2 v = p[i];
+    const uint32_t cx = (uint32_t)cell_coord(v.x, g.minx, g.ivx, gx) >> shift;
+    const uint32_t cy = (uint32_t)cell_coord(v.y, g.miny, g.ivy, gy) >> shift;
+    const uint32_t band = 31u - (uint32_t)__clz((unsigned)(i + 1));  // floor(log2(i + 1)) <= 31
+    key[t] = (band << 27) | ((spread_bits(cx) | (spread_bits(cy) << 1)) & ((1u << 27) - 1));
+    pos[t] = (int32_t)t;
+}
+
 // sklearn euclidean_rdist64 without contraction
 __device__ __forceinline__ double rdist(double qx, double qy, double px, double py) {
     const double t0 = __dsub_rn(qx, px);
@@ -180,13 +226,12 @@ template <int KMAX, bool PRIOR>
 __global__ __launch_bounds__(256) void knn_query_kernel(const double2* __restrict__ coords, int64_t n, int m,
                                                         const double2* __restrict__ query, int64_t q0, int64_t q1,
                                                         const int32_t* __restrict__ rows,
-                                                        int64_t brute_below, const Bbox* __restrict__ box, int gx,
-                                                        int gy, const int32_t* __restrict__ cell_start,
-                                                        const int32_t* __restrict__ idx_sorted,
-                                                        const double2* __restrict__ pts_sorted,
-                                                        int32_t* __restrict__ nbr) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q0 + t >= q1) return;
+                                                        const int32_t* __restrict__ perm,
+                                                        int64_t brute_below, const Bbox* __restrict__ box,
+                                                        const KnnLevels lv, int32_t* __restrict__ nbr) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q0 + u >= q1) return;
+    const int64_t t = perm != nullptr ? (int64_t)perm[u] : u;       // query position (output row)
     const int64_t i = rows != nullptr ? (int64_t)rows[t] : q0 + t;  // PRIOR with a row list: query row t is point rows[t]
     const int64_t limit = PRIOR ? i : n;  // candidates are reference points j < limit
     const int k = (int)(limit < m ? limit : m);
@@ -204,6 +249,20 @@ __global__ __launch_bounds__(256) void knn_query_kernel(const double2* __restric
             top.push(rdist(q.x, q.y, p.x, p.y), (int32_t)jj);
         }
     } else {
+        // the smallest prefix grid holding every candidate (prior: s[0:i]; query mode: level 0)
+        int L = 0;
+        if (PRIOR) {
+#pragma unroll 1
+            for (int l = lv.n - 1; l > 0; --l)
+                if (lv.np[l] >= i) {
+                    L = l;
+                    break;
+                }
+        }
+        const int gx = lv.g[L], gy = lv.g[L];
+        const int32_t* __restrict__ cell_start = lv.cell_start[L];
+        const int32_t* __restrict__ idx_sorted = lv.idx_sorted[L];
+        const double2* __restrict__ pts_sorted = lv.pts_sorted[L];
         const Grid g = make_grid(*box, gx, gy);
         const int cx = cell_coord(q.x, g.minx, g.ivx, gx);
         const int cy = cell_coord(q.y, g.miny, g.ivy, gy);
@@ -265,14 +324,27 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 hipError_t knn_plan(int64_t n_points, KnnPlan* plan) {
     KnnPlan p{};
     p.n_points = n_points;
-    p.gx = p.gy = grid_side(n_points);
-    p.n_cells = (int64_t)p.gx * p.gy;
+    // levels: prefixes n, n/4, n/16, ... down to kLevelMinPoints
+    p.n_levels = 0;
+    for (int64_t np = n_points; p.n_levels < kKnnMaxLevels; np = (np + 3) / 4) {
+        KnnLevel& L = p.lv[p.n_levels++];
+        L.np = np;
+        L.g = grid_side(np);
+        L.n_cells = (int64_t)L.g * L.g;
+        if ((np + 3) / 4 < kLevelMinPoints) break;
+    }
+    p.gx = p.gy = p.lv[0].g;
+    p.n_cells = p.lv[0].n_cells;
     unsigned bits = 1;
     while ((1ll << bits) < p.n_cells) ++bits;
-    size_t tb = 0;
+    size_t tb = 0, tq = 0;
     hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                              (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n_points, 0u, bits);
     if (e != hipSuccess) return e;
+    e = rocprim::radix_sort_pairs((void*)nullptr, tq, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n_points, 0u, 32u);
+    if (e != hipSuccess) return e;
+    if (tq > tb) tb = tq;
     p.sort_temp_bytes = tb;
     size_t off = 0;
     p.off_bbox = off;
@@ -283,12 +355,17 @@ hipError_t knn_plan(int64_t n_points, KnnPlan* plan) {
     off += align256(sizeof(uint32_t) * n_points);
     p.off_idx = off;
     off += align256(sizeof(int32_t) * n_points);
-    p.off_idx_sorted = off;
+    for (int l = 0; l < p.n_levels; ++l) {
+        KnnLevel& L = p.lv[l];
+        L.off_idx_sorted = off;
+        off += align256(sizeof(int32_t) * L.np);
+        L.off_pts_sorted = off;
+        off += align256(2 * sizeof(double) * L.np);
+        L.off_cell_start = off;
+        off += align256(sizeof(int32_t) * (L.n_cells + 1));
+    }
+    p.off_perm = off;
     off += align256(sizeof(int32_t) * n_points);
-    p.off_pts_sorted = off;
-    off += align256(2 * sizeof(double) * n_points);
-    p.off_cell_start = off;
-    off += align256(sizeof(int32_t) * (p.n_cells + 1));
     p.off_sort_temp = off;
     off += align256(tb);
     p.total_bytes = off;
@@ -298,18 +375,15 @@ hipError_t knn_plan(int64_t n_points, KnnPlan* plan) {
 
 template <int KMAX>
 static void launch_query(bool prior, const double* coords, int64_t n, int m, const double* query, int64_t q0,
-                         int64_t q1, const int32_t* rows, int64_t brute_below, const Bbox* box, const KnnPlan& pl,
-                         const int32_t* cell_start, const int32_t* idx_sorted, const double2* pts_sorted, int32_t* nbr,
-                         hipStream_t s) {
+                         int64_t q1, const int32_t* rows, const int32_t* perm, int64_t brute_below, const Bbox* box,
+                         const KnnLevels& lv, int32_t* nbr, hipStream_t s) {
     const dim3 grid((unsigned)((q1 - q0 + 255) / 256)), block(256);
     if (prior)
         hipLaunchKernelGGL((knn_query_kernel<KMAX, true>), grid, block, 0, s, (const double2*)coords, n, m,
-                           (const double2*)query, q0, q1, rows, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
-                           pts_sorted, nbr);
+                           (const double2*)query, q0, q1, rows, perm, brute_below, box, lv, nbr);
     else
         hipLaunchKernelGGL((knn_query_kernel<KMAX, false>), grid, block, 0, s, (const double2*)coords, n, m,
-                           (const double2*)query, q0, q1, rows, brute_below, box, pl.gx, pl.gy, cell_start, idx_sorted,
-                           pts_sorted, nbr);
+                           (const double2*)query, q0, q1, rows, perm, brute_below, box, lv, nbr);
 }
 
 hipError_t knn_launch(bool prior, const double* coords, int64_t n, int m, const double* query, int64_t q0, int64_t q1,
@@ -320,32 +394,62 @@ hipError_t knn_launch(bool prior, const double* coords, int64_t n, int m, const 
     uint32_t* key = (uint32_t*)(w + pl.off_key);
     uint32_t* key_sorted = (uint32_t*)(w + pl.off_key_sorted);
     int32_t* idx = (int32_t*)(w + pl.off_idx);
-    int32_t* idx_sorted = (int32_t*)(w + pl.off_idx_sorted);
-    double2* pts_sorted = (double2*)(w + pl.off_pts_sorted);
-    int32_t* cell_start = (int32_t*)(w + pl.off_cell_start);
     void* temp = (void*)(w + pl.off_sort_temp);
     const double2* p = (const double2*)coords;
-    const unsigned nb = (unsigned)((n + 255) / 256);
 
     hipLaunchKernelGGL(bbox_partial, dim3(256), dim3(256), 0, s, p, n, bpart);
     hipLaunchKernelGGL(bbox_final, dim3(1), dim3(64), 0, s, bpart, 256, box);
-    hipLaunchKernelGGL(cell_keys, dim3(nb), dim3(256), 0, s, p, n, box, pl.gx, pl.gy, key, idx);
-    unsigned bits = 1;
-    while ((1ll << bits) < pl.n_cells) ++bits;
-    size_t tb = pl.sort_temp_bytes;
-    hipError_t e = rocprim::radix_sort_pairs(temp, tb, key, key_sorted, idx, idx_sorted, (size_t)n, 0u, bits, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(cell_bounds, dim3((unsigned)((pl.n_cells + 1 + 255) / 256)), dim3(256), 0, s, key_sorted, n,
-                       pl.n_cells, cell_start);
-    hipLaunchKernelGGL(gather_sorted, dim3(nb), dim3(256), 0, s, p, idx_sorted, n, pts_sorted);
-    // brute force where scanning s[0:i] is cheaper than the grid rings it would need
-    int64_t brute_below = (int64_t)sqrt((double)m * (double)n / kPointsPerCell);
-    if (brute_below < 1024) brute_below = 1024;
-#define NNGP_Q(KM) launch_query<KM>(prior, coords, n, m, query, q0, q1, rows, brute_below, box, pl, cell_start, idx_sorted, pts_sorted, nbr, s)
+    // one grid per level over the prefix s[0:np] (query mode only needs level 0); every
+    // level shares the bounding box and the key / key_sorted / idx scratch
+    KnnLevels lv{};
+    lv.n = prior ? pl.n_levels : 1;
+    hipError_t e = hipSuccess;
+    for (int l = 0; l < lv.n; ++l) {
+        const KnnLevel& L = pl.lv[l];
+        int32_t* idx_sorted = (int32_t*)(w + L.off_idx_sorted);
+        double2* pts_sorted = (double2*)(w + L.off_pts_sorted);
+        int32_t* cell_start = (int32_t*)(w + L.off_cell_start);
+        const unsigned nb = (unsigned)((L.np + 255) / 256);
+        hipLaunchKernelGGL(cell_keys, dim3(nb), dim3(256), 0, s, p, L.np, box, L.g, L.g, key, idx);
+        unsigned bits = 1;
+        while ((1ll << bits) < L.n_cells) ++bits;
+        size_t tb = pl.sort_temp_bytes;
+        e = rocprim::radix_sort_pairs(temp, tb, key, key_sorted, idx, idx_sorted, (size_t)L.np, 0u, bits, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(cell_bounds, dim3((unsigned)((L.n_cells + 1 + 255) / 256)), dim3(256), 0, s, key_sorted,
+                           L.np, L.n_cells, cell_start);
+        hipLaunchKernelGGL(gather_sorted, dim3(nb), dim3(256), 0, s, p, idx_sorted, L.np, pts_sorted);
+        lv.np[l] = L.np;
+        lv.g[l] = L.g;
+        lv.cell_start[l] = cell_start;
+        lv.idx_sorted[l] = idx_sorted;
+        lv.pts_sorted[l] = pts_sorted;
+    }
+    // brute force where scanning s[0:i] is cheaper than any grid
+    int64_t brute_below = kBruteBelow > 8 * (int64_t)m ? kBruteBelow : 8 * (int64_t)m;
+    // prior mode: visit the queries in (log2 band, cell Morton) order (speed only); the cell
+    // sorts' key / key_sorted / idx scratch is free again
+    const int32_t* perm = nullptr;
+    const int64_t nq = q1 - q0;
+    if (prior && nq > 1 && nq <= n) {
+        int cb = 1;
+        while ((1 << cb) < (pl.gx > pl.gy ? pl.gx : pl.gy)) ++cb;
+        const int shift = cb > 13 ? cb - 13 : 0;  // 2 * 13 Morton bits + 5 band bits fit 32
+        int32_t* pos = (int32_t*)(w + pl.off_perm);
+        hipLaunchKernelGGL(query_keys, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, p, q0, nq, rows, box,
+                           pl.gx, pl.gy, shift, key, idx);
+        size_t tq = pl.sort_temp_bytes;
+        e = rocprim::radix_sort_pairs(temp, tq, key, key_sorted, idx, pos, (size_t)nq, 0u, 32u, s);
+        if (e != hipSuccess) return e;
+        perm = pos;
+    }
+#define NNGP_Q(KM) launch_query<KM>(prior, coords, n, m, query, q0, q1, rows, perm, brute_below, box, lv, nbr, s)
     if (m <= 8)
         NNGP_Q(8);
     else if (m <= 16)
         NNGP_Q(16);
+    else if (m <= 24)
+        NNGP_Q(24);
     else if (m <= 32)
         NNGP_Q(32);
     else if (m <= 64)

@@ -59,14 +59,24 @@ int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);
 int64_t bf_wave_blocks(int64_t n_rows);
 
+constexpr int kKnnMaxLevels = 16;
+// one grid over the prefix s[0:np] of the points (level 0: all of them)
+struct KnnLevel {
+    int64_t np;       // points in the prefix
+    int g;            // grid side (g x g cells over the common bounding box)
+    int64_t n_cells;  // g * g
+    size_t off_idx_sorted, off_pts_sorted, off_cell_start;  // byte offsets into the workspace
+};
 struct KnnPlan {
     int64_t n_points;
-    int gx, gy;
-    int64_t n_cells;
+    int gx, gy;       // level 0 grid
+    int64_t n_cells;  // level 0 cells
+    int n_levels;
+    KnnLevel lv[kKnnMaxLevels];
     size_t sort_temp_bytes;
     size_t total_bytes;
-    // byte offsets into the workspace
-    size_t off_bbox, off_key, off_key_sorted, off_idx_sorted, off_pts_sorted, off_cell_start, off_sort_temp, off_idx;
+    // byte offsets into the workspace (level 0's arrays are lv[0].off_*)
+    size_t off_bbox, off_key, off_key_sorted, off_sort_temp, off_idx, off_perm;
 };
 
 hipError_t knn_plan(int64_t n_points, KnnPlan* plan);
