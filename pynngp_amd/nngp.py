@@ -113,13 +113,19 @@ class NNGP:
     def _init_s(self):
         """Reference set S (nngp.py:21-40): 'S=T', ('subset', nRef) or ('random', nRef, bounds)."""
         self.s = reference_set(self.t, self.refType)
-        self._t_dev = torch.as_tensor(np.ascontiguousarray(self.t, dtype=np.float64)).to(self.device)
+        t_host = np.ascontiguousarray(self.t, dtype=np.float64)
+        if not np.all(np.isfinite(t_host)):  # as sklearn's KDTree / KNeighborsRegressor (nngp.py:46,55)
+            raise ValueError("Input contains NaN or infinity (ordinates t)")
+        self._t_dev = torch.as_tensor(t_host).to(self.device)
         if self._t_dev.dim() != 2 or self._t_dev.shape[1] != 2:
             raise ValueError(f"ordinates must be (N, 2), got {tuple(self._t_dev.shape)}")
         if self.s is self.t:
             self._s_dev = self._t_dev
         else:
-            self._s_dev = torch.as_tensor(np.ascontiguousarray(self.s, dtype=np.float64)).to(self.device)
+            s_host = np.ascontiguousarray(self.s, dtype=np.float64)
+            if not np.all(np.isfinite(s_host)):
+                raise ValueError("Input contains NaN or infinity (reference set s)")
+            self._s_dev = torch.as_tensor(s_host).to(self.device)
             if self._s_dev.dim() != 2 or self._s_dev.shape[1] != 2 or self._s_dev.shape[0] < 1:
                 raise ValueError(f"reference set must be (nRef >= 1, 2), got {tuple(self._s_dev.shape)}")
 

@@ -93,6 +93,10 @@ def test_callable_cov_and_errors(dev):
         NNGP(t, y, None, ("grid", 10), 4, None)
     with pytest.raises(ValueError):
         NNGP(t, y, None, "S=X", 4, None)
+    bad = t.copy()
+    bad[7, 1] = np.nan  # sklearn's KDTree raises on non-finite input too
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        NNGP(bad, y, None, "S=T", 4, None)
     dup = t.copy()
     model = NNGP(dup, y, None, "S=T", 4, Covariance("exponential", 1.0, 3.0, 0.0))
     nb = model.nbr.clone()
