@@ -62,7 +62,8 @@ const char *nngp_last_error(void);
  * For every query row i in [q0, q1): the k = min(m, i) nearest points among
  * coords[0:i], ascending fp64 rdist = (0 + t0*t0) + t1*t1 (no FMA), exact
  * ties by lower index, written to nbr[(i - q0) * m + s], s < k; -1 beyond.
- * Requires n_points <= INT32_MAX, 0 <= m <= 64, 0 <= q0 <= q1 <= n_points.
+ * Requires n_points <= INT32_MAX, 0 <= m <= 64, 0 <= q0 <= q1 <= n_points, and
+ * finite coordinates (NaN / inf give unspecified sets; the Python layer rejects them).
  * ------------------------------------------------------------------------- */
 size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m);
 int nngp_knn_prior(const double *coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t *nbr,
