@@ -109,7 +109,9 @@ int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_
  * i.e. pass nbr_sorted); values: (n_points,) or NULL;
  * B, F: may be NULL (log-lik only); R: NULL or (n_rows,) residuals
  * r_i = v_i - B_i v_N(i) (needs values; the Gibbs w-update keeps them current);
- * partials: 4 doubles.
+ * partials: 4 doubles, or NULL to defer the final fold: the per-block records stay in
+ * the workspace and nngp_bf_finalize (same n_rows, m, algo) folds them later, e.g. on
+ * another stream while the next sweep (with another workspace) runs.
  * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, algo) bytes, 256-B aligned.
  * ------------------------------------------------------------------------- */
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo);
@@ -117,6 +119,9 @@ int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, co
                   int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2, const double *values,
                   double *B, double *F, double *R, double *partials, void *workspace, size_t workspace_bytes,
                   int32_t algo, void *stream);
+/* The deferred fold of a sweep run with partials == NULL (fixed order: the same
+ * bits as the in-line fold). */
+int nngp_bf_finalize(const void *workspace, int64_t n_rows, int32_t m, int32_t algo, double *partials, void *stream);
 
 /* ---------------------------------------------------------------------------
  * B/F of query locations t against a reference set S (prediction / kriging at

@@ -26,6 +26,7 @@ SYMBOLS = (
     "nngp_bf_sweep_workspace_bytes",
     "nngp_bf_sweep",
     "nngp_bf_cross",
+    "nngp_bf_finalize",
     "nngp_loglik_from_partials",
     "nngp_check_partials",
     "nngp_row_order_workspace_bytes",
@@ -86,6 +87,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
+    lib.nngp_bf_finalize.argtypes = [P, I64, I32, I32, P, P]
+    lib.nngp_bf_finalize.restype = ctypes.c_int
     lib.nngp_combine_partials.restype = ctypes.c_int
     U64 = ctypes.c_uint64
     lib.nngp_reverse_workspace_bytes.argtypes = [I64, I32]
@@ -225,8 +228,12 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
              algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
              partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
              order: Optional[torch.Tensor] = None,
-             R: Optional[torch.Tensor] = None) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+             R: Optional[torch.Tensor] = None,
+             defer: bool = False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
+
+    ``defer=True`` (needs ``workspace``): the final fold is left to :func:`bf_finalize`
+    on the same workspace (e.g. on another stream); partials is returned as None.
 
     Returns ``(B, F, partials)`` (B, F None when ``want_bf`` is False); partials is a
     float64 device tensor ``[sum log F, sum r^2/F, first bad-pivot row, first bad-index row]``.
@@ -256,9 +263,14 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
         F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
     else:
         B = F = None
-    partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
+    if defer:
+        partials = None
+    else:
+        partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
     need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
     if workspace is None or workspace.numel() < need:
+        if defer:
+            raise ValueError("defer=True needs a workspace of nngp_bf_sweep_workspace_bytes bytes")
         workspace = _workspace(need, dev)
     if R is not None and (R.dtype != torch.float64 or R.shape != (rows,)):
         raise ValueError("R must be float64 (rows,)")
@@ -267,6 +279,17 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
     return B, F, partials
+
+
+def bf_finalize(workspace: torch.Tensor, rows: int, m: int, algo: str = "auto",
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fold the block records a ``bf_sweep(..., defer=True)`` left in ``workspace`` into
+    ``out`` (float64 (4,)), on torch's current stream (nngp_bf_finalize)."""
+    dev = _require_gpu(workspace, out)
+    out = torch.empty(4, dtype=torch.float64, device=dev) if out is None else out
+    _check(load().nngp_bf_finalize(_ptr(workspace), int(rows), int(m), ALGO_CODES[algo], _ptr(out), _stream(dev)),
+           "nngp_bf_finalize")
+    return out
 
 
 def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: str, sigma2: float, phi: float,

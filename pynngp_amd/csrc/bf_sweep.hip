@@ -244,11 +244,23 @@ static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
     }
 }
 
+int64_t bf_record_count(int64_t n_rows, int algo) {
+    if (n_rows == 0) return 0;
+    if (algo == kAlgoLane) return bf_lane_blocks(n_rows);
+    if (algo == kAlgoPairB || algo == kAlgoPair) return bf_group_blocks(n_rows, 2);
+    if (algo == kAlgoQuad) return bf_group_blocks(n_rows, 4);
+    return bf_wave_blocks(n_rows);
+}
+
+hipError_t bf_finalize_launch(const double* bpart, int64_t n_records, double* partials, hipStream_t s) {
+    hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, bpart, n_records, partials);
+    return hipGetLastError();
+}
+
+// a.partials == nullptr: leave the per-block records in a.bpart (bf_finalize_launch later)
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
-    if (a.n_rows == 0) {  // empty shard: partials = [0, 0, -1, -1]
-        hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.bpart, (int64_t)0, a.partials);
-        return hipGetLastError();
-    }
+    if (a.n_rows == 0)  // empty shard: partials = [0, 0, -1, -1]
+        return a.partials != nullptr ? bf_finalize_launch(a.bpart, 0, a.partials, s) : hipSuccess;
     const CovParams P = nngp_cov_params(a.sigma2, a.phi, a.tau2);
     bool ok;
     int64_t nb;
@@ -268,9 +280,8 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     }
     if (!ok) return hipErrorInvalidValue;
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(bf_finalize, dim3(1), dim3(1024), 0, s, a.bpart, nb, a.partials);
-    return hipGetLastError();
+    if (e != hipSuccess || a.partials == nullptr) return e;
+    return bf_finalize_launch(a.bpart, nb, a.partials, s);
 }
 
 }  // namespace nngp

@@ -79,8 +79,8 @@ static int bf_common(const double* coords, int64_t n_points, const double* qcoor
                      double sigma2, double phi, double tau2, const double* values, const double* qvalues, double* B,
                      double* F, double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo,
                      void* stream) {
-    if (coords == nullptr || qcoords == nullptr || partials == nullptr || workspace == nullptr)
-        return fail(NNGP_EINVAL, "coordinates, partials and workspace must be non-null");
+    if (coords == nullptr || qcoords == nullptr || workspace == nullptr)
+        return fail(NNGP_EINVAL, "coordinates and workspace must be non-null");
     if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
     if (m > 0 && n_rows > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null for m > 0");
     if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
@@ -129,6 +129,16 @@ int nngp_bf_cross(const double* ref, int64_t n_ref, const double* query, int64_t
         return fail(NNGP_EINVAL, "query_values need ref_values");
     return bf_common(ref, n_ref, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, ref_values,
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
+}
+
+int nngp_bf_finalize(const void* workspace, int64_t n_rows, int32_t m, int32_t algo, double* partials, void* stream) {
+    if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");
+    if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
+    const int a = resolve_algo(algo, m);
+    hipError_t e = nngp::bf_finalize_launch((const double*)workspace, nngp::bf_record_count(n_rows, a), partials,
+                                            (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "bf_finalize launch");
+    return NNGP_OK;
 }
 
 int nngp_combine_partials(const double* gathered, int32_t world, double* partials, void* stream) {

@@ -359,3 +359,19 @@ def test_config4_sharded_on_one_gpu(lib, dev, c_oracle):
                                             i0=int(inp[0]))
             assert abs(sh.F[rows[0]].item() - Fo[0]) <= RTOL_F * Fo[0]
     assert np.allclose(tot, pw[:2], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("algo", ["auto", "lane", "wave", "quad"])
+def test_deferred_finalize_same_bits(lib, dev, c_oracle, algo):
+    """nngp_bf_sweep with partials = NULL + nngp_bf_finalize (the pipelined benchmark's
+    path) gives exactly the in-line partials, for every record layout."""
+    m = {"auto": 15, "lane": 10, "wave": 15, "quad": 16}[algo]
+    coords, y = _field(20000, 77)
+    nbr = torch.from_numpy(c_oracle.c_knn_prior(coords, m)).to(dev)
+    c, v = torch.from_numpy(coords).to(dev), torch.from_numpy(y).to(dev)
+    _, _, p = lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 20.0, 0.1, values=v, algo=algo)
+    ws = lib.bf_workspace(nbr.shape[0], m, algo, dev)
+    _, _, none = lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 20.0, 0.1, values=v, algo=algo, workspace=ws, defer=True)
+    assert none is None
+    q = lib.bf_finalize(ws, nbr.shape[0], m, algo)
+    assert torch.equal(p, q)
