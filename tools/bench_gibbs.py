@@ -3,7 +3,8 @@
 One iteration = SeqNNGP.step(): MH proposal for phi (one fused B/F sweep + residuals),
 conjugate sigma2, the colour-ordered w sweep, tau2 and beta draws (host scalars).
 Synthetic response data y = 1 + w + eps from the seed; prints one JSON line.
-    python tools/bench_gibbs.py [--n 1000000 --m 15 --iters 50 --warmup 5]
+    python tools/bench_gibbs.py [--n 1000000 --m 15 --iters 300 --warmup 100]
+(100 warm-up iterations: the GPU clock settles over the first ~50 ms of sustained load)
 """
 import argparse
 import json
@@ -20,8 +21,8 @@ from pynngp_amd import SeqNNGP  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1_000_000)
 ap.add_argument("--m", type=int, default=15)
-ap.add_argument("--iters", type=int, default=50)
-ap.add_argument("--warmup", type=int, default=5)
+ap.add_argument("--iters", type=int, default=300)
+ap.add_argument("--warmup", type=int, default=100)
 args = ap.parse_args()
 # several GPUs (torchrun): independent chains, one per GPU ("replicas only")
 world = int(os.environ.get("WORLD_SIZE", "1"))
