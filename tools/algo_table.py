@@ -1,4 +1,4 @@
-"""Time every sweep kernel variant for m = 1..20 (N = 1e6, exponential, Z-order) in one process.
+"""Time every sweep kernel variant for m in a range (N = 1e6, exponential, Z-order) in one process.
 
 Prints one JSON line per (m, algo) with the mean kernel time from HIP events; used
 to choose the NNGP_ALGO_AUTO table in pynngp_amd/csrc/capi.hip.
@@ -21,6 +21,8 @@ ap.add_argument("--ms", default="1-20")
 ap.add_argument("--kind", default="exponential")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--rounds", type=int, default=6)
+ap.add_argument("--settle-ms", type=float, default=80.0,
+                help="back-to-back sweeps before each m's timing (the GPU clock settles over ~50 ms)")
 args = ap.parse_args()
 lo, hi = (int(x) for x in args.ms.split("-"))
 dev = torch.device("cuda", 0)
@@ -47,6 +49,12 @@ for m in range(lo, hi + 1):
     for a in algos:
         for _ in range(2):
             run(a)
+    import time
+    t_end = time.perf_counter() + args.settle_ms * 1e-3
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            run(algos[0])
+        torch.cuda.synchronize()
     times = {a: [] for a in algos}
     # interleaved rounds (clock / thermal drift hits every algo alike); median per algo
     for rnd in range(args.rounds):
