@@ -75,6 +75,20 @@ int oracle_knn_prior(const double *coords, int64_t n, int32_t m, int64_t q0, int
     return 0;
 }
 
+/* Same sets for an explicit list of query rows (parallel over the list): row t of nbr is
+ * the set of location rows[t].  Used for sampled-row checks at N = 1e7, where one call
+ * per row would scan s[0:i] on a single thread. */
+int oracle_knn_prior_rows(const double *coords, int64_t n, int32_t m, const int64_t *rows, int64_t n_rows,
+                          int32_t *nbr) {
+    if (m < 0 || n_rows < 0) return -1;
+    for (int64_t t = 0; t < n_rows; ++t)
+        if (rows[t] < 0 || rows[t] >= n) return -1;
+    int rc = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : rc)
+    for (int64_t t = 0; t < n_rows; ++t) rc |= oracle_knn_prior(coords, n, m, rows[t], rows[t] + 1, nbr + t * m);
+    return rc;
+}
+
 static inline double cov_eval(int kind, double d, double sigma2, double phi) {
     double e = exp(-phi * d);
     if (kind == 1) return sigma2 * (1.0 + phi * d) * e;

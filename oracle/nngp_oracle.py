@@ -241,6 +241,8 @@ def load_c_oracle():
     P = ctypes.c_void_p
     lib.oracle_knn_prior.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, P]
     lib.oracle_knn_prior.restype = ctypes.c_int
+    lib.oracle_knn_prior_rows.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64, P]
+    lib.oracle_knn_prior_rows.restype = ctypes.c_int
     lib.oracle_bf_sweep.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P,
                                     ctypes.c_int64, ctypes.c_int64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
@@ -264,6 +266,18 @@ def c_knn_prior(coords, m, q0=0, q1=None):
     rc = lib.oracle_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle_knn_prior failed: {rc}")
+    return out
+
+
+def c_knn_prior_rows(coords, m, rows):
+    """Prior neighbour sets of the locations ``rows`` (any order), one row each, in parallel."""
+    lib = load_c_oracle()
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    out = np.full((rows.size, m), -1, dtype=np.int32)
+    rc = lib.oracle_knn_prior_rows(_ptr(coords), coords.shape[0], m, _ptr(rows), rows.size, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle_knn_prior_rows failed: {rc}")
     return out
 
 

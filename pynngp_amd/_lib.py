@@ -165,6 +165,16 @@ def _as_coords(coords: torch.Tensor) -> torch.Tensor:
     return coords.contiguous()
 
 
+def _check_out(t: Optional[torch.Tensor], name: str, shape, dev: torch.device) -> None:
+    """Caller-supplied output buffer: float64, the exact shape, contiguous, on dev (the
+    kernel writes through the raw pointer, so a wrong buffer would be written out of bounds)."""
+    if t is None:
+        return
+    if t.dtype != torch.float64 or tuple(t.shape) != tuple(shape) or not t.is_contiguous() or t.device != dev:
+        raise ValueError(f"{name} must be a contiguous float64 {tuple(shape)} tensor on {dev}, got "
+                         f"{t.dtype} {tuple(t.shape)} contiguous={t.is_contiguous()} on {t.device}")
+
+
 def knn_prior(coords: torch.Tensor, m: int, q0: int = 0, q1: Optional[int] = None,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Ordered prior neighbour sets for rows [q0, q1): int32 (q1-q0, m), -1 padded.
@@ -259,6 +269,8 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     lib = load()
     a = ALGO_CODES[algo]
     if want_bf:
+        _check_out(B, "B", (rows, m), dev)
+        _check_out(F, "F", (rows,), dev)
         B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
         F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
     else:
@@ -266,14 +278,16 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     if defer:
         partials = None
     else:
+        _check_out(partials, "partials", (4,), dev)
         partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
     need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
     if workspace is None or workspace.numel() < need:
         if defer:
             raise ValueError("defer=True needs a workspace of nngp_bf_sweep_workspace_bytes bytes")
         workspace = _workspace(need, dev)
-    if R is not None and (R.dtype != torch.float64 or R.shape != (rows,)):
-        raise ValueError("R must be float64 (rows,)")
+    _check_out(R, "R", (rows,), dev)
+    if workspace.device != dev or not workspace.is_contiguous():
+        raise ValueError("workspace must be a contiguous tensor on the sweep's device")
     _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
                              float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
@@ -326,14 +340,16 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
         raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
     lib = load()
     a = ALGO_CODES[algo]
+    _check_out(B, "B", (rows, m), dev)
+    _check_out(F, "F", (rows,), dev)
+    _check_out(partials, "partials", (4,), dev)
+    _check_out(R, "R", (rows,), dev)
     B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
     F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
     partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
     need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
-    if R is not None and (R.dtype != torch.float64 or R.shape != (rows,)):
-        raise ValueError("R must be float64 (rows,)")
     _check(lib.nngp_bf_cross(_ptr(ref), ref.shape[0], _ptr(query), query.shape[0], _ptr(nbr), _ptr(order), rows, m,
                              int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(ref_values),
                              _ptr(query_values), _ptr(B), _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace),

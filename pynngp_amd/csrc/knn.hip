@@ -176,11 +176,16 @@ __global__ __launch_bounds__(256) void query_keys(const double2* __restrict__ p,
     pos[t] = (int32_t)t;
 }
 
-// sklearn euclidean_rdist64 without contraction
+// sklearn euclidean_rdist64 without contraction.  The pragma is what keeps it that way:
+// __dmul_rn / __dadd_rn are plain * and + in this ROCm's headers, and hipcc's default
+// -ffp-contract=fast-honor-pragmas turned t0*t0 + t1*t1 into one v_fmac_f64, which
+// rounds differently from sklearn's (0 + t0*t0) + t1*t1 on near-ties
+// (tests/test_gpu_knn.py::test_knn_fma_sensitive_ties).
 __device__ __forceinline__ double rdist(double qx, double qy, double px, double py) {
-    const double t0 = __dsub_rn(qx, px);
-    const double t1 = __dsub_rn(qy, py);
-    return __dadd_rn(__dmul_rn(t0, t0), __dmul_rn(t1, t1));
+#pragma clang fp contract(off)
+    const double t0 = qx - px;
+    const double t1 = qy - py;
+    return t0 * t0 + t1 * t1;
 }
 
 __device__ __forceinline__ bool key_less(double da, int32_t ia, double db, int32_t ib) {

@@ -66,6 +66,8 @@ class SeqNNGP:
         self.rng = np.random.default_rng(seed)
         to = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
         coords0 = to(coords)
+        if not bool(torch.isfinite(coords0).all()):
+            raise ValueError("coordinates must be finite (NaN / inf would silently decouple locations)")
         y0 = to(y)
         n = y0.shape[0]
         self.n = n
@@ -127,6 +129,7 @@ class SeqNNGP:
         self.w = to(np.zeros(n) if w_init is None else w_init)[self.perm].contiguous()  # storage order
         self.iteration = 0
         self.n_accept = 0
+        self.n_notpd_reject = 0  # phi proposals rejected because their factor was not positive definite
 
         # buffers: current and proposal factors of the unit-variance field
         z = lambda *s: torch.empty(s, dtype=torch.float64, device=dev)  # noqa: E731
@@ -158,7 +161,9 @@ class SeqNNGP:
     @staticmethod
     def _check(p):
         if p[2] >= 0:
-            raise NNGPNumericalError(f"latent NNGP factor not positive definite at location {int(p[2])}")
+            raise NNGPNumericalError(
+                f"latent NNGP factor not positive definite at location {int(p[2])} at the initial phi "
+                "(duplicate or near-duplicate coordinates make C_N singular; remove duplicates or lower phi)")
 
     def _ig(self, a, b):
         return 1.0 / self.rng.gamma(a, 1.0 / b)
@@ -176,7 +181,11 @@ class SeqNNGP:
         if lo <= phi_p <= hi:
             self._sweep_into(phi_p, self._B2, self._Ft2, self._r2)
             ph = self._part.cpu().numpy()
-            self._check(ph)
+        if lo <= phi_p <= hi and ph[2] >= 0:
+            # the proposal's latent factor is not positive definite (near-duplicate locations
+            # with tau2 = 0 and a large phi): zero density there, so the move is rejected
+            self.n_notpd_reject += 1
+        elif lo <= phi_p <= hi:
             l_new = self.loglik_w(ph[0], ph[1], self.sigma2)
             l_old = self.loglik_w(self.sum_logF, self.quad, self.sigma2)
             if math.log(u) < l_new - l_old + math.log(phi_p) - math.log(self.phi):

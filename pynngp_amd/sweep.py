@@ -71,6 +71,8 @@ class ShardedLogLik:
         if layout not in ("natural", "storage"):
             raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
         self.layout = layout
+        if not bool(torch.isfinite(coords).all()):
+            raise ValueError("coordinates must be finite (NaN / inf would silently decouple locations)")
         self.coords = coords
         self.n = coords.shape[0]
         self.m = int(m)

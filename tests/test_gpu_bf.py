@@ -315,52 +315,6 @@ def test_bf_tiny_fields(lib, dev, c_oracle):
             _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 5.0, 0.1), y, algo)
 
 
-def test_config2_full_parity(lib, dev, c_oracle):
-    """BASELINE config 2 at full size: N = 1e5, m = 15, Matern-3/2 (phi = sqrt(3)/0.1),
-    tau2 = 0.1, every row of B / F and the log-likelihood vs the C oracle."""
-    n, m = 100_000, 15
-    coords, y = _field(n, 2)
-    theta = (1.0, float(np.sqrt(3.0) / 0.1), 0.1)
-    nbr = lib.knn_prior(torch.from_numpy(coords).to(dev), m).cpu().numpy()
-    np.testing.assert_array_equal(nbr[:3000], c_oracle.c_knn_prior(coords, m, 0, 3000))
-    _check(dev, lib, c_oracle, coords, nbr, "matern32", theta, y, "auto")
-
-
-def test_config4_sharded_on_one_gpu(lib, dev, c_oracle):
-    """BASELINE config 4's decomposition (N = 1e7, m = 20, 8 shards of the Z-order storage
-    layout) run shard by shard on one GPU: the rank-order sum of the shards' partials equals
-    the one-shard sweep; sampled rows match the oracle on the shards' own neighbour sets."""
-    from pynngp_amd import Covariance, ShardedLogLik
-
-    n, m = 10_000_000, 20
-    rng = np.random.default_rng(1)
-    coords = rng.uniform(0, 1, (n, 2))
-    c = torch.from_numpy(coords).to(dev)
-    v = torch.from_numpy(rng.standard_normal(n)).to(dev)
-    cov = Covariance("exponential", 1.0, 30.0, 0.0)
-    whole = ShardedLogLik(c, m, 0, 1, layout="storage")
-    pw = whole.partials(cov, v).cpu().numpy()
-    tot = np.zeros(2)
-    for r in range(8):
-        sh = ShardedLogLik(c, m, r, 8, layout="storage")
-        p = sh.local_partials(cov, v).cpu().numpy()
-        assert p[2] == -1 and p[3] == -1
-        tot += p[:2]
-        if r in (0, 7):
-            rows = np.random.default_rng(r).integers(0, sh.hi - sh.lo, 300)
-            inp = sh.rows_input.cpu().numpy()[rows]
-            # neighbour sets of the sampled rows, back in input indices, vs brute force
-            nb = sh.perm.long()[sh.nbr[rows].long().clamp(min=0)].cpu().numpy()
-            nb = np.where(sh.nbr[rows].cpu().numpy() >= 0, nb, -1)
-            for t in range(0, 300, 30):
-                i = int(inp[t])
-                np.testing.assert_array_equal(nb[t], c_oracle.c_knn_prior(coords, m, i, i + 1)[0])
-            Bo, Fo, _ = c_oracle.c_bf_sweep(coords, nb.astype(np.int32)[:1], "exponential", cov.theta, None,
-                                            i0=int(inp[0]))
-            assert abs(sh.F[rows[0]].item() - Fo[0]) <= RTOL_F * Fo[0]
-    assert np.allclose(tot, pw[:2], rtol=1e-12, atol=0)
-
-
 @pytest.mark.parametrize("algo", ["auto", "lane", "wave", "quad"])
 def test_deferred_finalize_same_bits(lib, dev, c_oracle, algo):
     """nngp_bf_sweep with partials = NULL + nngp_bf_finalize (the pipelined benchmark's

@@ -85,28 +85,6 @@ def test_knn_edge_sizes_and_ranges(lib, dev, c_oracle):
         np.testing.assert_array_equal(lib.knn_prior(c, 15, q0, q1).cpu().numpy(), full[q0:q1])
 
 
-def test_knn_million_sampled_rows(lib, dev, c_oracle):
-    """Full-size config 3 field: sampled rows bit-exact vs brute force; global invariants on all rows."""
-    n, m = 1_000_000, 15
-    rng = np.random.default_rng(0)
-    coords = rng.uniform(0.0, 1.0, (n, 2))
-    got = lib.knn_prior(torch.from_numpy(coords).to(dev), m).cpu().numpy()
-    rows = np.unique(np.concatenate([np.arange(40), rng.integers(0, n, 300), n - 1 - np.arange(10)]))
-    for i in rows:
-        np.testing.assert_array_equal(got[i], c_oracle.c_knn_prior(coords, m, int(i), int(i) + 1)[0])
-    # invariants: prior, distinct, ascending rdist, count min(i, m)
-    idx = np.arange(n)[:, None]
-    valid = got >= 0
-    assert np.array_equal(valid.sum(1), np.minimum(np.arange(n), m))
-    assert np.all(np.where(valid, got < idx, True))
-    t = coords[np.where(valid, got, 0)] - coords[:, None, :]
-    d = (0.0 + t[..., 0] * t[..., 0]) + t[..., 1] * t[..., 1]
-    d = np.where(valid, d, np.inf)
-    assert np.all(np.diff(d[m:], axis=1) >= 0)
-    s = np.sort(np.where(valid, got, -1), axis=1)
-    assert not np.any((s[:, 1:] == s[:, :-1]) & (s[:, 1:] >= 0))
-
-
 @pytest.mark.parametrize("n_ref,n_q,k", [(5000, 5000, 5), (3000, 700, 15), (4, 10, 5)])
 def test_knn_query_vs_oracle(lib, dev, c_oracle, n_ref, n_q, k):
     rng = np.random.default_rng(n_ref + k)
@@ -116,6 +94,22 @@ def test_knn_query_vs_oracle(lib, dev, c_oracle, n_ref, n_q, k):
     kk = min(k, n_ref)
     np.testing.assert_array_equal(got[:, :kk], c_oracle.knn_all(qry, ref, kk))
     assert np.all(got[:, kk:] == -1)
+
+
+def test_knn_fma_sensitive_ties(lib, dev, c_oracle):
+    """Near-ties whose order flips if rdist is contracted into an FMA (either direction;
+    tests/fma_ties.py): every q must pick p1, as sklearn's unfused rdist and the oracle do,
+    through the brute-force prefix (i < 1024), the grid path and the unrestricted query."""
+    from fma_ties import fma_sensitive_clusters
+
+    coords, expect = fma_sensitive_clusters(3000, dim=2, seed=7)
+    got = lib.knn_prior(torch.from_numpy(coords).to(dev), 1).cpu().numpy()
+    np.testing.assert_array_equal(c_oracle.c_knn_prior(coords, 1)[2::3, 0], expect)
+    np.testing.assert_array_equal(got[2::3, 0], expect)
+    ref = np.delete(coords, np.s_[2::3], axis=0)  # p1, p2 of every cluster: rows 2c, 2c + 1
+    qry = coords[2::3].copy()
+    got = lib.knn_query(torch.from_numpy(ref).to(dev), torch.from_numpy(qry).to(dev), 1).cpu().numpy()
+    np.testing.assert_array_equal(got[:, 0], np.arange(len(qry)) * 2)
 
 
 def test_knn_ops_registered(dev):
