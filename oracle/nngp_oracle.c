@@ -37,9 +37,19 @@ static inline int key_less(double da, int64_t ia, double db, int64_t ib) {
     return da < db || (da == db && ia < ib);
 }
 
-/* nngp.py:49-62 -- brute force over j < i, kept sorted by (rdist, j). */
-int oracle_knn_prior(const double *coords, int64_t n, int32_t m, int64_t q0, int64_t q1, int32_t *nbr) {
-    if (m < 0 || q0 < 0 || q1 > n || q0 > q1) return -1;
+/* sklearn euclidean_rdist64: d = 0; d += t_k * t_k for k = 0 .. dim-1 (no FMA: -ffp-contract=off) */
+static inline double rdist(const double *a, const double *b, int dim) {
+    double d = 0.0;
+    for (int k = 0; k < dim; ++k) {
+        const double t = a[k] - b[k];
+        d += t * t;
+    }
+    return d;
+}
+
+/* nngp.py:49-62 -- brute force over j < i, kept sorted by (rdist, j); coords (n, dim). */
+int oracle_knn_prior(const double *coords, int64_t n, int32_t dim, int32_t m, int64_t q0, int64_t q1, int32_t *nbr) {
+    if (m < 0 || dim < 1 || q0 < 0 || q1 > n || q0 > q1) return -1;
     if (m == 0) return 0;
 #pragma omp parallel
     {
@@ -50,13 +60,9 @@ int oracle_knn_prior(const double *coords, int64_t n, int32_t m, int64_t q0, int
             int32_t *row = nbr + (i - q0) * m;
             int64_t k = i < m ? i : m;
             int64_t cnt = 0;
-            const double qx = coords[2 * i], qy = coords[2 * i + 1];
+            const double *qi = coords + i * dim;
             for (int64_t j = 0; j < i; ++j) {
-                double t0 = qx - coords[2 * j];
-                double t1 = qy - coords[2 * j + 1];
-                double d = 0.0;
-                d += t0 * t0;
-                d += t1 * t1;
+                const double d = rdist(qi, coords + j * dim, dim);
                 if (cnt == k && !key_less(d, j, bd[k - 1], bi[k - 1])) continue;
                 int64_t s = cnt < k ? cnt++ : k - 1;
                 while (s > 0 && key_less(d, j, bd[s - 1], bi[s - 1])) {
@@ -78,27 +84,32 @@ int oracle_knn_prior(const double *coords, int64_t n, int32_t m, int64_t q0, int
 /* Same sets for an explicit list of query rows (parallel over the list): row t of nbr is
  * the set of location rows[t].  Used for sampled-row checks at N = 1e7, where one call
  * per row would scan s[0:i] on a single thread. */
-int oracle_knn_prior_rows(const double *coords, int64_t n, int32_t m, const int64_t *rows, int64_t n_rows,
-                          int32_t *nbr) {
-    if (m < 0 || n_rows < 0) return -1;
+int oracle_knn_prior_rows(const double *coords, int64_t n, int32_t dim, int32_t m, const int64_t *rows,
+                          int64_t n_rows, int32_t *nbr) {
+    if (m < 0 || dim < 1 || n_rows < 0) return -1;
     for (int64_t t = 0; t < n_rows; ++t)
         if (rows[t] < 0 || rows[t] >= n) return -1;
     int rc = 0;
 #pragma omp parallel for schedule(dynamic, 1) reduction(| : rc)
-    for (int64_t t = 0; t < n_rows; ++t) rc |= oracle_knn_prior(coords, n, m, rows[t], rows[t] + 1, nbr + t * m);
+    for (int64_t t = 0; t < n_rows; ++t) rc |= oracle_knn_prior(coords, n, dim, m, rows[t], rows[t] + 1, nbr + t * m);
     return rc;
 }
 
+/* Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12), u = phi d:
+ *   0 exponential sigma2 e^-u   1 matern32 sigma2 (1 + u) e^-u   2 matern52 sigma2 (1 + u + u^2/3) e^-u
+ *   3 gaussian    sigma2 e^-u^2 4 spherical sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 */
 static inline double cov_eval(int kind, double d, double sigma2, double phi) {
-    double e = exp(-phi * d);
-    if (kind == 1) return sigma2 * (1.0 + phi * d) * e;
-    return sigma2 * e;
+    const double u = phi * d;
+    switch (kind) {
+        case 1: return sigma2 * (1.0 + u) * exp(-u);
+        case 2: return sigma2 * (1.0 + u + u * u / 3.0) * exp(-u);
+        case 3: return sigma2 * exp(-u * u);
+        case 4: return u < 1.0 ? sigma2 * (1.0 - 1.5 * u + 0.5 * u * u * u) : 0.0;
+        default: return sigma2 * exp(-u);
+    }
 }
 
-static inline double pdist(const double *a, const double *b) {
-    double dx = a[0] - b[0], dy = a[1] - b[1];
-    return sqrt(dx * dx + dy * dy);
-}
+static inline double pdist(const double *a, const double *b, int dim) { return sqrt(rdist(a, b, dim)); }
 
 /*
  * Per location: C_N (+tau2 I), c, C_ii -> Cholesky C_N = L L^T (row-oriented),
@@ -107,10 +118,10 @@ static inline double pdist(const double *a, const double *b) {
  * partials[2] = first row index whose pivot or F is not > 0 (or -1).
  * A slot is valid iff its index is >= 0; invalid slots give B = 0.
  */
-int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t m, int32_t kind,
+int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t dim, int32_t m, int32_t kind,
                     const double *theta, const double *values, double *Bout, double *Fout, double *partials,
                     int64_t i0, int64_t i1) {
-    if (m < 0 || i0 < 0 || i1 > n || i0 > i1 || (kind != 0 && kind != 1)) return -1;
+    if (m < 0 || dim < 1 || i0 < 0 || i1 > n || i0 > i1 || kind < 0 || kind > 4) return -1;
     const double sigma2 = theta[0], phi = theta[1], tau2 = theta[2];
     const int64_t rows = i1 - i0;
     double *logF = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1));
@@ -136,18 +147,18 @@ int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t
                     if (row[s] >= n) bad = 1;
                     slot[k++] = s;
                 }
-            const double *xi = coords + 2 * i;
+            const double *xi = coords + dim * i;
             double F = sigma2 + tau2;
             double rr = bad ? NAN : (values ? values[i] : 0.0);
             if (!bad) {
                 for (int a = 0; a < k; ++a) {
-                    const double *xa = coords + 2 * (int64_t)row[slot[a]];
+                    const double *xa = coords + dim * (int64_t)row[slot[a]];
                     for (int bb = 0; bb < a; ++bb) {
-                        const double *xb = coords + 2 * (int64_t)row[slot[bb]];
-                        L[a * k + bb] = cov_eval(kind, pdist(xa, xb), sigma2, phi);
+                        const double *xb = coords + dim * (int64_t)row[slot[bb]];
+                        L[a * k + bb] = cov_eval(kind, pdist(xa, xb, dim), sigma2, phi);
                     }
                     L[a * k + a] = sigma2 + tau2;
-                    c[a] = cov_eval(kind, pdist(xi, xa), sigma2, phi);
+                    c[a] = cov_eval(kind, pdist(xi, xa, dim), sigma2, phi);
                 }
                 /* Cholesky (Cholesky-Banachiewicz, row by row) */
                 for (int a = 0; a < k && !bad; ++a) {

@@ -38,9 +38,12 @@ What it restates (reference = ``bwpriest/pyNNGP`` at ``/root/reference``):
   the same algebra with the location row taken from t; parity unpinned by the
   reference, anchored by the dense GP conditional (``dense_kriging``) at m = |S|.
 
-Covariance kinds (the reference's ``cov`` plug-in, ``nngp.py:6,12``):
-``exponential`` C(d) = sigma2 exp(-phi d); ``matern32``
-C(d) = sigma2 (1 + phi d) exp(-phi d); d is Euclidean distance in fp64.
+Covariance kinds (the reference's ``cov`` plug-in, ``nngp.py:6,12``; u = phi d, d the
+Euclidean distance in fp64 over any number of coordinate columns -- the reference's
+KDTree takes ordinates of any dimension, ``nngp.py:55-61``):
+``exponential`` sigma2 e^-u; ``matern32`` sigma2 (1 + u) e^-u; ``matern52``
+sigma2 (1 + u + u^2/3) e^-u; ``gaussian`` sigma2 e^-u^2; ``spherical``
+sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family).
 """
 from __future__ import annotations
 
@@ -50,7 +53,7 @@ import subprocess
 
 import numpy as np
 
-KINDS = {"exponential": 0, "matern32": 1}
+KINDS = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4}
 LOG_2PI = float(np.log(2.0 * np.pi))
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -58,12 +61,18 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # ----------------------------------------------------------------------------
 # neighbour sets (nngp.py:49-62)
 # ----------------------------------------------------------------------------
+def rdist(t: np.ndarray) -> np.ndarray:
+    """sklearn euclidean_rdist64 of difference rows t (..., dim): d = 0; d += t_k * t_k in
+    axis order (``_dist_metrics.pxd:26-40``); separate ufuncs, so no FMA contraction."""
+    d = np.zeros(t.shape[:-1])
+    for k in range(t.shape[-1]):
+        d = d + t[..., k] * t[..., k]
+    return d
+
+
 def rdist_to_prior(coords: np.ndarray, i: int) -> np.ndarray:
-    """sklearn euclidean_rdist64 of s_i against s[0:i] (``_dist_metrics.pxd:26-40``)."""
-    t = coords[i][None, :] - coords[:i]
-    t0 = t[:, 0]
-    t1 = t[:, 1]
-    return (0.0 + t0 * t0) + t1 * t1  # separate ufuncs: no FMA contraction
+    """rdist of s_i against s[0:i]."""
+    return rdist(coords[i][None, :] - coords[:i])
 
 
 def knn_prior(coords: np.ndarray, m: int, q0: int = 0, q1: int | None = None) -> np.ndarray:
@@ -93,8 +102,7 @@ def knn_all(query: np.ndarray, ref: np.ndarray, k: int) -> np.ndarray:
     """k nearest of every query among all ref points (self included), (rdist, idx) order."""
     out = np.empty((query.shape[0], k), dtype=np.int64)
     for q in range(query.shape[0]):
-        t = query[q][None, :] - ref
-        d = (0.0 + t[:, 0] * t[:, 0]) + t[:, 1] * t[:, 1]
+        d = rdist(query[q][None, :] - ref)
         out[q] = np.lexsort((np.arange(ref.shape[0]), d))[:k]
     return out
 
@@ -109,18 +117,23 @@ def ws_init(t: np.ndarray, y: np.ndarray, s: np.ndarray, k: int = 5) -> np.ndarr
 # covariance plug-in and per-location algebra (nngp.py:73-96)
 # ----------------------------------------------------------------------------
 def cov_fn(kind: str, d: np.ndarray, sigma2: float, phi: float) -> np.ndarray:
+    """The covariance kinds, u = phi d (module docstring)."""
+    u = phi * np.asarray(d, dtype=np.float64)
     if kind == "exponential":
-        return sigma2 * np.exp(-phi * d)
+        return sigma2 * np.exp(-u)
     if kind == "matern32":
-        pd = phi * d
-        return sigma2 * (1.0 + pd) * np.exp(-pd)
+        return sigma2 * (1.0 + u) * np.exp(-u)
+    if kind == "matern52":
+        return sigma2 * (1.0 + u + u * u / 3.0) * np.exp(-u)
+    if kind == "gaussian":
+        return sigma2 * np.exp(-u * u)
+    if kind == "spherical":
+        return np.where(u < 1.0, sigma2 * (1.0 - 1.5 * u + 0.5 * u * u * u), 0.0)
     raise ValueError(f"unknown covariance kind {kind!r}")
 
 
 def _pair_dist(a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    dx = a[..., 0] - b[..., 0]
-    dy = a[..., 1] - b[..., 1]
-    return np.sqrt(dx * dx + dy * dy)
+    return np.sqrt(rdist(a - b))
 
 
 def location_blocks(coords, nbr_row, i, kind, theta):
@@ -239,18 +252,24 @@ def load_c_oracle():
         build_c_oracle()
     lib = ctypes.CDLL(path)
     P = ctypes.c_void_p
-    lib.oracle_knn_prior.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, P]
+    I32, I64 = ctypes.c_int32, ctypes.c_int64
+    lib.oracle_knn_prior.argtypes = [P, I64, I32, I32, I64, I64, P]
     lib.oracle_knn_prior.restype = ctypes.c_int
-    lib.oracle_knn_prior_rows.argtypes = [P, ctypes.c_int64, ctypes.c_int32, P, ctypes.c_int64, P]
+    lib.oracle_knn_prior_rows.argtypes = [P, I64, I32, I32, P, I64, P]
     lib.oracle_knn_prior_rows.restype = ctypes.c_int
-    lib.oracle_bf_sweep.argtypes = [P, P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, P, P, P, P, P,
-                                    ctypes.c_int64, ctypes.c_int64]
+    lib.oracle_bf_sweep.argtypes = [P, P, I64, I32, I32, I32, P, P, P, P, P, I64, I64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
     lib.oracle_num_threads.restype = ctypes.c_int
     lib.oracle_nngp_simulate.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int32, P, P]
     lib.oracle_nngp_simulate.restype = ctypes.c_int
     _C = lib
     return lib
+
+
+def _dim(coords):
+    if coords.ndim != 2 or coords.shape[1] < 1:
+        raise ValueError(f"coordinates must be (n, dim), got {coords.shape}")
+    return coords.shape[1]
 
 
 def _ptr(a):
@@ -263,7 +282,7 @@ def c_knn_prior(coords, m, q0=0, q1=None):
     n = coords.shape[0]
     q1 = n if q1 is None else q1
     out = np.full((q1 - q0, m), -1, dtype=np.int32)
-    rc = lib.oracle_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out))
+    rc = lib.oracle_knn_prior(_ptr(coords), n, _dim(coords), m, q0, q1, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle_knn_prior failed: {rc}")
     return out
@@ -275,7 +294,7 @@ def c_knn_prior_rows(coords, m, rows):
     coords = np.ascontiguousarray(coords, dtype=np.float64)
     rows = np.ascontiguousarray(rows, dtype=np.int64)
     out = np.full((rows.size, m), -1, dtype=np.int32)
-    rc = lib.oracle_knn_prior_rows(_ptr(coords), coords.shape[0], m, _ptr(rows), rows.size, _ptr(out))
+    rc = lib.oracle_knn_prior_rows(_ptr(coords), coords.shape[0], _dim(coords), m, _ptr(rows), rows.size, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle_knn_prior_rows failed: {rc}")
     return out
@@ -292,7 +311,7 @@ def c_bf_sweep(coords, nbr, kind, theta, values=None, i0=0, want_bf=True):
     B = np.zeros((n, m)) if want_bf else None
     F = np.zeros(n) if want_bf else None
     partials = np.zeros(3)
-    rc = lib.oracle_bf_sweep(_ptr(coords), _ptr(nbr), coords.shape[0], m, KINDS[kind], _ptr(th), _ptr(vals),
+    rc = lib.oracle_bf_sweep(_ptr(coords), _ptr(nbr), coords.shape[0], _dim(coords), m, KINDS[kind], _ptr(th), _ptr(vals),
                              _ptr(B), _ptr(F), _ptr(partials), i0, i0 + n)
     if rc != 0:
         raise RuntimeError(f"oracle_bf_sweep failed: {rc}")

@@ -19,7 +19,8 @@ nothing is written under the read-only reference tree.
 
 Usage::
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py        # the 2-D fixtures
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py dims   # 1-D and 3-D ordinates
 """
 import os
 import sys
@@ -65,7 +66,9 @@ def _tie_rows(coords, m):
     ties = np.zeros(n, dtype=bool)
     for i in range(1, n):
         t = coords[i][None, :] - coords[:i]
-        d = t[:, 0] * t[:, 0] + t[:, 1] * t[:, 1]
+        d = np.zeros(i)
+        for k in range(coords.shape[1]):  # sklearn's rdist order, any dimension
+            d = d + t[:, k] * t[:, k]
         k = min(m, i)
         srt = np.sort(d)
         # any tie among the first k, or between the k-th and the (k+1)-th
@@ -94,8 +97,17 @@ def make_case(pyNNGP, name, coords, y, m):
     print(f"wrote {path}: N={coords.shape[0]} m={m} tie_rows={int(out['tie_rows'].sum())}")
 
 
-def main():
+def main(only=None):
     pyNNGP = _import_reference()
+    if only == "dims":
+        # ordinates of dimension 1 and 3 (the reference's KDTree takes any d, nngp.py:55-61)
+        rng = np.random.default_rng(43)
+        c = rng.uniform(0.0, 1.0, (1000, 3))
+        make_case(pyNNGP, "knn_ref_n1000_m10_d3", c, rng.standard_normal(1000), 10)
+        rng = np.random.default_rng(44)
+        c = rng.uniform(0.0, 1.0, (1000, 1))
+        make_case(pyNNGP, "knn_ref_n1000_m8_d1", c, rng.standard_normal(1000), 8)
+        return
     # reference test shape (tests/test_init.py:7-17), seeded, scalar y
     rng = np.random.default_rng(7)
     c = rng.uniform(size=(200, 2))
@@ -114,4 +126,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

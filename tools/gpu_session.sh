@@ -5,7 +5,7 @@
 #   tests:<expr>     the same restricted with -k <expr>
 #   smoke            __graft_entry__.smoke()
 #   bench[:args]     python bench.py <args>  (one JSON line -> bench_<n>.json)
-#   ubench           tools/ubench/f64_latency and f64_rates (prebuilt in-tree)
+#   ubench           tools/ubench/f64_latency (prebuilt in-tree)
 #   sq[:args]        SQ counter pass over bench.py <args> (per-kernel CSV)
 #   sqmem[:args]     memory-pipeline counter pass over bench.py <args>
 #   trace[:args]     rocprofv3 --kernel-trace --stats over bench.py <args>
@@ -40,8 +40,7 @@ for step in "$@"; do
       python -c "import json,sys; d=json.load(open('$out/bench_$n.json')); print('value %.4g' % d['value'], 'ms/step %.4f' % d['ms_per_step'], 'kernel_ms %.4f' % d['roofline']['kernel_ms'], 'frac %.3f' % d['roofline']['frac'])" ;;
     ubench)
       timeout -k 10 120 tools/ubench/f64_latency > $out/f64_latency.txt 2>&1 || exit 1
-      timeout -k 10 120 tools/ubench/f64_rates > $out/f64_rates.txt 2>&1 || exit 1
-      cat $out/f64_latency.txt $out/f64_rates.txt ;;
+      cat $out/f64_latency.txt ;;
     sq)
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES \
         --output-format csv -d $out/sq_$n -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 $arg > $out/sq_$n.json 2> $out/sq_$n.err || { tail -5 $out/sq_$n.err; exit 1; }
