@@ -54,19 +54,22 @@ def synth(n_total, seed=0):
     return coords, values
 
 
-def knn_cpu_baseline(coords, m, n_full):
-    """Neighbour-set build on the host: the C oracle (exact brute force over s[0:i],
-    OpenMP) on the first 20,000 locations, extrapolated quadratically to n_full (the
-    reference rebuilds a KDTree per i, SURVEY.md 6: 12.7 s at N=1e4, single thread)."""
+def knn_cpu_baseline(coords, m, n_full, n_sample=10_000):
+    """Neighbour-set build on the host, the reference's own algorithm: a KD-tree over
+    s[0:i] rebuilt for every i, queried for min(i, m) neighbours (pyNNGP/nngp.py:49-62;
+    restated single-threaded in C, oracle_knn_prior_kdtree_rebuild, leaf size 40 as
+    sklearn's default).  Timed on the first ``n_sample`` locations and extrapolated to
+    ``n_full`` as N^2 log N (the rebuild of an i-point tree costs i log i; summed over i)."""
     from oracle import nngp_oracle as O
 
-    n = min(20_000, coords.shape[0])
+    n = min(n_sample, coords.shape[0])
     t = time.perf_counter()
-    O.c_knn_prior(coords[:n], m)
+    O.c_knn_prior_kdtree_rebuild(coords[:n], m)
     el = time.perf_counter() - t
-    return {"seconds_measured": el, "n_measured": n, "seconds_extrapolated": el * (n_full / n) ** 2,
-            "n_extrapolated": n_full, "cores": int(O.load_c_oracle().oracle_num_threads()),
-            "kind": "port (exact brute force, C oracle; extrapolated as N^2)"}
+    scale = (n_full / n) ** 2 * np.log(n_full) / np.log(n)
+    return {"seconds_measured": el, "n_measured": n, "seconds_extrapolated": el * scale,
+            "n_extrapolated": n_full, "cores": 1,
+            "kind": "port (per-i KD-tree rebuild as pyNNGP/nngp.py:55-61, C restatement; extrapolated as N^2 log N)"}
 
 
 def committed_profile(args, want_bf):
@@ -168,9 +171,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--n", "--n-per-gpu", dest="n", type=int, default=1_000_000, help="locations per GPU")
     ap.add_argument("--m", type=int, default=15)
-    ap.add_argument("--kind", default="exponential", choices=["exponential", "matern32"])
+    ap.add_argument("--kind", default="exponential", choices=list(_lib.KIND_CODES))
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
-    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad", "pairb"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad", "pairb", "pairb_r1"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
     ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order; natural layout)")
     ap.add_argument("--layout", default="storage", choices=["storage", "natural"],

@@ -54,8 +54,8 @@ int main(int argc, char** argv) {
     double *d_xy, *d_v, *d_B, *d_F, *d_p;
     int32_t* d_nbr;
     void *ws_knn, *ws_bf;
-    const size_t knn_bytes = nngp_knn_workspace_bytes(n, m);
-    const size_t bf_bytes = nngp_bf_sweep_workspace_bytes(n, m, NNGP_ALGO_AUTO);
+    const size_t knn_bytes = nngp_knn_workspace_bytes(n, 2, m);
+    const size_t bf_bytes = nngp_bf_sweep_workspace_bytes(n, m, NNGP_COV_EXPONENTIAL, 2, NNGP_ALGO_AUTO);
     CHECK_HIP(hipMalloc((void**)&d_xy, sizeof(double) * 2 * n));
     CHECK_HIP(hipMalloc((void**)&d_v, sizeof(double) * n));
     CHECK_HIP(hipMalloc((void**)&d_nbr, sizeof(int32_t) * n * (m > 0 ? m : 1)));
@@ -68,9 +68,9 @@ int main(int argc, char** argv) {
     CHECK_HIP(hipMemcpy(d_v, v, sizeof(double) * n, hipMemcpyHostToDevice));
 
     /* NNGP._make_s_neighbor_sets (nngp.py:49-62) */
-    CHECK_NNGP(nngp_knn_prior(d_xy, n, m, 0, n, d_nbr, ws_knn, knn_bytes, NULL));
+    CHECK_NNGP(nngp_knn_prior(d_xy, n, 2, m, 0, n, d_nbr, ws_knn, knn_bytes, NULL));
     /* _CNs / _Ccross / _Cs / _Bsi / _Fsi (nngp.py:73-96) + the log-likelihood for every location */
-    CHECK_NNGP(nngp_bf_sweep(d_xy, n, d_nbr, NULL, n, m, 0, NNGP_COV_EXPONENTIAL, 1.0, 30.0, 0.1, d_v, d_B, d_F, NULL,
+    CHECK_NNGP(nngp_bf_sweep(d_xy, n, 2, d_nbr, NULL, n, m, 0, NNGP_COV_EXPONENTIAL, 1.0, 30.0, 0.1, d_v, d_B, d_F, NULL,
                              d_p, ws_bf, bf_bytes, NNGP_ALGO_AUTO, NULL));
     double p[4], Flast;
     CHECK_HIP(hipMemcpy(p, d_p, sizeof p, hipMemcpyDeviceToHost));

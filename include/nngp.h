@@ -14,8 +14,10 @@
  *     tensor memory); the caller owns every buffer.
  *   - `stream` is a hipStream_t (NULL = default stream).  All work is
  *     stream-ordered; no call synchronises the host, allocates, or frees.
- *   - Coordinates are fp64 (n_points, 2) row-major; neighbour sets are int32
- *     (rows, m) row-major, padded with -1 (row i holds min(i, m) indices).
+ *   - Coordinates are fp64 (n_points, dim) row-major, dim = 1, 2 or 3 (the
+ *     reference's KDTree takes ordinates of any dimension, nngp.py:55-61); they
+ *     must be finite.  Neighbour sets are int32 (rows, m) row-major, padded with -1
+ *     (row i holds min(i, m) indices).
  *   - Return 0 on success or a negative NNGP_E* code (nngp_last_error() gives
  *     the message).  Numerical failures are data, not return codes, because the
  *     work is asynchronous: see `partials` of nngp_bf_sweep.
@@ -36,17 +38,25 @@ extern "C" {
 #define NNGP_EHIP (-3)      /* a HIP runtime call or kernel launch failed */
 #define NNGP_EUNSUP (-4)    /* unsupported configuration (e.g. m > 63) */
 
-#define NNGP_COV_EXPONENTIAL 0 /* sigma2 * exp(-phi d)                  */
-#define NNGP_COV_MATERN32 1    /* sigma2 * (1 + phi d) * exp(-phi d)      */
+/* covariance kinds (the reference's `cov` plug-in, nngp.py:6,12), u = phi d: */
+#define NNGP_COV_EXPONENTIAL 0 /* sigma2 exp(-u)                                    */
+#define NNGP_COV_MATERN32 1    /* sigma2 (1 + u) exp(-u)                            */
+#define NNGP_COV_MATERN52 2    /* sigma2 (1 + u + u^2/3) exp(-u)                    */
+#define NNGP_COV_GAUSSIAN 3    /* sigma2 exp(-u^2)                                  */
+#define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
 
-#define NNGP_ALGO_AUTO 0 /* fastest measured kernel for m (lane m <= 10, pairb 11..24, quad 25..32, wave) */
-#define NNGP_ALGO_LANE 1 /* one lane per location (m <= 16)           */
-#define NNGP_ALGO_WAVE 2 /* one wavefront per location (m <= 63)      */
-#define NNGP_ALGO_PAIR 3 /* two lanes per location (10 <= m <= 20)     */
-#define NNGP_ALGO_QUAD 4 /* four lanes per location (m in 15, 16, 20, 25..32) */
-#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked elimination (1 <= m <= 24) */
+/* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE, PAIR and
+ * QUAD serve 2-D exponential / Matern-3/2 only, PAIRB and WAVE every kind and dimension */
+#define NNGP_ALGO_AUTO 0  /* 2-D exp / Matern-3/2: lane m <= 10, pairb 11..24, quad 25..32, wave; else pairb / wave */
+#define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
+#define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
+#define NNGP_ALGO_PAIR 3  /* two lanes per location (10 <= m <= 20)                          */
+#define NNGP_ALGO_QUAD 4  /* four lanes per location (m in 15, 16, 20, 25..32)               */
+#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked, persistent (1 <= m <= 24) */
+#define NNGP_ALGO_PAIRB_R1 7 /* the round-1 pair kernel (m = 15, exponential, 2-D): same-box A/B only */
 
 #define NNGP_MAX_M 63
+#define NNGP_MAX_DIM 3
 
 /* Library version string, e.g. "pynngp_amd 0.1.0 gfx950". */
 const char *nngp_version(void);
@@ -61,20 +71,22 @@ const char *nngp_last_error(void);
  * sklearn/metrics/_dist_metrics.pxd:26-40).
  * For every query row i in [q0, q1): the k = min(m, i) nearest points among
  * coords[0:i], ascending fp64 rdist = (0 + t0*t0) + t1*t1 (no FMA), exact
- * ties by lower index, written to nbr[(i - q0) * m + s], s < k; -1 beyond.
- * Requires n_points <= INT32_MAX, 0 <= m <= 64, 0 <= q0 <= q1 <= n_points, and
- * finite coordinates (NaN / inf give unspecified sets; the Python layer rejects them).
+ * ties by lower index, written to nbr[(i - q0) * m + s], s < k; -1 beyond.  rdist
+ * sums t_k^2 over the dim coordinates in axis order, unfused, as sklearn does.
+ * Requires n_points <= INT32_MAX, 1 <= dim <= 3, 0 <= m <= 64,
+ * 0 <= q0 <= q1 <= n_points, and finite coordinates (NaN / inf give unspecified
+ * sets; the Python layer rejects them).
  * ------------------------------------------------------------------------- */
-size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m);
-int nngp_knn_prior(const double *coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t *nbr,
-                   void *workspace, size_t workspace_bytes, void *stream);
+size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t dim, int32_t m);
+int nngp_knn_prior(const double *coords, int64_t n_points, int32_t dim, int32_t m, int64_t q0, int64_t q1,
+                   int32_t *nbr, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Same neighbour sets for an arbitrary list of locations: query row t is point rows[t]
  * (its min(m, rows[t]) nearest among coords[0:rows[t]]), written to nbr[t * m + s].
  * Used to build a shard's sets when the shard is a range of a spatial storage order
  * (pynngp_amd.sweep.ShardedLogLik, layout "storage").  Workspace as nngp_knn_prior. */
-int nngp_knn_prior_rows(const double *coords, int64_t n_points, int32_t m, const int32_t *rows, int64_t n_rows,
-                        int32_t *nbr, void *workspace, size_t workspace_bytes, void *stream);
+int nngp_knn_prior_rows(const double *coords, int64_t n_points, int32_t dim, int32_t m, const int32_t *rows,
+                        int64_t n_rows, int32_t *nbr, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Unrestricted k-nearest neighbours of query points among a reference set.
@@ -83,10 +95,10 @@ int nngp_knn_prior_rows(const double *coords, int64_t n_points, int32_t m, const
  * NNGP._make_t_neighbor_sets (nngp.py:64-71, KDTree(s).query(t, m)).
  * nbr[q * k + s] = index into ref of the s-th nearest point to query[q]
  * ((rdist, index) order, self included when a query point is in ref), -1 for
- * s >= n_ref.  Workspace: nngp_knn_workspace_bytes(n_ref, k).
+ * s >= n_ref.  ref and query are (n, dim).  Workspace: nngp_knn_workspace_bytes(n_ref, dim, k).
  * ------------------------------------------------------------------------- */
-int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_t n_query, int32_t k, int32_t *nbr,
-                   void *workspace, size_t workspace_bytes, void *stream);
+int nngp_knn_query(const double *ref, int64_t n_ref, int32_t dim, const double *query, int64_t n_query, int32_t k,
+                   int32_t *nbr, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Fused B/F + log-likelihood sweep over locations i0 .. i0 + n_rows - 1.
@@ -104,24 +116,25 @@ int nngp_knn_query(const double *ref, int64_t n_ref, const double *query, int64_
  *   log-lik = -1/2 (n_rows log 2 pi + partials[0] + partials[1]).
  * Rows flagged in partials[2] get B = F = NaN.  The sum order is fixed, so the
  * partials are bit-reproducible run to run.
- * coords: (n_points, 2); nbr: (n_rows, m); order: NULL (row t of nbr is location
+ * coords: (n_points, dim); nbr: (n_rows, m); order: NULL (row t of nbr is location
  * i0 + t) or the nngp_row_order layout (row t of nbr is location i0 + order[t],
  * i.e. pass nbr_sorted); values: (n_points,) or NULL;
  * B, F: may be NULL (log-lik only); R: NULL or (n_rows,) residuals
  * r_i = v_i - B_i v_N(i) (needs values; the Gibbs w-update keeps them current);
  * partials: 4 doubles, or NULL to defer the final fold: the per-block records stay in
- * the workspace and nngp_bf_finalize (same n_rows, m, algo) folds them later, e.g. on
- * another stream while the next sweep (with another workspace) runs.
- * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, algo) bytes, 256-B aligned.
+ * the workspace and nngp_bf_finalize (same n_rows, m, kind, dim, algo) folds them later,
+ * e.g. on another stream while the next sweep (with another workspace) runs.
+ * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo) bytes, 256-B aligned.
  * ------------------------------------------------------------------------- */
-size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo);
-int nngp_bf_sweep(const double *coords, int64_t n_points, const int32_t *nbr, const int32_t *order, int64_t n_rows,
-                  int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2, const double *values,
-                  double *B, double *F, double *R, double *partials, void *workspace, size_t workspace_bytes,
-                  int32_t algo, void *stream);
+size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo);
+int nngp_bf_sweep(const double *coords, int64_t n_points, int32_t dim, const int32_t *nbr, const int32_t *order,
+                  int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
+                  const double *values, double *B, double *F, double *R, double *partials, void *workspace,
+                  size_t workspace_bytes, int32_t algo, void *stream);
 /* The deferred fold of a sweep run with partials == NULL (fixed order: the same
  * bits as the in-line fold). */
-int nngp_bf_finalize(const void *workspace, int64_t n_rows, int32_t m, int32_t algo, double *partials, void *stream);
+int nngp_bf_finalize(const void *workspace, int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo,
+                     double *partials, void *stream);
 
 /* ---------------------------------------------------------------------------
  * B/F of query locations t against a reference set S (prediction / kriging at
@@ -137,12 +150,13 @@ int nngp_bf_finalize(const void *workspace, int64_t n_rows, int32_t m, int32_t a
  * the kriging mean).  partials as nngp_bf_sweep (with query_values: the
  * conditional log density of v_t given v_S).  Rows q in [q0, q0 + n_rows) of
  * n_query; order / workspace as nngp_bf_sweep (nngp_row_order on the query
- * coordinates; nngp_bf_sweep_workspace_bytes).
+ * coordinates; nngp_bf_sweep_workspace_bytes).  ref and query are (n, dim).
  * ------------------------------------------------------------------------- */
-int nngp_bf_cross(const double *ref, int64_t n_ref, const double *query, int64_t n_query, const int32_t *nbr,
-                  const int32_t *order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind, double sigma2,
-                  double phi, double tau2, const double *ref_values, const double *query_values, double *B, double *F,
-                  double *R, double *partials, void *workspace, size_t workspace_bytes, int32_t algo, void *stream);
+int nngp_bf_cross(const double *ref, int64_t n_ref, int32_t dim, const double *query, int64_t n_query,
+                  const int32_t *nbr, const int32_t *order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind,
+                  double sigma2, double phi, double tau2, const double *ref_values, const double *query_values,
+                  double *B, double *F, double *R, double *partials, void *workspace, size_t workspace_bytes,
+                  int32_t algo, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Visiting order for nngp_bf_sweep (a speed option; no reference counterpart:
@@ -157,8 +171,9 @@ int nngp_bf_cross(const double *ref, int64_t n_ref, const double *query, int64_t
  * Workspace: nngp_row_order_workspace_bytes(n_rows).
  * ------------------------------------------------------------------------- */
 size_t nngp_row_order_workspace_bytes(int64_t n_rows);
-int nngp_row_order(const double *coords, int64_t n_points, const int32_t *nbr, int32_t m, int64_t i0, int64_t n_rows,
-                   int32_t *order, int32_t *nbr_sorted, void *workspace, size_t workspace_bytes, void *stream);
+int nngp_row_order(const double *coords, int64_t n_points, int32_t dim, const int32_t *nbr, int32_t m, int64_t i0,
+                   int64_t n_rows, int32_t *order, int32_t *nbr_sorted, void *workspace, size_t workspace_bytes,
+                   void *stream);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU: fold the all-gathered partials of `world` ranks (device array

@@ -98,6 +98,157 @@ int oracle_knn_prior_rows(const double *coords, int64_t n, int32_t dim, int32_t 
 /* Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12), u = phi d:
  *   0 exponential sigma2 e^-u   1 matern32 sigma2 (1 + u) e^-u   2 matern52 sigma2 (1 + u + u^2/3) e^-u
  *   3 gaussian    sigma2 e^-u^2 4 spherical sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 */
+/* ---------------------------------------------------------------------------
+ * The reference's own neighbour-set ALGORITHM, restated for the CPU baseline:
+ * NNGP._make_s_neighbor_sets (nngp.py:49-62) builds a fresh sklearn KDTree over
+ * s[0:i] for every i (nngp.py:55) and queries the k = min(m, i) nearest
+ * (nngp.py:56-61), O(N^2 log N) in all.  Same construction here, single thread (the
+ * reference's loop is a single Python thread): per i, a kd-tree over s[0:i] with
+ * sklearn's defaults (leaf_size 40, split on the dimension of largest spread at the
+ * median, sklearn/neighbors/_kd_tree.pyx + _binary_tree.pxi.tp:1086-1195), then a
+ * depth-first query with a bounded max-heap and node-box pruning
+ * (_binary_tree.pxi.tp:1604-1658).  Keys are (rdist, index), so the result equals
+ * oracle_knn_prior bit for bit (the box bound is a true lower bound of the fp rdist:
+ * correctly rounded sub / mul / add are monotone).
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    int64_t start, end;  /* idx[start:end] */
+    int64_t left, right; /* children, -1 for a leaf */
+} KdNode;
+
+typedef struct {
+    const double *pts;
+    int dim;
+    int64_t *idx;
+    KdNode *nodes;
+    double *lo, *hi; /* node boxes, dim each */
+    int64_t n_nodes;
+} KdTree;
+
+static void kd_swap(int64_t *a, int64_t *b) { int64_t t = *a; *a = *b; *b = t; }
+
+/* place the median (by coordinate k) at idx[mid], smaller before, larger after (quickselect) */
+static void kd_select(const double *pts, int dim, int k, int64_t *idx, int64_t lo, int64_t hi, int64_t mid) {
+    while (hi - lo > 1) {
+        const double pv = pts[idx[(lo + hi) / 2] * dim + k];
+        int64_t a = lo, b = hi - 1;
+        while (a <= b) {
+            while (pts[idx[a] * dim + k] < pv) ++a;
+            while (pts[idx[b] * dim + k] > pv) --b;
+            if (a <= b) kd_swap(&idx[a++], &idx[b--]);
+        }
+        if (mid <= b) hi = b + 1;
+        else if (mid >= a) lo = a;
+        else return;
+    }
+}
+
+static int64_t kd_build(KdTree *t, int64_t start, int64_t end) {
+    const int64_t id = t->n_nodes++;
+    KdNode *nd = &t->nodes[id];
+    nd->start = start;
+    nd->end = end;
+    nd->left = nd->right = -1;
+    double *lo = t->lo + id * t->dim, *hi = t->hi + id * t->dim;
+    for (int k = 0; k < t->dim; ++k) {
+        lo[k] = INFINITY;
+        hi[k] = -INFINITY;
+    }
+    for (int64_t a = start; a < end; ++a)
+        for (int k = 0; k < t->dim; ++k) {
+            const double v = t->pts[t->idx[a] * t->dim + k];
+            if (v < lo[k]) lo[k] = v;
+            if (v > hi[k]) hi[k] = v;
+        }
+    if (end - start <= 40) return id; /* sklearn's default leaf_size */
+    int ks = 0;
+    for (int k = 1; k < t->dim; ++k)
+        if (hi[k] - lo[k] > hi[ks] - lo[ks]) ks = k;
+    const int64_t mid = start + (end - start) / 2;
+    kd_select(t->pts, t->dim, ks, t->idx, start, end, mid);
+    const int64_t l = kd_build(t, start, mid);
+    const int64_t r = kd_build(t, mid, end);
+    t->nodes[id].left = l;
+    t->nodes[id].right = r;
+    return id;
+}
+
+static double kd_min_rdist(const KdTree *t, int64_t id, const double *q) {
+    const double *lo = t->lo + id * t->dim, *hi = t->hi + id * t->dim;
+    double d = 0.0;
+    for (int k = 0; k < t->dim; ++k) {
+        double e = 0.0;
+        if (q[k] < lo[k]) e = lo[k] - q[k];
+        else if (q[k] > hi[k]) e = q[k] - hi[k];
+        d += e * e;
+    }
+    return d;
+}
+
+/* bounded sorted list of the k best (rdist, j) */
+static void kd_push(double *bd, int64_t *bi, int64_t *cnt, int64_t k, double d, int64_t j) {
+    if (*cnt == k && !key_less(d, j, bd[k - 1], bi[k - 1])) return;
+    int64_t s = *cnt < k ? (*cnt)++ : k - 1;
+    while (s > 0 && key_less(d, j, bd[s - 1], bi[s - 1])) {
+        bd[s] = bd[s - 1];
+        bi[s] = bi[s - 1];
+        --s;
+    }
+    bd[s] = d;
+    bi[s] = j;
+}
+
+static void kd_query(const KdTree *t, int64_t id, const double *q, int64_t k, double *bd, int64_t *bi, int64_t *cnt) {
+    const KdNode *nd = &t->nodes[id];
+    if (*cnt == k && kd_min_rdist(t, id, q) > bd[k - 1]) return;
+    if (nd->left < 0) {
+        for (int64_t a = nd->start; a < nd->end; ++a) {
+            const int64_t j = t->idx[a];
+            kd_push(bd, bi, cnt, k, rdist(q, t->pts + j * t->dim, t->dim), j);
+        }
+        return;
+    }
+    const double dl = kd_min_rdist(t, nd->left, q), dr = kd_min_rdist(t, nd->right, q);
+    const int64_t first = dl <= dr ? nd->left : nd->right, second = dl <= dr ? nd->right : nd->left;
+    kd_query(t, first, q, k, bd, bi, cnt);
+    kd_query(t, second, q, k, bd, bi, cnt);
+}
+
+int oracle_knn_prior_kdtree_rebuild(const double *coords, int64_t n, int32_t dim, int32_t m, int64_t q0, int64_t q1,
+                                    int32_t *nbr) {
+    if (m < 0 || dim < 1 || q0 < 0 || q1 > n || q0 > q1) return -1;
+    if (m == 0 || q1 == q0) return 0;
+    const int64_t cap = q1 > 1 ? q1 : 1;
+    KdTree t;
+    t.pts = coords;
+    t.dim = dim;
+    t.idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)cap);
+    t.nodes = (KdNode *)malloc(sizeof(KdNode) * (size_t)(2 * cap / 20 + 8));
+    t.lo = (double *)malloc(sizeof(double) * (size_t)dim * (size_t)(2 * cap / 20 + 8));
+    t.hi = (double *)malloc(sizeof(double) * (size_t)dim * (size_t)(2 * cap / 20 + 8));
+    double *bd = (double *)malloc(sizeof(double) * (size_t)m);
+    int64_t *bi = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+    for (int64_t i = q0; i < q1; ++i) {
+        int32_t *row = nbr + (i - q0) * m;
+        const int64_t k = i < m ? i : m;
+        int64_t cnt = 0;
+        if (i > 0) {
+            for (int64_t a = 0; a < i; ++a) t.idx[a] = a; /* KDTree(s[0:i]): a fresh tree per i */
+            t.n_nodes = 0;
+            kd_build(&t, 0, i);
+            kd_query(&t, 0, coords + i * dim, k, bd, bi, &cnt);
+        }
+        for (int64_t s = 0; s < m; ++s) row[s] = s < cnt ? (int32_t)bi[s] : -1;
+    }
+    free(t.idx);
+    free(t.nodes);
+    free(t.lo);
+    free(t.hi);
+    free(bd);
+    free(bi);
+    return 0;
+}
+
 static inline double cov_eval(int kind, double d, double sigma2, double phi) {
     const double u = phi * d;
     switch (kind) {

@@ -257,6 +257,8 @@ def load_c_oracle():
     lib.oracle_knn_prior.restype = ctypes.c_int
     lib.oracle_knn_prior_rows.argtypes = [P, I64, I32, I32, P, I64, P]
     lib.oracle_knn_prior_rows.restype = ctypes.c_int
+    lib.oracle_knn_prior_kdtree_rebuild.argtypes = [P, I64, I32, I32, I64, I64, P]
+    lib.oracle_knn_prior_kdtree_rebuild.restype = ctypes.c_int
     lib.oracle_bf_sweep.argtypes = [P, P, I64, I32, I32, I32, P, P, P, P, P, I64, I64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
     lib.oracle_num_threads.restype = ctypes.c_int
@@ -285,6 +287,20 @@ def c_knn_prior(coords, m, q0=0, q1=None):
     rc = lib.oracle_knn_prior(_ptr(coords), n, _dim(coords), m, q0, q1, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle_knn_prior failed: {rc}")
+    return out
+
+
+def c_knn_prior_kdtree_rebuild(coords, m, q0=0, q1=None):
+    """The reference's algorithm (a fresh kd-tree over s[0:i] per i, nngp.py:55-61),
+    single-threaded C: the CPU baseline of the neighbour build.  Same output as c_knn_prior."""
+    lib = load_c_oracle()
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    n = coords.shape[0]
+    q1 = n if q1 is None else q1
+    out = np.full((q1 - q0, m), -1, dtype=np.int32)
+    rc = lib.oracle_knn_prior_kdtree_rebuild(_ptr(coords), n, _dim(coords), m, q0, q1, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle_knn_prior_kdtree_rebuild failed: {rc}")
     return out
 
 

@@ -14,7 +14,8 @@ __version__ = "0.1.0"
 
 
 def load_ops():
-    """Register ``torch.ops.nngp.*`` (imports torch.library custom ops)."""
-    from . import ops  # noqa: F401
+    """Register ``torch.ops.nngp.*`` (loads the native operator library, libnngp_torch_ops.so)."""
+    from . import ops
 
+    ops.load()
     return ops

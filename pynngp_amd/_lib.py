@@ -43,9 +43,10 @@ SYMBOLS = (
     "nngp_gibbs_stats",
 )
 
-KIND_CODES = {"exponential": 0, "matern32": 1}
-ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4, "pairb": 5}
+KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4}
+ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4, "pairb": 5, "pairb_r1": 7}
 MAX_M = 63
+MAX_DIM = 3
 
 
 class NNGPExtensionError(RuntimeError):
@@ -69,25 +70,26 @@ def load() -> ctypes.CDLL:
     P, I32, I64, D, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
     lib.nngp_version.restype = ctypes.c_char_p
     lib.nngp_last_error.restype = ctypes.c_char_p
-    lib.nngp_knn_workspace_bytes.argtypes = [I64, I32]
+    lib.nngp_knn_workspace_bytes.argtypes = [I64, I32, I32]
     lib.nngp_knn_workspace_bytes.restype = SZ
-    lib.nngp_knn_prior.argtypes = [P, I64, I32, I64, I64, P, P, SZ, P]
+    lib.nngp_knn_prior.argtypes = [P, I64, I32, I32, I64, I64, P, P, SZ, P]
     lib.nngp_knn_prior.restype = ctypes.c_int
-    lib.nngp_knn_prior_rows.argtypes = [P, I64, I32, P, I64, P, P, SZ, P]
+    lib.nngp_knn_prior_rows.argtypes = [P, I64, I32, I32, P, I64, P, P, SZ, P]
     lib.nngp_knn_prior_rows.restype = ctypes.c_int
-    lib.nngp_knn_query.argtypes = [P, I64, P, I64, I32, P, P, SZ, P]
+    lib.nngp_knn_query.argtypes = [P, I64, I32, P, I64, I32, P, P, SZ, P]
     lib.nngp_knn_query.restype = ctypes.c_int
-    lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32]
+    lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32, I32, I32]
     lib.nngp_bf_sweep_workspace_bytes.restype = SZ
-    lib.nngp_bf_sweep.argtypes = [P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, I32, P]
-    lib.nngp_bf_cross.argtypes = [P, I64, P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_sweep.argtypes = [P, I64, I32, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_cross.argtypes = [P, I64, I32, P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, P, SZ, I32,
+                                  P]
     lib.nngp_bf_cross.restype = ctypes.c_int
     lib.nngp_row_order_workspace_bytes.argtypes = [I64]
     lib.nngp_row_order_workspace_bytes.restype = SZ
-    lib.nngp_row_order.argtypes = [P, I64, P, I32, I64, I64, P, P, P, SZ, P]
+    lib.nngp_row_order.argtypes = [P, I64, I32, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
-    lib.nngp_bf_finalize.argtypes = [P, I64, I32, I32, P, P]
+    lib.nngp_bf_finalize.argtypes = [P, I64, I32, I32, I32, I32, P, P]
     lib.nngp_bf_finalize.restype = ctypes.c_int
     lib.nngp_combine_partials.restype = ctypes.c_int
     U64 = ctypes.c_uint64
@@ -160,9 +162,18 @@ def _workspace(nbytes: int, dev: torch.device) -> torch.Tensor:
 
 
 def _as_coords(coords: torch.Tensor) -> torch.Tensor:
-    if coords.dim() != 2 or coords.shape[1] != 2 or coords.dtype != torch.float64:
-        raise ValueError(f"coords must be float64 (N, 2), got {tuple(coords.shape)} {coords.dtype}")
+    """float64 (N, dim) ordinates, 1 <= dim <= 3 (nngp.py:55-61 takes any dimension)."""
+    if coords.dim() != 2 or not 1 <= coords.shape[1] <= MAX_DIM or coords.dtype != torch.float64:
+        raise ValueError(f"coords must be float64 (N, dim), 1 <= dim <= {MAX_DIM}, got {tuple(coords.shape)} "
+                         f"{coords.dtype}")
     return coords.contiguous()
+
+
+def _same_dim(*coords: torch.Tensor) -> int:
+    dims = {c.shape[1] for c in coords}
+    if len(dims) != 1:
+        raise ValueError(f"coordinate arrays of different dimensions: {sorted(dims)}")
+    return dims.pop()
 
 
 def _check_out(t: Optional[torch.Tensor], name: str, shape, dev: torch.device) -> None:
@@ -190,8 +201,9 @@ def knn_prior(coords: torch.Tensor, m: int, q0: int = 0, q1: Optional[int] = Non
     if out is None:
         out = torch.empty((q1 - q0, m), dtype=torch.int32, device=dev)
     lib = load()
-    ws = _workspace(lib.nngp_knn_workspace_bytes(n, m), dev)
-    _check(lib.nngp_knn_prior(_ptr(coords), n, m, q0, q1, _ptr(out), _ptr(ws), ws.numel(), _stream(dev)),
+    d = coords.shape[1]
+    ws = _workspace(lib.nngp_knn_workspace_bytes(n, d, m), dev)
+    _check(lib.nngp_knn_prior(_ptr(coords), n, d, m, q0, q1, _ptr(out), _ptr(ws), ws.numel(), _stream(dev)),
            "nngp_knn_prior")
     return out
 
@@ -209,8 +221,9 @@ def knn_prior_rows(coords: torch.Tensor, m: int, rows: torch.Tensor,
     if out is None:
         out = torch.empty((rows.shape[0], m), dtype=torch.int32, device=dev)
     lib = load()
-    ws = _workspace(lib.nngp_knn_workspace_bytes(n, m), dev)
-    _check(lib.nngp_knn_prior_rows(_ptr(coords), n, m, _ptr(rows), rows.shape[0], _ptr(out), _ptr(ws), ws.numel(),
+    d = coords.shape[1]
+    ws = _workspace(lib.nngp_knn_workspace_bytes(n, d, m), dev)
+    _check(lib.nngp_knn_prior_rows(_ptr(coords), n, d, m, _ptr(rows), rows.shape[0], _ptr(out), _ptr(ws), ws.numel(),
                                    _stream(dev)), "nngp_knn_prior_rows")
     return out
 
@@ -224,11 +237,12 @@ def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
     """
     ref = _as_coords(ref)
     query = _as_coords(query)
+    d = _same_dim(ref, query)
     dev = _require_gpu(ref, query)
     out = torch.empty((query.shape[0], k), dtype=torch.int32, device=dev)
     lib = load()
-    ws = _workspace(lib.nngp_knn_workspace_bytes(ref.shape[0], k), dev)
-    _check(lib.nngp_knn_query(_ptr(ref), ref.shape[0], _ptr(query), query.shape[0], k, _ptr(out), _ptr(ws),
+    ws = _workspace(lib.nngp_knn_workspace_bytes(ref.shape[0], d, k), dev)
+    _check(lib.nngp_knn_query(_ptr(ref), ref.shape[0], d, _ptr(query), query.shape[0], k, _ptr(out), _ptr(ws),
                               ws.numel(), _stream(dev)), "nngp_knn_query")
     return out
 
@@ -280,7 +294,8 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     else:
         _check_out(partials, "partials", (4,), dev)
         partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
-    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
+    d = coords.shape[1]
+    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, KIND_CODES[kind], d, a)
     if workspace is None or workspace.numel() < need:
         if defer:
             raise ValueError("defer=True needs a workspace of nngp_bf_sweep_workspace_bytes bytes")
@@ -288,7 +303,7 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     _check_out(R, "R", (rows,), dev)
     if workspace.device != dev or not workspace.is_contiguous():
         raise ValueError("workspace must be a contiguous tensor on the sweep's device")
-    _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
+    _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], d, _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
                              float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
@@ -296,13 +311,14 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
 
 
 def bf_finalize(workspace: torch.Tensor, rows: int, m: int, algo: str = "auto",
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, kind: str = "exponential", dim: int = 2) -> torch.Tensor:
     """Fold the block records a ``bf_sweep(..., defer=True)`` left in ``workspace`` into
-    ``out`` (float64 (4,)), on torch's current stream (nngp_bf_finalize)."""
+    ``out`` (float64 (4,)), on torch's current stream (nngp_bf_finalize); ``kind`` / ``dim``
+    as the sweep's (they select the kernel, hence the record layout, under ``algo="auto"``)."""
     dev = _require_gpu(workspace, out)
     out = torch.empty(4, dtype=torch.float64, device=dev) if out is None else out
-    _check(load().nngp_bf_finalize(_ptr(workspace), int(rows), int(m), ALGO_CODES[algo], _ptr(out), _stream(dev)),
-           "nngp_bf_finalize")
+    _check(load().nngp_bf_finalize(_ptr(workspace), int(rows), int(m), KIND_CODES[kind], int(dim), ALGO_CODES[algo],
+                                   _ptr(out), _stream(dev)), "nngp_bf_finalize")
     return out
 
 
@@ -321,6 +337,7 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
     kriging mean when ``query_values`` is None).
     """
     ref, query = _as_coords(ref), _as_coords(query)
+    d = _same_dim(ref, query)
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
         raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
     nbr = nbr.contiguous()
@@ -347,10 +364,10 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
     B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
     F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
     partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
-    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, a)
+    need = lib.nngp_bf_sweep_workspace_bytes(rows, m, KIND_CODES[kind], d, a)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
-    _check(lib.nngp_bf_cross(_ptr(ref), ref.shape[0], _ptr(query), query.shape[0], _ptr(nbr), _ptr(order), rows, m,
+    _check(lib.nngp_bf_cross(_ptr(ref), ref.shape[0], d, _ptr(query), query.shape[0], _ptr(nbr), _ptr(order), rows, m,
                              int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(ref_values),
                              _ptr(query_values), _ptr(B), _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace),
                              workspace.numel(), a, _stream(dev)), "nngp_bf_cross")
@@ -381,8 +398,8 @@ def row_order(coords: torch.Tensor, i0: int = 0, rows: Optional[int] = None,
     if need == 0:
         raise NNGPExtensionError("nngp_row_order_workspace_bytes failed")
     ws = _workspace(need, dev)
-    _check(lib.nngp_row_order(_ptr(coords), n, _ptr(nbr), m, i0, rows, _ptr(out), _ptr(srt), _ptr(ws), ws.numel(),
-                              _stream(dev)), "nngp_row_order")
+    _check(lib.nngp_row_order(_ptr(coords), n, coords.shape[1], _ptr(nbr), m, i0, rows, _ptr(out), _ptr(srt), _ptr(ws),
+                              ws.numel(), _stream(dev)), "nngp_row_order")
     return out, srt
 
 
@@ -398,9 +415,12 @@ def combine_partials(gathered: torch.Tensor, out: Optional[torch.Tensor] = None)
     return out
 
 
-def bf_workspace(rows: int, m: int, algo: str, device) -> torch.Tensor:
-    """Pre-allocate a sweep workspace (reuse it across calls in a hot loop)."""
-    return _workspace(load().nngp_bf_sweep_workspace_bytes(rows, m, ALGO_CODES[algo]), torch.device(device))
+def bf_workspace(rows: int, m: int, algo: str, device, kind: Optional[str] = None, dim: int = 2) -> torch.Tensor:
+    """Pre-allocate a sweep workspace (reuse it across calls in a hot loop); ``kind=None``
+    sizes it for any covariance kind."""
+    kinds = KIND_CODES.values() if kind is None else (KIND_CODES[kind],)
+    need = max(load().nngp_bf_sweep_workspace_bytes(rows, m, k, int(dim), ALGO_CODES[algo]) for k in kinds)
+    return _workspace(need, torch.device(device))
 
 
 # ---------------------------------------------------------------------------- Gibbs sampler pieces

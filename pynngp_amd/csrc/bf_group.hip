@@ -11,10 +11,6 @@ bool bf_pair_launch_d(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch_b(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch_c(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pairb_launch_a(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pairb_launch_b(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pairb_launch_c(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pairb_launch_d(const BfArgs&, const CovParams&, hipStream_t);
 
 int64_t bf_group_blocks(int64_t n_rows, int P) { return (n_rows * P + 255) / 256; }
 
@@ -32,16 +28,6 @@ bool bf_group_launch(const BfArgs& a, const CovParams& Pc, int P, hipStream_t s)
     if (a.m <= 16) return bf_pair_launch_b(a, Pc, s);
     if (a.m <= 18) return bf_pair_launch_c(a, Pc, s);
     return bf_pair_launch_d(a, Pc, s);
-}
-
-bool bf_pairb_supported(int m) { return m >= 1 && m <= 24; }
-
-bool bf_pairb_launch(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    if (!bf_pairb_supported(a.m)) return false;
-    if (a.m <= 11) return bf_pairb_launch_a(a, Pc, s);
-    if (a.m <= 16) return bf_pairb_launch_b(a, Pc, s);
-    if (a.m <= 20) return bf_pairb_launch_c(a, Pc, s);
-    return bf_pairb_launch_d(a, Pc, s);
 }
 
 }  // namespace nngp

@@ -30,6 +30,7 @@
 
 #include "nngp_math.h"
 #include "nngp_internal.h"
+#include "bf_pairb.h"
 
 namespace nngp {
 
@@ -244,10 +245,11 @@ static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
     }
 }
 
-int64_t bf_record_count(int64_t n_rows, int algo) {
+int64_t bf_record_count(int64_t n_rows, int algo, int m) {
     if (n_rows == 0) return 0;
     if (algo == kAlgoLane) return bf_lane_blocks(n_rows);
-    if (algo == kAlgoPairB || algo == kAlgoPair) return bf_group_blocks(n_rows, 2);
+    if (algo == kAlgoPairB) return bf_pairb_blocks(n_rows, m);
+    if (algo == kAlgoPair || algo == kAlgoPairBR1) return bf_group_blocks(n_rows, 2);
     if (algo == kAlgoQuad) return bf_group_blocks(n_rows, 4);
     return bf_wave_blocks(n_rows);
 }
@@ -261,18 +263,22 @@ hipError_t bf_finalize_launch(const double* bpart, int64_t n_records, double* pa
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     if (a.n_rows == 0)  // empty shard: partials = [0, 0, -1, -1]
         return a.partials != nullptr ? bf_finalize_launch(a.bpart, 0, a.partials, s) : hipSuccess;
-    const CovParams P = nngp_cov_params(a.sigma2, a.phi, a.tau2);
+    const CovParams P = nngp_cov_params(a.kind, a.sigma2, a.phi, a.tau2);
     bool ok;
     int64_t nb;
     if (algo == kAlgoLane) {
-        ok = a.kind == 1 ? launch_lane_m<1>(a, P, s) : launch_lane_m<0>(a, P, s);
+        ok = a.dim == 2 && (a.kind == 1 ? launch_lane_m<1>(a, P, s) : a.kind == 0 && launch_lane_m<0>(a, P, s));
         nb = bf_lane_blocks(a.n_rows);
     } else if (algo == kAlgoPairB) {
-        ok = bf_pairb_launch(a, P, s);
+        // unit-variance factorisation (nngp_cov_unit), F scaled by sigma2 in the kernel
+        ok = bf_pairb_launch(a, nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2), s);
+        nb = bf_pairb_blocks(a.n_rows, a.m);
+    } else if (algo == kAlgoPairBR1) {
+        ok = bf_pairb_r1_launch(a, P, s);
         nb = bf_group_blocks(a.n_rows, 2);
     } else if (algo == kAlgoPair || algo == kAlgoQuad) {
         const int lanes = algo == kAlgoPair ? 2 : 4;
-        ok = bf_group_launch(a, P, lanes, s);
+        ok = a.dim == 2 && a.kind <= 1 && bf_group_launch(a, P, lanes, s);
         nb = bf_group_blocks(a.n_rows, lanes);
     } else {
         nb = bf_wave_blocks(a.n_rows);

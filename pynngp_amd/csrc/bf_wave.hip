@@ -15,11 +15,28 @@ namespace nngp {
 // --------------------------------------------------------------------------
 // one wave per location; lane a owns row a of the joint block (NR >= M+1 rows)
 // --------------------------------------------------------------------------
+// Generic path: the kind and the dimension are runtime arguments (wave-uniform, so the
+// kind switch is a scalar branch and only one path runs), coordinates are zero-padded to
+// three axes (the extra terms of the squared distance add exact zeros, so D = 1 / 2 give the
+// bits of their own point_d2<D>): three instantiations instead of one per (kind, D).
 template <int NR, int KIND>
-__global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coords, int64_t n_points,
+__device__ __forceinline__ void wave_row(const CovParams& P, const double* etab, const double (&xg)[3], int lane,
+                                         double (&row)[NR]) {
+#pragma unroll
+    for (int b = 0; b < NR; ++b) {
+        double xb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xb[k] = wave_bcast(xg[k], b);
+        const double c = nngp_cov_d2<KIND>(P, etab, point_d2<3>(xg, xb));
+        row[b] = b == lane ? P.diag : c;
+    }
+}
+
+template <int NR>
+__global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords, int64_t n_points, int dim, int kind,
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0, int M,
-                                               const CovParams P, const double* __restrict__ values, const double2* __restrict__ qcoords, const double* __restrict__ qvalues,
+                                               const CovParams P, const double* __restrict__ values, const double* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
                                                double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
@@ -39,21 +56,23 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
         const bool is_self = lane == M;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
         const bool bad_index = j >= 0 && !in_range;
-        const double2* pc = is_self ? qcoords + i : (in_range ? coords + j : kFarPoints + lane);
+        const double* pc = is_self ? qcoords + i * dim
+                                   : (in_range ? coords + (int64_t)j * dim : far_point<1>(lane));  // far: (x, 0, 0)
         const double* pv = is_self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                    : ((values != nullptr && in_range) ? values + j : kZeroValue);
-        const double2 xg = *pc;
-        const double xx = xg.x, xy = xg.y;
+        double xg[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) xg[k] = (k < dim && (k == 0 || is_self || in_range)) ? pc[k] : 0.0;
         double zv = *pv;
 
         // row `lane` of the joint block (entries b <= lane are meaningful)
         double row[NR];
-#pragma unroll
-        for (int b = 0; b < NR; ++b) {
-            const double bx = wave_bcast(xx, b);
-            const double by = wave_bcast(xy, b);
-            const double c = nngp_cov_d2<KIND>(P, etab, nngp_d2(xx, xy, bx, by));
-            row[b] = b == lane ? P.diag : c;
+        switch (kind) {
+            case 0: wave_row<NR, 0>(P, etab, xg, lane, row); break;
+            case 1: wave_row<NR, 1>(P, etab, xg, lane, row); break;
+            case 2: wave_row<NR, 2>(P, etab, xg, lane, row); break;
+            case 3: wave_row<NR, 3>(P, etab, xg, lane, row); break;
+            default: wave_row<NR, 4>(P, etab, xg, lane, row); break;
         }
         bool bad = false;
         double ip_mine = 1.0;  // lane p keeps 1/L[p][p]
@@ -111,10 +130,11 @@ __global__ __launch_bounds__(256) void bf_wave(const double2* __restrict__ coord
     block_partials_store(lf_acc, q_acc, badp, badi, bpart, blockIdx.x);
 }
 
-template <int NR, int KIND>
+template <int NR>
 static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s) {
-    hipLaunchKernelGGL((bf_wave<NR, KIND>), dim3((unsigned)n_blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
+    hipLaunchKernelGGL((bf_wave<NR>), dim3((unsigned)n_blocks), dim3(256), 0, s, a.coords, a.n_points, a.dim,
+                       a.kind, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R,
+                       a.bpart);
 }
 
 int64_t bf_wave_blocks(int64_t n_rows) {
@@ -123,21 +143,18 @@ int64_t bf_wave_blocks(int64_t n_rows) {
     return b < 1 ? 1 : (b > 2048 ? 2048 : b);
 }
 
-template <int KIND>
-static bool launch_wave_m_k(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
+// every kind and dimension: the generic path (any m <= 63)
+bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
+    if (a.dim < 1 || a.dim > 3 || a.kind < 0 || a.kind > 4) return false;
     if (a.m + 1 <= 16)
-        launch_wave<16, KIND>(a, P, nb, s);
+        launch_wave<16>(a, P, nb, s);
     else if (a.m + 1 <= 32)
-        launch_wave<32, KIND>(a, P, nb, s);
+        launch_wave<32>(a, P, nb, s);
     else if (a.m + 1 <= 64)
-        launch_wave<64, KIND>(a, P, nb, s);
+        launch_wave<64>(a, P, nb, s);
     else
         return false;
     return true;
-}
-
-bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
-    return a.kind == 1 ? launch_wave_m_k<1>(a, P, nb, s) : launch_wave_m_k<0>(a, P, nb, s);
 }
 
 }  // namespace nngp

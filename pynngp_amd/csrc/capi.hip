@@ -8,6 +8,7 @@
 
 #include "../../include/nngp.h"
 #include "nngp_internal.h"
+#include "bf_pairb.h"
 
 namespace {
 thread_local char g_err[512] = "";
@@ -27,25 +28,25 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order
-// (tools/algo_table.py; DESIGN.md 4, profiles/r01d/algo_table.jsonl): one lane per
-// location while the joint block still leaves room for latency hiding (m <= 10; the
-// blocked pair kernel is within 2-7 % there), the 2x2-blocked two-lane kernel for
-// 11 <= m <= 24 (~10x the wavefront kernel even at one wave per SIMD), one wavefront
-// per location above.
-int resolve_algo(int32_t algo, int32_t m) {
+// (tools/algo_table.py): for the configurations' 2-D exponential / Matern-3/2
+// fields one lane per location while the joint block still leaves room for latency
+// hiding (m <= 10), the persistent 2x2-blocked two-lane kernel for 11 <= m <= 24, four lanes
+// for 25..32, one wavefront per location above.  Other kinds and dimensions are
+// instantiated for the blocked pair kernel (m <= 24) and the wavefront kernel.
+int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     if (algo != NNGP_ALGO_AUTO) return algo;
-    if (m >= 1 && m <= 10) return nngp::kAlgoLane;
-    if (m >= 11 && m <= 24) return nngp::kAlgoPairB;
-    if (m >= 25 && m <= 32) return nngp::kAlgoQuad;  // ~10x bf_wave (tools/algo_table.py)
+    const bool classic = dim == 2 && (kind == NNGP_COV_EXPONENTIAL || kind == NNGP_COV_MATERN32);
+    if (classic) {
+        if (m >= 1 && m <= 10) return nngp::kAlgoLane;
+        if (m >= 11 && m <= 24) return nngp::kAlgoPairB;
+        if (m >= 25 && m <= 32) return nngp::kAlgoQuad;  // ~10x bf_wave (tools/algo_table.py)
+        return nngp::kAlgoWave;
+    }
+    if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
     return nngp::kAlgoWave;
 }
 
-int64_t bf_blocks(int64_t n_rows, int algo) {
-    if (algo == nngp::kAlgoLane) return nngp::bf_lane_blocks(n_rows);
-    if (algo == nngp::kAlgoPair || algo == nngp::kAlgoPairB) return nngp::bf_group_blocks(n_rows, 2);
-    if (algo == nngp::kAlgoQuad) return nngp::bf_group_blocks(n_rows, 4);
-    return nngp::bf_wave_blocks(n_rows);
-}
+int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_count(n_rows, algo, m); }
 }  // namespace
 
 extern "C" {
@@ -67,75 +68,84 @@ double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
     return -0.5 * ((double)n_rows * 1.8378770664093453 + p[0] + p[1]);
 }
 
-size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t algo) {
-    if (n_rows < 0) return 0;
-    const int a = resolve_algo(algo, m);
-    const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a) : 0;
+size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo) {
+    if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return 0;
+    const int a = resolve_algo(algo, m, kind, dim);
+    const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a, m) : 0;
     return align256((size_t)nb * 4 * sizeof(double));
 }
 
-static int bf_common(const double* coords, int64_t n_points, const double* qcoords, int64_t n_locs,
+static int bf_common(const double* coords, int64_t n_points, int32_t dim, const double* qcoords, int64_t n_locs,
                      const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t i0, int32_t kind,
                      double sigma2, double phi, double tau2, const double* values, const double* qvalues, double* B,
                      double* F, double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo,
                      void* stream) {
     if (coords == nullptr || qcoords == nullptr || workspace == nullptr)
         return fail(NNGP_EINVAL, "coordinates and workspace must be non-null");
+    if (dim < 1 || dim > NNGP_MAX_DIM) return fail(NNGP_EUNSUP, "dim=%d outside [1, %d]", dim, NNGP_MAX_DIM);
     if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
     if (m > 0 && n_rows > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null for m > 0");
     if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
                     (long long)n_locs);
-    if (kind != NNGP_COV_EXPONENTIAL && kind != NNGP_COV_MATERN32) return fail(NNGP_EINVAL, "unknown kind %d", kind);
+    if (kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_SPHERICAL) return fail(NNGP_EINVAL, "unknown kind %d", kind);
     if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
     if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
     if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
     if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
-    int a = resolve_algo(algo, m);
-    if (a < nngp::kAlgoLane || a > nngp::kAlgoPairB) return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    int a = resolve_algo(algo, m, kind, dim);
+    if (a < nngp::kAlgoLane || a > nngp::kAlgoPairBR1 || a == 6) return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    if (a == nngp::kAlgoPairBR1 && !(m == 15 && kind == NNGP_COV_EXPONENTIAL && dim == 2))
+        return fail(NNGP_EUNSUP, "the round-1 A/B kernel is instantiated for m = 15, exponential, 2-D only");
+    const bool classic = dim == 2 && kind <= NNGP_COV_MATERN32;
+    if ((a == nngp::kAlgoLane || a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !classic)
+        return fail(NNGP_EUNSUP, "the lane / pair / quad kernels serve 2-D exponential and Matern-3/2 only "
+                                 "(kind=%d, dim=%d): use NNGP_ALGO_AUTO, PAIRB or WAVE", kind, dim);
     if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
         return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
     if ((a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !nngp::bf_group_supported(m, a == nngp::kAlgoPair ? 2 : 4))
         return fail(NNGP_EUNSUP, "no %s-lane kernel instantiated for m=%d", a == nngp::kAlgoPair ? "2" : "4", m);
     if (a == nngp::kAlgoPairB && !nngp::bf_pairb_supported(m))
         return fail(NNGP_EUNSUP, "no blocked pair kernel instantiated for m=%d", m);
-    const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, algo);
+    const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo);
     if (workspace_bytes < need)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
 
     hipStream_t s = (hipStream_t)stream;
-    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, sigma2, phi, tau2, order, values, qcoords,
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, dim, sigma2, phi, tau2, order, values, qcoords,
                       qvalues, B, F, R, partials, (double*)workspace};
     hipError_t e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
     return NNGP_OK;
 }
 
-int nngp_bf_sweep(const double* coords, int64_t n_points, const int32_t* nbr, const int32_t* order, int64_t n_rows,
-                  int32_t m, int64_t i0,
-                  int32_t kind, double sigma2, double phi, double tau2, const double* values, double* B, double* F,
-                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
-    return bf_common(coords, n_points, coords, n_points, nbr, order, n_rows, m, i0, kind, sigma2, phi, tau2, values,
-                     values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
+int nngp_bf_sweep(const double* coords, int64_t n_points, int32_t dim, const int32_t* nbr, const int32_t* order,
+                  int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
+                  const double* values, double* B, double* F, double* R, double* partials, void* workspace,
+                  size_t workspace_bytes, int32_t algo, void* stream) {
+    return bf_common(coords, n_points, dim, coords, n_points, nbr, order, n_rows, m, i0, kind, sigma2, phi, tau2,
+                     values, values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
-int nngp_bf_cross(const double* ref, int64_t n_ref, const double* query, int64_t n_query, const int32_t* nbr,
-                  const int32_t* order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind, double sigma2,
-                  double phi, double tau2, const double* ref_values, const double* query_values, double* B, double* F,
-                  double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo, void* stream) {
+int nngp_bf_cross(const double* ref, int64_t n_ref, int32_t dim, const double* query, int64_t n_query,
+                  const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind,
+                  double sigma2, double phi, double tau2, const double* ref_values, const double* query_values,
+                  double* B, double* F, double* R, double* partials, void* workspace, size_t workspace_bytes,
+                  int32_t algo, void* stream) {
     if (query_values != nullptr && ref_values == nullptr)
         return fail(NNGP_EINVAL, "query_values need ref_values");
-    return bf_common(ref, n_ref, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, ref_values,
+    return bf_common(ref, n_ref, dim, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, ref_values,
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
-int nngp_bf_finalize(const void* workspace, int64_t n_rows, int32_t m, int32_t algo, double* partials, void* stream) {
+int nngp_bf_finalize(const void* workspace, int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo,
+                     double* partials, void* stream) {
     if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
-    const int a = resolve_algo(algo, m);
-    hipError_t e = nngp::bf_finalize_launch((const double*)workspace, nngp::bf_record_count(n_rows, a), partials,
+    const int a = resolve_algo(algo, m, kind, dim);
+    hipError_t e = nngp::bf_finalize_launch((const double*)workspace, nngp::bf_record_count(n_rows, a, m), partials,
                                             (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "bf_finalize launch");
     return NNGP_OK;
@@ -244,9 +254,11 @@ int nngp_gibbs_stats(int64_t n, const double* r, const double* Ft, const double*
 
 size_t nngp_row_order_workspace_bytes(int64_t n_rows) { return nngp::row_order_workspace_bytes(n_rows); }
 
-int nngp_row_order(const double* coords, int64_t n_points, const int32_t* nbr, int32_t m, int64_t i0, int64_t n_rows,
-                   int32_t* order, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes, void* stream) {
+int nngp_row_order(const double* coords, int64_t n_points, int32_t dim, const int32_t* nbr, int32_t m, int64_t i0,
+                   int64_t n_rows, int32_t* order, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes,
+                   void* stream) {
     if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
+    if (dim < 1 || dim > NNGP_MAX_DIM) return fail(NNGP_EUNSUP, "dim=%d outside [1, %d]", dim, NNGP_MAX_DIM);
     if (n_rows < 0 || i0 < 0 || i0 + n_rows > n_points)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
                     (long long)n_points);
@@ -259,74 +271,73 @@ int nngp_row_order(const double* coords, int64_t n_points, const int32_t* nbr, i
     const size_t need = nngp::row_order_workspace_bytes(n_rows);
     if (need == 0 || workspace_bytes < need)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
-    hipError_t e = nngp::row_order_launch(coords, i0, n_rows, order, nbr, m, nbr_sorted, workspace, workspace_bytes,
-                                          (hipStream_t)stream);
+    hipError_t e = nngp::row_order_launch(coords, dim, i0, n_rows, order, nbr, m, nbr_sorted, workspace,
+                                          workspace_bytes, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "row_order launch");
     return NNGP_OK;
 }
 
-size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t m) {
+size_t nngp_knn_workspace_bytes(int64_t n_points, int32_t dim, int32_t m) {
     (void)m;
-    if (n_points < 1 || n_points > INT32_MAX) return 0;
+    if (n_points < 1 || n_points > INT32_MAX || dim < 1 || dim > NNGP_MAX_DIM) return 0;
     nngp::KnnPlan p;
-    if (nngp::knn_plan(n_points, &p) != hipSuccess) return 0;
+    if (nngp::knn_plan(n_points, dim, &p) != hipSuccess) return 0;
     return p.total_bytes;
 }
 
-int nngp_knn_prior(const double* coords, int64_t n_points, int32_t m, int64_t q0, int64_t q1, int32_t* nbr,
-                   void* workspace, size_t workspace_bytes, void* stream) {
+static int knn_checks(const double* coords, int64_t n_points, int32_t dim, int32_t m, void* workspace,
+                      size_t workspace_bytes, nngp::KnnPlan* plan) {
     if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
     if (n_points < 1 || n_points > INT32_MAX) return fail(NNGP_EINVAL, "n_points=%lld outside [1, 2^31)", (long long)n_points);
+    if (dim < 1 || dim > NNGP_MAX_DIM) return fail(NNGP_EUNSUP, "dim=%d outside [1, %d]", dim, NNGP_MAX_DIM);
     if (m < 0 || m > 64) return fail(NNGP_EUNSUP, "m=%d outside [0, 64]", m);
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    hipError_t e = nngp::knn_plan(n_points, dim, plan);
+    if (e != hipSuccess) return hip_fail(e, "knn plan");
+    if (workspace_bytes < plan->total_bytes)
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan->total_bytes);
+    return NNGP_OK;
+}
+
+int nngp_knn_prior(const double* coords, int64_t n_points, int32_t dim, int32_t m, int64_t q0, int64_t q1,
+                   int32_t* nbr, void* workspace, size_t workspace_bytes, void* stream) {
+    nngp::KnnPlan plan;
+    const int rc = knn_checks(coords, n_points, dim, m, workspace, workspace_bytes, &plan);
+    if (rc != NNGP_OK) return rc;
     if (q0 < 0 || q1 < q0 || q1 > n_points) return fail(NNGP_EINVAL, "query rows [%lld, %lld) invalid", (long long)q0, (long long)q1);
     if (q1 > q0 && m > 0 && nbr == nullptr) return fail(NNGP_EINVAL, "nbr must be non-null");
-    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
-    nngp::KnnPlan plan;
-    hipError_t e = nngp::knn_plan(n_points, &plan);
-    if (e != hipSuccess) return hip_fail(e, "knn plan");
-    if (workspace_bytes < plan.total_bytes)
-        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
     if (q1 == q0 || m == 0) return NNGP_OK;
-    e = nngp::knn_launch(true, coords, n_points, m, coords, q0, q1, nullptr, nbr, workspace, plan, (hipStream_t)stream);
+    hipError_t e = nngp::knn_launch(true, coords, n_points, m, coords, q0, q1, nullptr, nbr, workspace, plan,
+                                    (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "knn_prior launch");
     return NNGP_OK;
 }
 
-int nngp_knn_prior_rows(const double* coords, int64_t n_points, int32_t m, const int32_t* rows, int64_t n_rows,
-                        int32_t* nbr, void* workspace, size_t workspace_bytes, void* stream) {
-    if (coords == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "coords and workspace must be non-null");
-    if (n_points < 1 || n_points > INT32_MAX) return fail(NNGP_EINVAL, "n_points=%lld outside [1, 2^31)", (long long)n_points);
-    if (m < 0 || m > 64) return fail(NNGP_EUNSUP, "m=%d outside [0, 64]", m);
+int nngp_knn_prior_rows(const double* coords, int64_t n_points, int32_t dim, int32_t m, const int32_t* rows,
+                        int64_t n_rows, int32_t* nbr, void* workspace, size_t workspace_bytes, void* stream) {
+    nngp::KnnPlan plan;
+    const int rc = knn_checks(coords, n_points, dim, m, workspace, workspace_bytes, &plan);
+    if (rc != NNGP_OK) return rc;
     if (n_rows < 0) return fail(NNGP_EINVAL, "n_rows < 0");
     if (n_rows > 0 && m > 0 && (nbr == nullptr || rows == nullptr)) return fail(NNGP_EINVAL, "rows and nbr must be non-null");
-    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
-    nngp::KnnPlan plan;
-    hipError_t e = nngp::knn_plan(n_points, &plan);
-    if (e != hipSuccess) return hip_fail(e, "knn plan");
-    if (workspace_bytes < plan.total_bytes)
-        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
     if (n_rows == 0 || m == 0) return NNGP_OK;
-    e = nngp::knn_launch(true, coords, n_points, m, coords, 0, n_rows, rows, nbr, workspace, plan, (hipStream_t)stream);
+    hipError_t e = nngp::knn_launch(true, coords, n_points, m, coords, 0, n_rows, rows, nbr, workspace, plan,
+                                    (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "knn_prior_rows launch");
     return NNGP_OK;
 }
 
-int nngp_knn_query(const double* ref, int64_t n_ref, const double* query, int64_t n_query, int32_t k, int32_t* nbr,
-                   void* workspace, size_t workspace_bytes, void* stream) {
-    if (ref == nullptr || workspace == nullptr) return fail(NNGP_EINVAL, "ref and workspace must be non-null");
-    if (n_ref < 1 || n_ref > INT32_MAX) return fail(NNGP_EINVAL, "n_ref=%lld outside [1, 2^31)", (long long)n_ref);
-    if (k < 0 || k > 64) return fail(NNGP_EUNSUP, "k=%d outside [0, 64]", k);
+int nngp_knn_query(const double* ref, int64_t n_ref, int32_t dim, const double* query, int64_t n_query, int32_t k,
+                   int32_t* nbr, void* workspace, size_t workspace_bytes, void* stream) {
+    nngp::KnnPlan plan;
+    const int rc = knn_checks(ref, n_ref, dim, k, workspace, workspace_bytes, &plan);
+    if (rc != NNGP_OK) return rc;
     if (n_query < 0) return fail(NNGP_EINVAL, "n_query < 0");
     if (n_query > 0 && k > 0 && (query == nullptr || nbr == nullptr))
         return fail(NNGP_EINVAL, "query and nbr must be non-null");
-    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
-    nngp::KnnPlan plan;
-    hipError_t e = nngp::knn_plan(n_ref, &plan);
-    if (e != hipSuccess) return hip_fail(e, "knn plan");
-    if (workspace_bytes < plan.total_bytes)
-        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, plan.total_bytes);
     if (n_query == 0 || k == 0) return NNGP_OK;
-    e = nngp::knn_launch(false, ref, n_ref, k, query, 0, n_query, nullptr, nbr, workspace, plan, (hipStream_t)stream);
+    hipError_t e = nngp::knn_launch(false, ref, n_ref, k, query, 0, n_query, nullptr, nbr, workspace, plan,
+                                    (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "knn_query launch");
     return NNGP_OK;
 }

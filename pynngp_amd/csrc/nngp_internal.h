@@ -18,6 +18,44 @@ constexpr double kFar = 1e150;
 // the compiler issues them back to back (no exec-masked branch per slot).
 static __device__ double2 kFarPoints[64] = {{1e150, 0.0}, {2e150, 0.0}, {3e150, 0.0}, {4e150, 0.0}, {5e150, 0.0}, {6e150, 0.0}, {7e150, 0.0}, {8e150, 0.0}, {9e150, 0.0}, {10e150, 0.0}, {11e150, 0.0}, {12e150, 0.0}, {13e150, 0.0}, {14e150, 0.0}, {15e150, 0.0}, {16e150, 0.0}, {17e150, 0.0}, {18e150, 0.0}, {19e150, 0.0}, {20e150, 0.0}, {21e150, 0.0}, {22e150, 0.0}, {23e150, 0.0}, {24e150, 0.0}, {25e150, 0.0}, {26e150, 0.0}, {27e150, 0.0}, {28e150, 0.0}, {29e150, 0.0}, {30e150, 0.0}, {31e150, 0.0}, {32e150, 0.0}, {33e150, 0.0}, {34e150, 0.0}, {35e150, 0.0}, {36e150, 0.0}, {37e150, 0.0}, {38e150, 0.0}, {39e150, 0.0}, {40e150, 0.0}, {41e150, 0.0}, {42e150, 0.0}, {43e150, 0.0}, {44e150, 0.0}, {45e150, 0.0}, {46e150, 0.0}, {47e150, 0.0}, {48e150, 0.0}, {49e150, 0.0}, {50e150, 0.0}, {51e150, 0.0}, {52e150, 0.0}, {53e150, 0.0}, {54e150, 0.0}, {55e150, 0.0}, {56e150, 0.0}, {57e150, 0.0}, {58e150, 0.0}, {59e150, 0.0}, {60e150, 0.0}, {61e150, 0.0}, {62e150, 0.0}, {63e150, 0.0}, {64e150, 0.0}};
 static __device__ double kZeroValue[1] = {0.0};
+// the same far points for 1-D and 3-D ordinates (coordinate 0 at (a + 1) 1e150, the rest 0)
+static __device__ double kFarPoints1[64] = {1e150, 2e150, 3e150, 4e150, 5e150, 6e150, 7e150, 8e150, 9e150, 10e150, 11e150, 12e150, 13e150, 14e150, 15e150, 16e150, 17e150, 18e150, 19e150, 20e150, 21e150, 22e150, 23e150, 24e150, 25e150, 26e150, 27e150, 28e150, 29e150, 30e150, 31e150, 32e150, 33e150, 34e150, 35e150, 36e150, 37e150, 38e150, 39e150, 40e150, 41e150, 42e150, 43e150, 44e150, 45e150, 46e150, 47e150, 48e150, 49e150, 50e150, 51e150, 52e150, 53e150, 54e150, 55e150, 56e150, 57e150, 58e150, 59e150, 60e150, 61e150, 62e150, 63e150, 64e150};
+static __device__ double kFarPoints3[64 * 3] = {1e150, 0.0, 0.0, 2e150, 0.0, 0.0, 3e150, 0.0, 0.0, 4e150, 0.0, 0.0, 5e150, 0.0, 0.0, 6e150, 0.0, 0.0, 7e150, 0.0, 0.0, 8e150, 0.0, 0.0, 9e150, 0.0, 0.0, 10e150, 0.0, 0.0, 11e150, 0.0, 0.0, 12e150, 0.0, 0.0, 13e150, 0.0, 0.0, 14e150, 0.0, 0.0, 15e150, 0.0, 0.0, 16e150, 0.0, 0.0, 17e150, 0.0, 0.0, 18e150, 0.0, 0.0, 19e150, 0.0, 0.0, 20e150, 0.0, 0.0, 21e150, 0.0, 0.0, 22e150, 0.0, 0.0, 23e150, 0.0, 0.0, 24e150, 0.0, 0.0, 25e150, 0.0, 0.0, 26e150, 0.0, 0.0, 27e150, 0.0, 0.0, 28e150, 0.0, 0.0, 29e150, 0.0, 0.0, 30e150, 0.0, 0.0, 31e150, 0.0, 0.0, 32e150, 0.0, 0.0, 33e150, 0.0, 0.0, 34e150, 0.0, 0.0, 35e150, 0.0, 0.0, 36e150, 0.0, 0.0, 37e150, 0.0, 0.0, 38e150, 0.0, 0.0, 39e150, 0.0, 0.0, 40e150, 0.0, 0.0, 41e150, 0.0, 0.0, 42e150, 0.0, 0.0, 43e150, 0.0, 0.0, 44e150, 0.0, 0.0, 45e150, 0.0, 0.0, 46e150, 0.0, 0.0, 47e150, 0.0, 0.0, 48e150, 0.0, 0.0, 49e150, 0.0, 0.0, 50e150, 0.0, 0.0, 51e150, 0.0, 0.0, 52e150, 0.0, 0.0, 53e150, 0.0, 0.0, 54e150, 0.0, 0.0, 55e150, 0.0, 0.0, 56e150, 0.0, 0.0, 57e150, 0.0, 0.0, 58e150, 0.0, 0.0, 59e150, 0.0, 0.0, 60e150, 0.0, 0.0, 61e150, 0.0, 0.0, 62e150, 0.0, 0.0, 63e150, 0.0, 0.0, 64e150, 0.0, 0.0};
+
+// ---------------------------------------------------------------- D-dimensional points
+// Ordinates are fp64 (n, D) row-major (the reference's KDTree takes any dimension,
+// nngp.py:55-61).  D = 2 loads a point with one 16-byte load.
+template <int D>
+__device__ __forceinline__ const double* far_point(int a) {
+    if constexpr (D == 1) return kFarPoints1 + (a & 63);
+    else if constexpr (D == 2) return (const double*)(kFarPoints + (a & 63));
+    else return kFarPoints3 + 3 * (a & 63);
+}
+
+template <int D>
+__device__ __forceinline__ void load_point(const double* __restrict__ p, double (&x)[D]) {
+    if constexpr (D == 2) {
+        const double2 v = *(const double2*)p;
+        x[0] = v.x;
+        x[1] = v.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = p[k];
+    }
+}
+
+// squared distance for the covariance, floored at 2^-1000 (nngp_d2's order for D = 2:
+// the last coordinate first, each term one FMA)
+template <int D>
+__device__ __forceinline__ double point_d2(const double (&a)[D], const double (&b)[D]) {
+    double acc = NNGP_D2_FLOOR;
+#pragma unroll
+    for (int k = D - 1; k >= 0; --k) {
+        const double t = a[k] - b[k];
+        acc = fma(t, t, acc);
+    }
+    return acc;
+}
 
 constexpr int kAlgoAuto = 0;
 constexpr int kAlgoLane = 1;
@@ -25,16 +63,18 @@ constexpr int kAlgoWave = 2;
 constexpr int kAlgoPair = 3;  // bf_group, 2 lanes per location
 constexpr int kAlgoQuad = 4;  // bf_group, 4 lanes per location
 constexpr int kAlgoPairB = 5; // bf_pairb, 2 lanes per location, 2x2-blocked elimination
+constexpr int kAlgoPairBR1 = 7;  // the round-1 bf_pairb (m = 15, exponential, 2-D), kept for same-box A/B
 constexpr int kLaneMaxM = 16;
 
 struct BfArgs {
-    const double* coords;  // (n_points, 2) row-major
+    const double* coords;  // (n_points, dim) row-major
     int64_t n_points;
     const int32_t* nbr;  // (n_rows, m), -1 padded; row t is location i0 + (order ? order[t] : t)
     int64_t n_rows;
     int64_t i0;
     int m;
     int kind;
+    int dim;                   // coordinate dimension (1..3)
     double sigma2, phi, tau2;
     const int32_t* order;      // (n_rows,) local row of nbr row t (nngp_row_order layout), or null (identity)
     const double* values;      // (n_points,) or null
@@ -47,7 +87,7 @@ struct BfArgs {
     double* bpart;             // 4 doubles per block: sum log F, sum r^2/F, first bad-pivot row, first bad-index row
 };
 
-int64_t bf_record_count(int64_t n_rows, int algo);
+int64_t bf_record_count(int64_t n_rows, int algo, int m);
 hipError_t bf_finalize_launch(const double* bpart, int64_t n_records, double* partials, hipStream_t s);
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
 hipError_t combine_partials_launch(const double* gathered, int world, double* out, hipStream_t s);
@@ -56,6 +96,7 @@ bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t
 bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
+bool bf_pairb_r1_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 // number of 256-thread blocks (= partial records) each kernel launches for n_rows
 int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);
@@ -65,13 +106,14 @@ constexpr int kKnnMaxLevels = 16;
 // one grid over the prefix s[0:np] of the points (level 0: all of them)
 struct KnnLevel {
     int64_t np;       // points in the prefix
-    int g;            // grid side (g x g cells over the common bounding box)
+    int g;            // grid side (g^dim cells over the common bounding box)
     int64_t n_cells;  // g * g
     size_t off_idx_sorted, off_pts_sorted, off_cell_start;  // byte offsets into the workspace
 };
 struct KnnPlan {
     int64_t n_points;
-    int gx, gy;       // level 0 grid
+    int dim;          // coordinate dimension (1..3)
+    int g;            // level 0 grid side (g^dim cells)
     int64_t n_cells;  // level 0 cells
     int n_levels;
     KnnLevel lv[kKnnMaxLevels];
@@ -81,7 +123,7 @@ struct KnnPlan {
     size_t off_bbox, off_key, off_key_sorted, off_sort_temp, off_idx, off_perm;
 };
 
-hipError_t knn_plan(int64_t n_points, KnnPlan* plan);
+hipError_t knn_plan(int64_t n_points, int dim, KnnPlan* plan);
 // prior mode: rows [q0, q1) of coords against coords[0:i]; query mode: query[q0:q1] against all coords
 // rows: NULL, or (prior mode) the point index of each of the q1 - q0 query rows
 hipError_t knn_launch(bool prior, const double* coords, int64_t n_points, int m, const double* query, int64_t q0,
@@ -110,8 +152,9 @@ hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, cons
 
 // row-order plan (nngp_row_order): Morton-sorted local rows for cache locality
 size_t row_order_workspace_bytes(int64_t n_rows);
-hipError_t row_order_launch(const double* coords, int64_t i0, int64_t n_rows, int32_t* order, const int32_t* nbr,
-                            int m, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes, hipStream_t s);
+hipError_t row_order_launch(const double* coords, int dim, int64_t i0, int64_t n_rows, int32_t* order,
+                            const int32_t* nbr, int m, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes,
+                            hipStream_t s);
 
 // Bijective XCD-aware block remap: blocks are dealt round-robin over the 8 XCDs
 // (b % 8 shares an L2), so give each XCD a contiguous range of logical blocks;

@@ -55,23 +55,42 @@ static __device__ const double kExp2Tab[256] = NNGP_EXP2_TAB;
 #define NNGP_D2_FLOOR 0x1p-1000
 #define NNGP_EXP_TAB_N 256
 
+// Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12; the spNNGP family), u = phi d:
+#define NNGP_KIND_EXPONENTIAL 0  // sigma2 e^-u
+#define NNGP_KIND_MATERN32 1     // sigma2 (1 + u) e^-u
+#define NNGP_KIND_MATERN52 2     // sigma2 (1 + u + u^2 / 3) e^-u
+#define NNGP_KIND_GAUSSIAN 3     // sigma2 e^-u^2          (no square root: the exponent is phi^2 d^2)
+#define NNGP_KIND_SPHERICAL 4    // sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0   (no exponential)
+#define NNGP_N_KINDS 5
+
 // Covariance parameters, built once on the host (nngp_cov_params) and passed by value.
 struct CovParams {
     double q[4];     // (2^(f/256) - 1) / f ~= q0 + q1 f + q2 f^2 + q3 f^3, |f| <= 1/2
-    double nphi256;  // -256 phi log2(e): table units of the exponent per unit distance
-    double d2max;    // squared distance at which sigma2 2^(nphi256 d / 256) has underflowed
-    double phi;      // phi (Matern-3/2 needs phi d)
+    double nphi256;  // table units of the exponent per unit of its variable: -256 log2(e) phi
+                     // (variable d) or -256 log2(e) phi^2 (gaussian: variable d^2)
+    double d2max;    // squared distance beyond which the covariance is 0 (underflowed / past the range)
+    double phi;
     double diag;     // sigma2 + tau2
     double sigma2;
 };
 
-NNGP_HD CovParams nngp_cov_params(double sigma2, double phi, double tau2) {
+NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double tau2) {
     const double q[4] = NNGP_EXP2_Q;
     CovParams p;
     for (int k = 0; k < 4; ++k) p.q[k] = q[k];
-    p.nphi256 = -256.0 * (phi * NNGP_LOG2E);
-    const double dmax = 1080.0 / (phi * NNGP_LOG2E);  // 2^-1080 sigma2 == 0 (or a negligible subnormal)
-    p.d2max = dmax * dmax;
+    if (kind == NNGP_KIND_GAUSSIAN) {
+        p.nphi256 = -256.0 * (phi * phi * NNGP_LOG2E);
+        p.d2max = 1080.0 / (phi * phi * NNGP_LOG2E);  // sigma2 2^-1080: zero (or a negligible subnormal)
+    } else if (kind == NNGP_KIND_SPHERICAL) {
+        p.nphi256 = 0.0;
+        p.d2max = 4.0 / (phi * phi);  // any d2 past (1/phi)^2 gives 0; the clamp keeps sqrt in range
+    } else {
+        p.nphi256 = -256.0 * (phi * NNGP_LOG2E);
+        // 2^-1080 sigma2 == 0; the polynomial factor of the Matern kinds (<= 1 + u + u^2/3 at
+        // u ~ 750) leaves it a subnormal far below any pivot
+        const double dmax = 1080.0 / (phi * NNGP_LOG2E);
+        p.d2max = dmax * dmax;
+    }
     p.phi = phi;
     p.diag = sigma2 + tau2;
     p.sigma2 = sigma2;
@@ -128,17 +147,27 @@ NNGP_FN double nngp_rsqrt(double x) {
     return fma(y, g, y);
 }
 
-// Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12):
-//   0 exponential  sigma2 * exp(-phi d)
-//   1 matern32     sigma2 * (1 + phi d) * exp(-phi d)
-// d2 from nngp_d2 (>= 2^-1000); tab from nngp_exp_table_load(tab, P.sigma2).
+// Covariance of kind KIND (NNGP_KIND_*) at squared distance d2 (from nngp_d2, >= 2^-1000);
+// tab from nngp_exp_table_load(tab, P.sigma2) (unused by the spherical kind).
 template <int KIND>
 NNGP_FN double nngp_cov_d2(const CovParams& P, const double* tab, double d2) {
-    const double d = nngp_sqrt(fmin(d2, P.d2max));
+    const double x = fmin(d2, P.d2max);
+    if (KIND == NNGP_KIND_GAUSSIAN) return nngp_exp_tab(P, tab, x);  // sigma2 2^(nphi256 d2 / 256)
+    const double d = nngp_sqrt(x);
+    if (KIND == NNGP_KIND_SPHERICAL) {
+        const double u = fmin(P.phi * d, 1.0);                       // u = 1: the polynomial is exactly 0
+        const double p = fma(u, fma(0.5 * u, u, -1.5), 1.0);         // 1 + u (u^2 / 2 - 3/2)
+        return P.sigma2 * p;
+    }
     const double e = nngp_exp_tab(P, tab, d);
-    if (KIND == 1) {
+    if (KIND == NNGP_KIND_MATERN32) {
         const double pd = P.phi * d;
         return fma(pd, e, e);
+    }
+    if (KIND == NNGP_KIND_MATERN52) {
+        const double u = P.phi * d;
+        const double p = fma(fma(u, 1.0 / 3.0, 1.0), u, 1.0);       // 1 + u + u^2 / 3
+        return p * e;
     }
     return e;
 }
@@ -150,3 +179,86 @@ NNGP_FN double nngp_d2(double ax, double ay, double bx, double by) {
     const double dy = ay - by;
     return fma(dx, dx, fma(dy, dy, NNGP_D2_FLOOR));
 }
+
+// ---------------------------------------------------------------- unit-variance covariances
+// The persistent kernels (bf_pairb) factor the unit-variance block R + (tau2 / sigma2) I and
+// scale F by sigma2 at the end (B and the value residual are scale-invariant).  With unit
+// variance every table entry 2^(j/256) lies in [1, 2), so 2^n can be applied by adding n to
+// the exponent field instead of an ldexp: the LDS table stores 2^(j/256) with (j << 12)
+// pre-subtracted from its high dword, and for k = 256 n + j the high dword of
+// 2^(j/256) 2^n is (stored high dword) + (k << 12) -- one v_lshl_add_u32 instead of an
+// ashr + v_ldexp_f64.  The exponent argument is clamped so that n >= -1021 (results stay
+// normal): a covariance never falls below 2^-1021 (= 0 for every purpose of the
+// factorisation; far-away padding points decouple to within 4.5e-308).
+NNGP_HD CovParams nngp_cov_params_unit(int kind, double phi, double tau2_over_sigma2) {
+    CovParams p = nngp_cov_params(kind, 1.0, phi, tau2_over_sigma2);
+    if (kind == NNGP_KIND_GAUSSIAN) {
+        p.d2max = 1021.0 / (phi * phi * NNGP_LOG2E);
+    } else if (kind != NNGP_KIND_SPHERICAL) {
+        const double dmax = 1021.0 / (phi * NNGP_LOG2E);
+        p.d2max = dmax * dmax;
+    }
+    return p;
+}
+
+NNGP_FN double nngp_exp_unit(const CovParams& P, const double* tab, double u) {
+    const double t = fma(P.nphi256, u, NNGP_EXP_MAGIC);  // 1.5 2^52 + k, k = rint(nphi256 u) >= -1021 * 256
+    const double k = t - NNGP_EXP_MAGIC;
+    const double f = fma(P.nphi256, u, -k);               // |f| <= 1/2
+    const int32_t ki = nngp_lo_dword(t);
+    const double Tadj = tab[ki & (NNGP_EXP_TAB_N - 1)];   // 2^(j/256), high dword - (j << 12)
+#ifdef NNGP_MATH_HOST
+    uint64_t bits;
+    memcpy(&bits, &Tadj, 8);
+    bits += (uint64_t)((uint32_t)ki << 12) << 32;         // high dword += k << 12 (mod 2^32)
+    double Ts;
+    memcpy(&Ts, &bits, 8);
+#else
+    const long long tb = __double_as_longlong(Tadj);
+    const int32_t hi = (int32_t)(tb >> 32) + (int32_t)((uint32_t)ki << 12);
+    const double Ts = __hiloint2double(hi, (int32_t)(tb & 0xffffffffll));  // 2^(j/256) 2^n
+#endif
+    double q = fma(P.q[3], f, P.q[2]);
+    q = fma(q, f, P.q[1]);
+    q = fma(q, f, P.q[0]);
+    return fma(Ts, f * q, Ts);
+}
+
+// unit-variance covariance of kind KIND at squared distance d2 (tab: nngp_exp_table_load_unit)
+template <int KIND>
+NNGP_FN double nngp_cov_unit(const CovParams& P, const double* tab, double d2) {
+    const double x = fmin(d2, P.d2max);
+    if (KIND == NNGP_KIND_GAUSSIAN) return nngp_exp_unit(P, tab, x);
+    const double d = nngp_sqrt(x);
+    if (KIND == NNGP_KIND_SPHERICAL) {
+        const double u = fmin(P.phi * d, 1.0);
+        return fma(u, fma(0.5 * u, u, -1.5), 1.0);
+    }
+    const double e = nngp_exp_unit(P, tab, d);
+    if (KIND == NNGP_KIND_MATERN32) return fma(P.phi * d, e, e);
+    if (KIND == NNGP_KIND_MATERN52) {
+        const double u = P.phi * d;
+        return fma(fma(u, 1.0 / 3.0, 1.0), u, 1.0) * e;
+    }
+    return e;
+}
+
+#ifndef NNGP_MATH_HOST
+// LDS table for nngp_exp_unit (every thread of the block calls it)
+NNGP_FN void nngp_exp_table_load_unit(double* tab) {
+    for (int j = threadIdx.x; j < NNGP_EXP_TAB_N; j += blockDim.x) {
+        const long long b = __double_as_longlong(kExp2Tab[j]);
+        tab[j] = __hiloint2double((int32_t)(b >> 32) - (j << 12), (int32_t)(b & 0xffffffffll));
+    }
+    __syncthreads();
+}
+#else
+static inline void nngp_exp_table_load_unit(double* tab) {
+    for (int j = 0; j < NNGP_EXP_TAB_N; ++j) {
+        uint64_t b;
+        memcpy(&b, &kExp2Tab[j], 8);
+        b -= (uint64_t)((uint32_t)j << 12) << 32;
+        memcpy(&tab[j], &b, 8);
+    }
+}
+#endif

@@ -17,65 +17,30 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "geom.h"
 #include "nngp_internal.h"
 
 namespace nngp {
 
-__global__ __launch_bounds__(256) void order_bbox_partial(const double2* __restrict__ p, int64_t n,
-                                                          double* __restrict__ out) {
-    double a = INFINITY, b = INFINITY, c = -INFINITY, d = -INFINITY;
-    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
-        const double2 v = p[k];
-        a = fmin(a, v.x);
-        b = fmin(b, v.y);
-        c = fmax(c, v.x);
-        d = fmax(d, v.y);
-    }
-    __shared__ double s[4][256];
-    s[0][threadIdx.x] = a;
-    s[1][threadIdx.x] = b;
-    s[2][threadIdx.x] = c;
-    s[3][threadIdx.x] = d;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            s[0][threadIdx.x] = fmin(s[0][threadIdx.x], s[0][threadIdx.x + o]);
-            s[1][threadIdx.x] = fmin(s[1][threadIdx.x], s[1][threadIdx.x + o]);
-            s[2][threadIdx.x] = fmax(s[2][threadIdx.x], s[2][threadIdx.x + o]);
-            s[3][threadIdx.x] = fmax(s[3][threadIdx.x], s[3][threadIdx.x + o]);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x < 4) out[4 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
-}
-
-__device__ __forceinline__ uint32_t spread_bits16(uint32_t v) {
-    v &= 0xffffu;
-    v = (v | (v << 8)) & 0x00ff00ffu;
-    v = (v | (v << 4)) & 0x0f0f0f0fu;
-    v = (v | (v << 2)) & 0x33333333u;
-    v = (v | (v << 1)) & 0x55555555u;
-    return v;
-}
-
-__global__ __launch_bounds__(256) void morton_keys(const double2* __restrict__ p, int64_t n,
+// Morton code of each row's point, quantised to morton_bits<D>() bits per axis over the
+// bounding box of the rows (folded from the per-block partials by every thread)
+template <int D>
+__global__ __launch_bounds__(256) void morton_keys(const double* __restrict__ p, int64_t n,
                                                    const double* __restrict__ part, int nblk,
                                                    uint32_t* __restrict__ key, int32_t* __restrict__ val) {
-    double minx = INFINITY, miny = INFINITY, maxx = -INFINITY, maxy = -INFINITY;
-    for (int k = 0; k < nblk; ++k) {  // every thread folds the 256 block partials (tiny, cached)
-        minx = fmin(minx, part[4 * k]);
-        miny = fmin(miny, part[4 * k + 1]);
-        maxx = fmax(maxx, part[4 * k + 2]);
-        maxy = fmax(maxy, part[4 * k + 3]);
-    }
+    const Bbox b = bbox_fold<D>(part, nblk);
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    const double sx = maxx > minx ? 65535.0 / (maxx - minx) : 0.0;
-    const double sy = maxy > miny ? 65535.0 / (maxy - miny) : 0.0;
-    const double2 v = p[t];
-    const uint32_t qx = (uint32_t)fmin(fmax((v.x - minx) * sx, 0.0), 65535.0);
-    const uint32_t qy = (uint32_t)fmin(fmax((v.y - miny) * sy, 0.0), 65535.0);
-    key[t] = spread_bits16(qx) | (spread_bits16(qy) << 1);
+    const double top = (double)((1ull << morton_bits<D>()) - 1);
+    double x[D];
+    load_point<D>(p + t * D, x);
+    uint32_t c[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const double sc = b.hi[k] > b.lo[k] ? top / (b.hi[k] - b.lo[k]) : 0.0;
+        c[k] = (uint32_t)fmin(fmax((x[k] - b.lo[k]) * sc, 0.0), top);
+    }
+    key[t] = morton<D>(c);
     val[t] = (int32_t)t;
 }
 
@@ -101,26 +66,41 @@ size_t row_order_workspace_bytes(int64_t n_rows) {
     if (n_rows < 1) return 256;
     const size_t tb = sort_temp_bytes(n_rows);
     if (tb == 0) return 0;
-    return align256(4 * 256 * sizeof(double)) + 3 * align256((size_t)n_rows * 4) + align256(tb);
+    return align256(2 * kMaxDim * 256 * sizeof(double)) + 3 * align256((size_t)n_rows * 4) + align256(tb);
 }
 
-hipError_t row_order_launch(const double* coords, int64_t i0, int64_t n_rows, int32_t* order, const int32_t* nbr,
-                            int m, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes, hipStream_t s) {
+hipError_t row_order_launch(const double* coords, int dim, int64_t i0, int64_t n_rows, int32_t* order,
+                            const int32_t* nbr, int m, int32_t* nbr_sorted, void* workspace, size_t workspace_bytes,
+                            hipStream_t s) {
     if (n_rows < 1) return hipSuccess;
     const size_t tb = sort_temp_bytes(n_rows);
     char* w = (char*)workspace;
     double* part = (double*)w;
-    w += align256(4 * 256 * sizeof(double));
+    w += align256(2 * kMaxDim * 256 * sizeof(double));
     uint32_t* key = (uint32_t*)w;
     w += align256((size_t)n_rows * 4);
     uint32_t* key_sorted = (uint32_t*)w;
     w += align256((size_t)n_rows * 4);
     int32_t* val = (int32_t*)w;
     w += align256((size_t)n_rows * 4);
-    const double2* p = (const double2*)coords + i0;
-    hipLaunchKernelGGL(order_bbox_partial, dim3(256), dim3(256), 0, s, p, n_rows, part);
-    hipLaunchKernelGGL(morton_keys, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s, p, n_rows, part, 256,
-                       key, val);
+    const double* p = coords + i0 * dim;
+    const dim3 nb((unsigned)((n_rows + 255) / 256));
+    switch (dim) {
+        case 1:
+            hipLaunchKernelGGL((bbox_partial<1>), dim3(256), dim3(256), 0, s, p, n_rows, part);
+            hipLaunchKernelGGL((morton_keys<1>), nb, dim3(256), 0, s, p, n_rows, part, 256, key, val);
+            break;
+        case 2:
+            hipLaunchKernelGGL((bbox_partial<2>), dim3(256), dim3(256), 0, s, p, n_rows, part);
+            hipLaunchKernelGGL((morton_keys<2>), nb, dim3(256), 0, s, p, n_rows, part, 256, key, val);
+            break;
+        case 3:
+            hipLaunchKernelGGL((bbox_partial<3>), dim3(256), dim3(256), 0, s, p, n_rows, part);
+            hipLaunchKernelGGL((morton_keys<3>), nb, dim3(256), 0, s, p, n_rows, part, 256, key, val);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
     size_t t = tb;
     (void)workspace_bytes;
     hipError_t e = rocprim::radix_sort_pairs((void*)w, t, key, key_sorted, val, order, (size_t)n_rows, 0u, 32u, s);

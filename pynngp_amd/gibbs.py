@@ -39,7 +39,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ops
 from .nngp import NNGPNumericalError, _default_device
 
 
@@ -137,7 +137,9 @@ class SeqNNGP:
         self._B2, self._Ft2, self._r2 = z(n, self.m), z(n), z(n)
         self._part = z(4)
         self._z = z(n)
-        self._ws = _lib.bf_workspace(n, self.m, algo, dev)
+        self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
+        ops.load()  # the sweep goes through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
+        self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
         self._stats = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
         self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k)
@@ -155,8 +157,8 @@ class SeqNNGP:
 
     def _sweep_into(self, phi, B, Ft, r):
         """Factors of the unit-variance NNGP at phi, and residuals of the current w."""
-        _lib.bf_sweep(self.coords, self.nbr, 0, self.kind, 1.0, phi, 0.0, values=self.w, want_bf=True,
-                      algo=self.algo, B=B, F=Ft, partials=self._part, workspace=self._ws, R=r)
+        torch.ops.nngp.bf_sweep_out(self.coords, self.nbr, None, 0, self._kind_code, 1.0, float(phi), 0.0, self.w, B,
+                                    Ft, r, self._part, self._ws, self._algo_code)
 
     @staticmethod
     def _check(p):

@@ -40,12 +40,14 @@ LOG_2PI = math.log(2.0 * math.pi)
 
 @dataclasses.dataclass(frozen=True)
 class Covariance:
-    """Parent-GP covariance plug-in (the reference's ``cov``, nngp.py:6,12).
+    """Parent-GP covariance plug-in (the reference's ``cov``, nngp.py:6,12), u = phi d:
 
-    ``exponential``: sigma2 exp(-phi d); ``matern32``: sigma2 (1 + phi d) exp(-phi d);
+    ``exponential`` sigma2 e^-u; ``matern32`` sigma2 (1 + u) e^-u; ``matern52``
+    sigma2 (1 + u + u^2/3) e^-u; ``gaussian`` sigma2 e^-u^2; ``spherical``
+    sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family, fused in the kernels).
     ``tau2`` is a nugget added to the diagonal (response model; 0 = latent model).
-    Called as ``cov(a, b)`` on coordinate rows (numpy or torch), it returns the
-    cross-covariance matrix without the nugget, like a reference plug-in would.
+    Called as ``cov(a, b)`` on coordinate rows of any dimension (numpy or torch), it
+    returns the cross-covariance matrix without the nugget, like a reference plug-in would.
     """
 
     kind: str
@@ -68,13 +70,21 @@ class Covariance:
 
     def __call__(self, a, b):
         lib = torch if isinstance(a, torch.Tensor) else np
-        a = a.reshape(-1, 2)
-        b = b.reshape(-1, 2)
-        dx = a[:, None, 0] - b[None, :, 0]
-        dy = a[:, None, 1] - b[None, :, 1]
-        pd = self.phi * lib.sqrt(dx * dx + dy * dy)
-        e = self.sigma2 * lib.exp(-pd)
-        return e * (1.0 + pd) if self.kind == "matern32" else e
+        d = a.shape[-1] if a.ndim > 1 else b.shape[-1] if b.ndim > 1 else 1
+        a = a.reshape(-1, d)
+        b = b.reshape(-1, d)
+        t = a[:, None, :] - b[None, :, :]
+        u = self.phi * lib.sqrt((t * t).sum(-1))
+        if self.kind == "gaussian":
+            return self.sigma2 * lib.exp(-u * u)
+        if self.kind == "spherical":
+            return lib.where(u < 1.0, self.sigma2 * (1.0 - 1.5 * u + 0.5 * u * u * u), 0.0 * u)
+        e = self.sigma2 * lib.exp(-u)
+        if self.kind == "matern32":
+            return e * (1.0 + u)
+        if self.kind == "matern52":
+            return e * (1.0 + u + u * u / 3.0)
+        return e
 
 
 CovLike = Union[Covariance, Callable, None]
@@ -116,18 +126,24 @@ class NNGP:
         t_host = np.ascontiguousarray(self.t, dtype=np.float64)
         if not np.all(np.isfinite(t_host)):  # as sklearn's KDTree / KNeighborsRegressor (nngp.py:46,55)
             raise ValueError("Input contains NaN or infinity (ordinates t)")
+        if t_host.ndim == 1:  # a 1-D series given as a vector
+            t_host = t_host[:, None]
         self._t_dev = torch.as_tensor(t_host).to(self.device)
-        if self._t_dev.dim() != 2 or self._t_dev.shape[1] != 2:
-            raise ValueError(f"ordinates must be (N, 2), got {tuple(self._t_dev.shape)}")
+        if self._t_dev.dim() != 2 or not 1 <= self._t_dev.shape[1] <= _lib.MAX_DIM:
+            raise ValueError(f"ordinates must be (N, d) with 1 <= d <= {_lib.MAX_DIM}, got {tuple(self._t_dev.shape)}")
         if self.s is self.t:
             self._s_dev = self._t_dev
         else:
             s_host = np.ascontiguousarray(self.s, dtype=np.float64)
+            if s_host.ndim == 1:
+                s_host = s_host[:, None]
             if not np.all(np.isfinite(s_host)):
                 raise ValueError("Input contains NaN or infinity (reference set s)")
             self._s_dev = torch.as_tensor(s_host).to(self.device)
-            if self._s_dev.dim() != 2 or self._s_dev.shape[1] != 2 or self._s_dev.shape[0] < 1:
-                raise ValueError(f"reference set must be (nRef >= 1, 2), got {tuple(self._s_dev.shape)}")
+            if (self._s_dev.dim() != 2 or self._s_dev.shape[1] != self._t_dev.shape[1]
+                    or self._s_dev.shape[0] < 1):
+                raise ValueError(f"reference set must be (nRef >= 1, {self._t_dev.shape[1]}), "
+                                 f"got {tuple(self._s_dev.shape)}")
 
     def _init_wt(self):
         self.wt = np.copy(self.y)

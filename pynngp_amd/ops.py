@@ -1,82 +1,96 @@
-"""PyTorch-ROCm custom ops over the C ABI: ``torch.ops.nngp.*``.
+"""PyTorch-ROCm operators ``torch.ops.nngp.*`` (native: ``libnngp_torch_ops.so``).
 
-Registered with ``torch.library.custom_op`` for the CUDA (= HIP on ROCm)
-dispatch key only, so CPU tensors raise instead of silently falling back.
-Fake (meta) kernels give shapes for tracing.
+The operators are registered in C++ with ``TORCH_LIBRARY(nngp, ...)``
+(``pynngp_amd/csrc/torch_ops.cpp``) and implemented for the CUDA (= HIP on ROCm)
+dispatch key only, straight over the C ABI of ``libnngp_hip.so`` on torch's current
+stream: CPU tensors raise, there is no fallback.  :func:`load` (called by
+``pynngp_amd.load_ops()`` and by the classes that sweep through these ops) loads the
+library, loudly failing when it is not built, and registers the fake (meta) kernels used
+for tracing.
 
-    torch.ops.nngp.bf_sweep(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo)
-        -> (B, F, partials)
     torch.ops.nngp.knn_prior(coords, m, q0, q1) -> nbr
+    torch.ops.nngp.knn_prior_rows(coords, m, rows) -> nbr
     torch.ops.nngp.knn_query(ref, query, k) -> nbr
+    torch.ops.nngp.bf_sweep(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None)
+        -> (B, F, partials)
+    torch.ops.nngp.bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials,
+                                workspace, algo) -> ()       # the hot path: caller-owned buffers
     torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo) -> (B, F, mean)
+    torch.ops.nngp.row_order(coords, i0, rows, nbr) -> (order, nbr_sorted)
+    torch.ops.nngp.combine_partials_out(gathered, out) -> ()
+
+``kind`` / ``algo`` are the integer codes of include/nngp.h (:func:`kind_code`, :func:`algo_code`).
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+import os
 
 import torch
 
 from . import _lib
 
-_KINDS = ("exponential", "matern32")
-_ALGOS = ("auto", "lane", "wave", "pair", "quad", "pairb")
+_KINDS = tuple(_lib.KIND_CODES)  # code order: exponential, matern32, matern52, gaussian, spherical
+_ALGOS = dict(_lib.ALGO_CODES)
+LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libnngp_torch_ops.so")
+
+_loaded = False
 
 
-@torch.library.custom_op("nngp::bf_sweep", mutates_args=(), device_types="cuda")
-def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: int, sigma2: float, phi: float, tau2: float,
-             values: Optional[torch.Tensor], want_bf: bool, algo: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    B, F, partials = _lib.bf_sweep(coords, nbr, i0, _KINDS[kind], sigma2, phi, tau2, values, want_bf, _ALGOS[algo])
-    if not want_bf:
+def load() -> None:
+    """Load the operator library once (it links libnngp_hip.so); raise if it is not built."""
+    global _loaded
+    if _loaded:
+        return
+    if not os.path.exists(LIB_PATH):
+        raise _lib.NNGPExtensionError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(pynngp_amd has no CPU fallback)")
+    _lib.load()  # the libnngp_hip.so the op library links (one copy in the process)
+    torch.ops.load_library(LIB_PATH)
+    _register_fakes()
+    _loaded = True
+
+
+def _register_fakes() -> None:
+    def fake(name):
+        return torch.library.register_fake(f"nngp::{name}")
+
+    @fake("knn_prior")
+    def _(coords, m, q0, q1):
+        return coords.new_empty((q1 - q0, m), dtype=torch.int32)
+
+    @fake("knn_prior_rows")
+    def _(coords, m, rows):
+        return coords.new_empty((rows.shape[0], m), dtype=torch.int32)
+
+    @fake("knn_query")
+    def _(ref, query, k):
+        return query.new_empty((query.shape[0], k), dtype=torch.int32)
+
+    @fake("bf_sweep")
+    def _(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None):
         rows, m = nbr.shape
-        B = coords.new_empty((0, m))
-        F = coords.new_empty((0,))
-    return B, F, partials
+        if want_bf:
+            return coords.new_empty((rows, m)), coords.new_empty((rows,)), coords.new_empty((4,))
+        return coords.new_empty((0, m)), coords.new_empty((0,)), coords.new_empty((4,))
 
+    @fake("bf_sweep_out")
+    def _(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials, workspace, algo):
+        return None
 
-@bf_sweep.register_fake
-def _(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo):
-    rows, m = nbr.shape
-    if want_bf:
-        return coords.new_empty((rows, m)), coords.new_empty((rows,)), coords.new_empty((4,))
-    return coords.new_empty((0, m)), coords.new_empty((0,)), coords.new_empty((4,))
+    @fake("bf_cross")
+    def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo):
+        rows, m = nbr.shape
+        return query.new_empty((rows, m)), query.new_empty((rows,)), query.new_empty((rows,))
 
+    @fake("row_order")
+    def _(coords, i0, rows, nbr):
+        srt = torch.empty_like(nbr) if nbr is not None else coords.new_empty((0, 0), dtype=torch.int32)
+        return coords.new_empty((rows,), dtype=torch.int32), srt
 
-@torch.library.custom_op("nngp::knn_prior", mutates_args=(), device_types="cuda")
-def knn_prior(coords: torch.Tensor, m: int, q0: int, q1: int) -> torch.Tensor:
-    return _lib.knn_prior(coords, m, q0, q1)
-
-
-@knn_prior.register_fake
-def _(coords, m, q0, q1):
-    return coords.new_empty((q1 - q0, m), dtype=torch.int32)
-
-
-@torch.library.custom_op("nngp::knn_query", mutates_args=(), device_types="cuda")
-def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
-    return _lib.knn_query(ref, query, k)
-
-
-@knn_query.register_fake
-def _(ref, query, k):
-    return query.new_empty((query.shape[0], k), dtype=torch.int32)
-
-
-@torch.library.custom_op("nngp::bf_cross", mutates_args=(), device_types="cuda")
-def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: int, sigma2: float, phi: float,
-             tau2: float, ref_values: Optional[torch.Tensor], algo: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """B_t, F_t against the reference set and the kriging mean B_t v_N(t) (zeros without ref_values)."""
-    rows = nbr.shape[0]
-    R = torch.empty((rows,), dtype=torch.float64, device=query.device) if ref_values is not None else None
-    B, F, _ = _lib.bf_cross(ref, query, nbr, _KINDS[kind], sigma2, phi, tau2, ref_values=ref_values,
-                            algo=_ALGOS[algo], R=R)
-    mean = -R if R is not None else torch.zeros((rows,), dtype=torch.float64, device=query.device)
-    return B, F, mean
-
-
-@bf_cross.register_fake
-def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo):
-    rows, m = nbr.shape
-    return query.new_empty((rows, m)), query.new_empty((rows,)), query.new_empty((rows,))
+    @fake("combine_partials_out")
+    def _(gathered, out):
+        return None
 
 
 def kind_code(kind: str) -> int:
@@ -88,6 +102,16 @@ def kind_code(kind: str) -> int:
 
 def algo_code(algo: str) -> int:
     try:
-        return _ALGOS.index(algo)
-    except ValueError:
-        raise ValueError(f"unknown algo {algo!r}; expected one of {_ALGOS}") from None
+        return _ALGOS[algo]
+    except KeyError:
+        raise ValueError(f"unknown algo {algo!r}; expected one of {tuple(_ALGOS)}") from None
+
+
+def bf_sweep_out(coords, nbr, order, i0, kind: str, theta, values, B, F, R, partials, workspace,
+                 algo: str = "auto") -> None:
+    """The fused sweep into caller-owned buffers through ``torch.ops.nngp.bf_sweep_out``
+    (stream-ordered on torch's current stream, no host synchronisation)."""
+    load()
+    torch.ops.nngp.bf_sweep_out(coords, nbr, order, int(i0), kind_code(kind), float(theta[0]), float(theta[1]),
+                                float(theta[2]), values, B, F, R, partials, workspace, algo_code(algo))
+

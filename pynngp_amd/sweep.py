@@ -11,7 +11,8 @@ so the result is bit-identical on every rank and run to run.
 
 The per-shard compute and neighbour build are injectable so the distributed
 combination logic is testable on CPU with the oracle (tests/test_distributed.py);
-the default compute is the HIP kernel through ``_lib``.
+the default compute is the HIP kernel through the native operator
+``torch.ops.nngp.bf_sweep_out`` (pynngp_amd/ops.py, libnngp_torch_ops.so).
 """
 from __future__ import annotations
 
@@ -21,7 +22,7 @@ from typing import Callable, Optional
 import torch
 import torch.distributed as dist
 
-from . import _lib
+from . import _lib, ops
 from .nngp import Covariance, LOG_2PI, _raise_on_bad
 
 
@@ -40,7 +41,9 @@ def combine_partials(local: torch.Tensor, world: int, group=None) -> torch.Tenso
     gathered = torch.empty((world, 4), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(gathered, local.reshape(1, 4), group=group)
     if gathered.device.type == "cuda":
-        return _lib.combine_partials(gathered)  # one tiny HIP kernel, rank order
+        out = torch.empty(4, dtype=local.dtype, device=local.device)
+        torch.ops.nngp.combine_partials_out(gathered, out)  # one tiny HIP kernel, rank order
+        return out
     # CPU (gloo) path: the same fold on the host, for the multi-process tests
     return combine_partials_host(gathered)
 
@@ -107,7 +110,9 @@ class ShardedLogLik:
             if compute is None and spatial_order and self.hi > self.lo:
                 self.order, self._nbr_sweep = _lib.row_order(coords, self.lo, self.hi - self.lo, self.nbr)
         if compute is None:
-            self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device)
+            ops.load()  # sweeps go through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
+            self._algo_code = ops.algo_code(algo)
+            self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device, dim=coords.shape[1])
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
             self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
             self._F = torch.empty((self.hi - self.lo,), dtype=torch.float64, device=coords.device)
@@ -125,10 +130,11 @@ class ShardedLogLik:
             p = self._compute(self, cov, values, want_bf)
             return p if out is None else out.copy_(p)
         B, F = (self._B, self._F) if want_bf else (None, None)
-        _, _, p = _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, *cov.theta, values=values,
-                                want_bf=want_bf, algo=self.algo, B=B, F=F,
-                                partials=self._partials if out is None else out, workspace=self._ws,
-                                order=self.order)
+        p = self._partials if out is None else out
+        s2, phi, tau2 = cov.theta
+        torch.ops.nngp.bf_sweep_out(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
+                                    float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws,
+                                    self._algo_code)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
@@ -216,7 +222,7 @@ class PipelinedCombine:
             return
         with torch.cuda.stream(self.side):
             work.wait()  # the side stream waits for the collective, the compute stream does not
-            _lib.combine_partials(self.gathered[k], out=self.results[k])
+            torch.ops.nngp.combine_partials_out(self.gathered[k], self.results[k])
 
     def finish(self) -> torch.Tensor:
         if self.world == 1:

@@ -46,18 +46,22 @@ def test_version_and_loglik_helper(lib):
 
 
 def test_workspace_sizes(lib):
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0) >= 4 * 8 * (1_000_000 // 256)
-    assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0) == 0
-    assert lib.nngp_bf_sweep_workspace_bytes(0, 15, 0) == 0
-    assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0) > 0
+    # (n_rows, m, kind, dim, algo): the persistent pair kernel keeps <= 512 records, the lane kernel n / 256
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 0) == 4 * 8 * 512
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 0, 2, 0) >= 4 * 8 * (1_000_000 // 256)
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 3, 2, 0) == 4 * 8 * 512  # gaussian: pair kernel
+    assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0, 2, 0) == 0
+    assert lib.nngp_bf_sweep_workspace_bytes(0, 15, 0, 2, 0) == 0
+    assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0, 3, 0) > 0
 
 
 def _sweep(lib, **kw):
-    a = dict(coords=1, n_points=10, nbr=1, n_rows=10, m=15, i0=0, kind=0, sigma2=1.0, phi=1.0, tau2=0.0,
+    a = dict(coords=1, n_points=10, dim=2, nbr=1, n_rows=10, m=15, i0=0, kind=0, sigma2=1.0, phi=1.0, tau2=0.0,
              values=None, B=None, F=None, partials=1, workspace=256, workspace_bytes=1 << 20, algo=0, stream=None)
     a.update(kw)
     P = lambda v: None if v is None else ctypes.c_void_p(v)  # noqa: E731
-    return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], P(a["nbr"]), None, a["n_rows"], a["m"], a["i0"], a["kind"],
+    return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], a["dim"], P(a["nbr"]), None, a["n_rows"], a["m"], a["i0"],
+                             a["kind"],
                              a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]), P(a.get("R")),
                              P(a["partials"]), P(a["workspace"]), a["workspace_bytes"], a["algo"], P(a["stream"]))
 
@@ -69,6 +73,12 @@ def _sweep(lib, **kw):
     (dict(n_rows=11), -1, "outside"),
     (dict(i0=5), -1, "outside"),
     (dict(kind=7), -1, "unknown kind"),
+    (dict(kind=-1), -1, "unknown kind"),
+    (dict(dim=0), -4, "dim=0"),
+    (dict(dim=4), -4, "dim=4"),
+    (dict(algo=1, m=8, kind=2), -4, "2-D exponential and Matern-3/2 only"),
+    (dict(algo=3, m=15, dim=3), -4, "2-D exponential and Matern-3/2 only"),
+    (dict(algo=5, m=25), -4, "blocked pair kernel"),
     (dict(sigma2=0.0), -1, "theta"),
     (dict(phi=float("nan")), -1, "theta"),
     (dict(tau2=-1.0), -1, "theta"),
@@ -87,21 +97,26 @@ def test_bf_sweep_rejects(lib, kw, code, msg):
 
 def test_row_order_rejects(lib):
     P = ctypes.c_void_p
-    assert lib.nngp_row_order(None, 10, None, 0, 0, 10, P(1), None, P(256), 1 << 20, None) == -1
-    assert lib.nngp_row_order(P(1), 10, None, 0, 5, 6, P(1), None, P(256), 1 << 20, None) == -1
-    assert lib.nngp_row_order(P(1), 10, None, 0, 0, 10, None, None, P(256), 1 << 20, None) == -1
-    assert lib.nngp_row_order(P(1), 10, None, 5, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -1
-    assert lib.nngp_row_order(P(1), 10, P(1), 70, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_row_order(None, 10, 2, None, 0, 0, 10, P(1), None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, 2, None, 0, 5, 6, P(1), None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, 2, None, 0, 0, 10, None, None, P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, 2, None, 5, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_row_order(P(1), 10, 2, P(1), 70, 0, 10, P(1), P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_row_order(P(1), 10, 4, None, 0, 0, 10, P(1), None, P(256), 1 << 20, None) == -4
 
 
 def test_knn_rejects(lib):
     P = ctypes.c_void_p
-    assert lib.nngp_knn_prior(None, 10, 5, 0, 10, P(1), P(256), 1 << 20, None) == -1
-    assert lib.nngp_knn_prior(P(1), 10, 65, 0, 10, P(1), P(256), 1 << 20, None) == -4
-    assert lib.nngp_knn_prior(P(1), 10, 5, 3, 2, P(1), P(256), 1 << 20, None) == -1
-    assert lib.nngp_knn_prior(P(1), 0, 5, 0, 0, P(1), P(256), 1 << 20, None) == -1
-    assert lib.nngp_knn_query(P(1), 10, None, 5, 3, P(1), P(256), 1 << 20, None) == -1
-    assert lib.nngp_knn_query(P(1), 10, P(1), 5, 99, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_prior(None, 10, 2, 5, 0, 10, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_prior(P(1), 10, 2, 65, 0, 10, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_prior(P(1), 10, 2, 5, 3, 2, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_prior(P(1), 0, 2, 5, 0, 0, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_prior(P(1), 10, 0, 5, 0, 10, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_prior(P(1), 10, 4, 5, 0, 10, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_query(P(1), 10, 2, None, 5, 3, P(1), P(256), 1 << 20, None) == -1
+    assert lib.nngp_knn_query(P(1), 10, 2, P(1), 5, 99, P(1), P(256), 1 << 20, None) == -4
+    assert lib.nngp_knn_workspace_bytes(1000, 3, 15) > lib.nngp_knn_workspace_bytes(1000, 1, 15) > 0
+    assert lib.nngp_knn_workspace_bytes(1000, 4, 15) == 0
 
 
 def test_no_cpu_fallback():

@@ -141,7 +141,9 @@ def test_nngp_random_reftype(dev, c_oracle):
 
 
 def test_bf_cross_op_registered(dev, c_oracle):
-    from pynngp_amd import ops
+    from pynngp_amd import load_ops
+
+    ops = load_ops()
 
     ref, query, vr, _ = _sets(500, 200, 1)
     g = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731

@@ -113,11 +113,15 @@ def test_knn_fma_sensitive_ties(lib, dev, c_oracle):
 
 
 def test_knn_ops_registered(dev):
-    from pynngp_amd import ops
+    from pynngp_amd import load_ops
+
+    ops = load_ops()
 
     coords = torch.rand((500, 2), dtype=torch.float64, device=dev)
     a = torch.ops.nngp.knn_prior(coords, 7, 0, 500)
-    b = ops.knn_prior(coords, 7, 0, 500)
+    from pynngp_amd import _lib
+
+    b = _lib.knn_prior(coords, 7, 0, 500)
     assert torch.equal(a, b) and a.dtype == torch.int32
     with pytest.raises(Exception):
         torch.ops.nngp.knn_prior(coords.cpu(), 7, 0, 500)

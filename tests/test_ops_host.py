@@ -1,0 +1,47 @@
+"""The native operator library loads without a GPU and registers every torch.ops.nngp
+operator with its schema; CPU tensors are refused (there is no CPU implementation)."""
+import pytest
+import torch
+
+OPS = ["knn_prior", "knn_prior_rows", "knn_query", "bf_sweep", "bf_sweep_out", "bf_cross", "row_order",
+       "combine_partials_out"]
+
+
+def test_op_library_registers_all_ops():
+    from pynngp_amd import load_ops
+
+    ops = load_ops()
+    for name in OPS:
+        assert hasattr(torch.ops.nngp, name), name
+    schema = str(torch.ops.nngp.bf_sweep_out.default._schema)
+    assert "Tensor(a!)? B" in schema and "Tensor(d!) partials" in schema
+    assert ops.kind_code("gaussian") == 3 and ops.algo_code("pairb") >= 0
+    with pytest.raises(ValueError):
+        ops.kind_code("cauchy")
+
+
+def test_ops_refuse_cpu_tensors():
+    from pynngp_amd import load_ops
+
+    load_ops()
+    c = torch.rand((50, 2), dtype=torch.float64)
+    with pytest.raises(NotImplementedError):
+        torch.ops.nngp.knn_prior(c, 4, 0, 50)
+    with pytest.raises(NotImplementedError):
+        torch.ops.nngp.bf_sweep(c, torch.zeros((50, 4), dtype=torch.int32), 0, 0, 1.0, 5.0, 0.0, None, False, 0)
+
+
+def test_fake_kernels_trace_shapes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    from pynngp_amd import load_ops
+
+    load_ops()
+    with FakeTensorMode():
+        c = torch.empty((64, 3), dtype=torch.float64)
+        nb = torch.ops.nngp.knn_prior(c, 6, 0, 64)
+        B, F, p = torch.ops.nngp.bf_sweep(c, nb, 0, 1, 1.0, 5.0, 0.0, None, True, 0)
+        o, s = torch.ops.nngp.row_order(c, 0, 64, nb)
+    assert tuple(nb.shape) == (64, 6) and nb.dtype == torch.int32
+    assert tuple(B.shape) == (64, 6) and tuple(F.shape) == (64,) and tuple(p.shape) == (4,)
+    assert tuple(o.shape) == (64,) and tuple(s.shape) == (64, 6)

@@ -11,6 +11,7 @@
 #   trace[:args]     rocprofv3 --kernel-trace --stats over bench.py <args>
 #   fetch[:args] / write[:args]   FETCH_SIZE / WRITE_SIZE passes
 #   py:<file>        python <file> (a tools/ script)
+#   env:<K=V>        export K=V for the following steps (A/B knobs such as NNGP_PAIRB_BLOCKS)
 # Every GPU step has its own time limit; the first failing step ends the session.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -58,6 +59,8 @@ for step in "$@"; do
     write)
       timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write_$n -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 $arg > $out/write_$n.json 2> $out/write_$n.err || exit 1
       python3 tools/pmc_summary.py $out/write_$n ;;
+    env)
+      export "$arg"; echo "export $arg" ;;
     counters)
       timeout -s KILL 60 rocprofv3 -L > $out/counters.txt 2>&1 || true
       wc -l $out/counters.txt ;;
