@@ -62,3 +62,32 @@ def moral_edges(nbr):
 
 def coloring_is_valid(nbr, colors):
     return all(colors[a] != colors[b] for a, b in moral_edges(nbr))
+
+
+# ---------------------------------------------------------------- S != T (reference set)
+def reference_dag(s, t_out, m):
+    """The DAG of the reference-set model (nngp.py:42-71; TEST INFRASTRUCTURE ONLY): nodes
+    [S; T_out]; a reference point's parents are the min(i, m) nearest earlier points of S
+    (``_make_s_neighbor_sets``), a data location outside S is a leaf whose parents are its
+    m nearest points of S (``_make_t_neighbor_sets``, kdtree.query(t, m) over all of S).
+    Returns (coords (n_s + n_out, d), nbr (n_s + n_out, m) int32, -1 padded)."""
+    from oracle import nngp_oracle as O
+
+    s = np.asarray(s, dtype=np.float64)
+    t_out = np.asarray(t_out, dtype=np.float64)
+    nbr_s = O.c_knn_prior(s, m)
+    k = min(m, len(s))
+    nbr_t = np.full((len(t_out), m), -1, dtype=np.int32)
+    if len(t_out):
+        nbr_t[:, :k] = O.knn_all(t_out, s, k)
+    return np.concatenate([s, t_out]), np.concatenate([nbr_s, nbr_t]).astype(np.int32)
+
+
+def dag_posterior(nbr, B, F, sigma2, tau2, h, yres):
+    """Exact Gaussian full posterior of w over the DAG's nodes: precision
+    P = (I - B)^T (sigma2 F)^-1 (I - B) + diag(h / tau2), linear term b = h yres / tau2
+    (h = 0 at nodes without an observation).  Returns (P, b, mean, cov)."""
+    P = precision(nbr, B, F * sigma2) + np.diag(np.asarray(h) / tau2)
+    b = np.asarray(h) * np.asarray(yres) / tau2
+    cov = np.linalg.inv(P)
+    return P, b, cov @ b, cov

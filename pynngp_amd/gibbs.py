@@ -43,6 +43,32 @@ from . import _lib, ops
 from .nngp import NNGPNumericalError, _default_device
 
 
+def _as_points(a, what):
+    h = np.ascontiguousarray(a, dtype=np.float64)
+    if h.ndim == 1:
+        h = h[:, None]
+    if h.ndim != 2 or not 1 <= h.shape[1] <= _lib.MAX_DIM or h.shape[0] < 1:
+        raise ValueError(f"{what} must be (N >= 1, d) with 1 <= d <= {_lib.MAX_DIM}, got {h.shape}")
+    if not np.all(np.isfinite(h)):
+        raise ValueError(f"{what} must be finite (NaN / inf would silently decouple locations)")
+    return h
+
+
+def colour_dag(nbr, off, rev_j, n_s):
+    """Colour the moral graph of the DAG whose first ``n_s`` nodes are the reference points
+    and the rest leaves (host arrays in model order: nbr (n, m), reverse CSR off / rev_j).
+    Greedy over the reference points (leaves come later, so only their co-parent edges
+    constrain S); the leaves, never parents and so pairwise non-adjacent, share one last
+    colour.  Returns (colors, n_colors, n_colors_ref)."""
+    colors, n_colors = _lib.color_moral_graph(nbr, off, rev_j)
+    n = colors.shape[0]
+    if n > n_s:
+        n_colors = int(colors[:n_s].max()) + 1 if n_s else 0
+        colors[n_s:] = n_colors
+        return colors, n_colors + 1, n_colors
+    return colors, n_colors, n_colors
+
+
 @dataclasses.dataclass
 class Priors:
     sigma2_ig: tuple = (2.0, 1.0)  # inverse-gamma (shape, scale)
@@ -51,11 +77,24 @@ class Priors:
 
 
 class SeqNNGP:
-    """NNGP response-model Gibbs sampler (see module docstring)."""
+    """NNGP response-model Gibbs sampler (see module docstring).
+
+    ``ref=None``: the latent field lives on the data locations (S = T).  With ``ref`` (an
+    (n_S, d) reference set S, e.g. the reference's ('random', nRef, bounds) or ('subset',
+    nRef) sets) the field lives on S and on the data locations outside S, as the
+    reference's ``wt`` / ``ws`` (nngp.py:42-47) linked by ``Nt`` (nngp.py:64-71): the
+    DAG's nodes are S (parents: the m nearest earlier points of S) followed by every data
+    location not in S as a leaf (parents: its m nearest points of S).  A data location
+    that coincides with a point of S carries its observation on that node.  ``y`` may hold
+    NaN for unobserved locations: they enter no likelihood term and get posterior-
+    predictive draws (``update_y_unobserved``), as do the reference points without data
+    when their covariates are known (``X`` None = intercept, or ``X_ref``).
+    """
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
-                 seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False):
+                 seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
+                 ref=None, X_ref=None):
         self.device = _default_device(device)
         dev = self.device
         self.kind = kind
@@ -65,68 +104,165 @@ class SeqNNGP:
         self.seed = int(seed)
         self.rng = np.random.default_rng(seed)
         to = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
-        coords0 = to(coords)
-        if not bool(torch.isfinite(coords0).all()):
-            raise ValueError("coordinates must be finite (NaN / inf would silently decouple locations)")
-        y0 = to(y)
-        n = y0.shape[0]
-        self.n = n
-        X0 = to(np.ones((n, 1)) if X is None else np.asarray(X, dtype=np.float64).reshape(n, -1))
-        self.p = X0.shape[1]
-        Xh = X0.cpu().numpy()
+        t_host = _as_points(coords, "coordinates")
+        y_host = np.asarray(y, dtype=np.float64).reshape(-1)
+        n_t = t_host.shape[0]
+        if y_host.shape != (n_t,):
+            raise ValueError(f"y must hold one response per location ({n_t}), got {y_host.shape}")
+        if np.any(np.isinf(y_host)):
+            raise ValueError("y must be finite or NaN (NaN = unobserved)")
+        observed = np.isfinite(y_host)
+        X_t = np.ones((n_t, 1)) if X is None else np.asarray(X, dtype=np.float64).reshape(n_t, -1)
+        if not np.all(np.isfinite(X_t)):
+            raise ValueError("X must be finite")
+        self.p = X_t.shape[1]
         self.fix_tau2 = bool(fix_tau2)
         if eps is None:
-            hh = np.ones(n)
-            h0 = None
+            h_t = np.ones(n_t)
         else:
             ev = np.asarray(eps, dtype=np.float64).reshape(-1)
-            if ev.shape != (n,) or not np.all(np.isfinite(ev)) or not np.all(ev > 0):
-                raise ValueError(f"eps must hold {n} positive finite measurement sigmas")
-            hh = 1.0 / ev ** 2
-            h0 = to(hh)
-        self._XtX_inv = np.linalg.inv((Xh * hh[:, None]).T @ Xh)
-        self._XtX_inv_chol = np.linalg.cholesky(self._XtX_inv)
+            if ev.shape != (n_t,) or not np.all(np.isfinite(ev)) or not np.all(ev > 0):
+                raise ValueError(f"eps must hold {n_t} positive finite measurement sigmas")
+            h_t = 1.0 / ev ** 2
+        self.n_t = n_t
 
-        # neighbour sets in the model's (input) order; then every per-location array is
-        # relabelled into Z-order STORAGE (slot p holds location perm[p]), so that a
-        # location's parents and children sit near it in memory: the gathers and
-        # scatters of the sweeps share cache lines.  The model is label-invariant
-        # (neighbour sets, colouring, conditionals); w is mapped back on output.
-        nbr0 = _lib.knn_prior(coords0, self.m)
+        # ---- the DAG's nodes: S (model rows 0..n_s-1), then the data locations outside S
+        t_dev = to(t_host)
+        if ref is None:
+            s_dev, n_s = t_dev, n_t
+            node_of_t = np.arange(n_t)
+            nbr0 = _lib.knn_prior(t_dev, self.m)
+            coords0 = t_dev
+            x_s_known = True
+        else:
+            s_host = _as_points(ref, "reference set")
+            if s_host.shape[1] != t_host.shape[1]:
+                raise ValueError(f"reference set has dimension {s_host.shape[1]}, locations {t_host.shape[1]}")
+            s_dev, n_s = to(s_host), s_host.shape[0]
+            nbr_s = _lib.knn_prior(s_dev, self.m)
+            if n_s > 1:  # a repeated reference point makes C_N singular
+                j1 = nbr_s[1:, 0].long()
+                dup = torch.nonzero((s_dev[1:] == s_dev[j1]).all(dim=1)).flatten()
+                if dup.numel() > 0:
+                    k = int(dup[0]) + 1
+                    raise ValueError(f"reference set point {k} repeats point {int(j1[k - 1])} (C_N would be "
+                                     "singular; e.g. ('subset', nRef) draws with replacement)")
+            # data locations that coincide with a reference point carry their data on that node
+            j0 = _lib.knn_query(s_dev, t_dev, 1)[:, 0].long()
+            hit = (t_dev == s_dev[j0]).all(dim=1).cpu().numpy()
+            j0h = j0.cpu().numpy()
+            if np.unique(j0h[hit]).size != int(hit.sum()):
+                raise ValueError("two data locations coincide with the same reference point")
+            out_idx = np.nonzero(~hit)[0]
+            node_of_t = np.where(hit, j0h, 0)
+            node_of_t[out_idx] = n_s + np.arange(out_idx.size)
+            k = min(self.m, n_s)
+            t_out = t_dev[torch.from_numpy(out_idx).to(dev)]
+            nbr_t = _lib.knn_query(s_dev, t_out, k) if out_idx.size else torch.empty((0, k), dtype=torch.int32,
+                                                                                       device=dev)
+            if k < self.m:
+                nbr_t = torch.cat([nbr_t, torch.full((nbr_t.shape[0], self.m - k), -1, dtype=torch.int32,
+                                                     device=dev)], dim=1)
+            nbr0 = torch.cat([nbr_s, nbr_t]).contiguous()
+            coords0 = torch.cat([s_dev, t_out]).contiguous()
+            x_s_known = X is None or X_ref is not None
+        n = coords0.shape[0]
+        self.n, self.n_s = n, n_s
+        self.node_of_t = torch.from_numpy(node_of_t.astype(np.int64)).to(dev)
+
+        # per-node data: observation weight h (0 = no observation), y, X
+        h_n = np.zeros(n)
+        y_n = np.zeros(n)
+        X_n = np.zeros((n, self.p))
+        h_n[node_of_t[observed]] = h_t[observed]
+        y_n[node_of_t[observed]] = y_host[observed]
+        X_n[node_of_t] = X_t
+        self.n_obs = int(observed.sum())
+        if self.n_obs == 0:
+            raise ValueError("no observed responses (y is all NaN)")
+        # unobserved responses drawn each iteration: data locations with NaN y, then (S != T)
+        # the reference points that carry no data, when their covariates are known
+        un_t = np.nonzero(~observed)[0]
+        un_nodes = node_of_t[un_t]
+        un_sd = 1.0 / np.sqrt(h_t[un_t])
+        x_un = X_t[un_t]
+        self.unobserved_t = un_t  # data-location indices of the first len(un_t) draws
+        self.unobserved_ref = np.zeros(0, dtype=np.int64)
+        if ref is not None and x_s_known:
+            free = np.ones(n_s, dtype=bool)
+            free[node_of_t[node_of_t < n_s]] = False
+            self.unobserved_ref = np.nonzero(free)[0]
+            if X is None:
+                x_ref = np.ones((n_s, 1))
+            else:
+                x_ref = np.asarray(X_ref, dtype=np.float64).reshape(n_s, -1)
+                if x_ref.shape[1] != self.p or not np.all(np.isfinite(x_ref)):
+                    raise ValueError(f"X_ref must be finite ({n_s}, {self.p})")
+                X_n[:n_s][free] = x_ref[free]
+            un_nodes = np.concatenate([un_nodes, self.unobserved_ref])
+            un_sd = np.concatenate([un_sd, np.ones(self.unobserved_ref.size)])
+            x_un = np.concatenate([x_un, x_ref[self.unobserved_ref]])
+        XtX = (X_n * h_n[:, None]).T @ X_n
+        if np.linalg.matrix_rank(XtX) < self.p:
+            raise ValueError("X' H X is singular over the observed locations")
+        self._XtX_inv = np.linalg.inv(XtX)
+        self._XtX_inv_chol = np.linalg.cholesky(self._XtX_inv)
+        homoscedastic = eps is None and self.n_obs == n  # every node observed with weight 1
+
+        # neighbour sets in the model's (node) order; then every per-node array is relabelled
+        # into Z-order STORAGE (slot p holds node perm[p]), so that a node's parents and
+        # children sit near it in memory: the gathers and scatters of the sweeps share cache
+        # lines.  The model is label-invariant (neighbour sets, colouring, conditionals); w is
+        # mapped back on output.
         perm, _ = _lib.row_order(coords0)
         self.perm = perm.long()
         self.pos = torch.empty_like(self.perm)
         self.pos[self.perm] = torch.arange(n, device=dev)
         self.coords = coords0[self.perm].contiguous()
-        self.y = y0[self.perm].contiguous()
-        self.X = X0[self.perm].contiguous()
-        self.noise_w = None if h0 is None else h0[self.perm].contiguous()  # h_i = 1 / eps_i^2, storage order
+        self.y = to(y_n)[self.perm].contiguous()
+        self.X = to(X_n)[self.perm].contiguous()
+        self.noise_w = None if homoscedastic else to(h_n)[self.perm].contiguous()  # h_i, storage order
         nb = nbr0[self.perm].long()
         self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
         self.off, self.rev_j, self.rev_k = _lib.reverse_neighbors(self.nbr)
-        # greedy colouring visits the locations in INPUT order (spatially scattered for
-        # generation-order data: ~2x fewer colours than a scan in the spatial storage
-        # order); the moral graph is label-invariant, so the colours carry over
+        # greedy colouring visits the nodes in MODEL order (S first, spatially scattered for
+        # generation-order data: ~2x fewer colours than a scan in the spatial storage order);
+        # the moral graph is label-invariant, so the colours carry over.  The leaves (data
+        # locations outside S) are never parents, hence pairwise non-adjacent: they form one
+        # last colour of their own, swept by update_wt.
         off0, rev_j0, _ = _lib.reverse_neighbors(nbr0)
-        colors0, self.n_colors = _lib.color_moral_graph(nbr0.cpu().numpy(), off0.cpu().numpy(),
-                                                        rev_j0.cpu().numpy())
+        colors0, self.n_colors, self.n_colors_ref = colour_dag(nbr0.cpu().numpy(), off0.cpu().numpy(),
+                                                               rev_j0.cpu().numpy(), n_s)
         colors = colors0[self.perm.cpu().numpy()]
         self.colors = colors
         # members grouped by colour, storage (= Z) order inside a colour
         self.members = torch.from_numpy(np.argsort(colors, kind="stable").astype(np.int32)).to(dev)
         self.color_off = np.concatenate([[0], np.cumsum(np.bincount(colors, minlength=self.n_colors))]).astype(
             np.int32)
+        pos_h = self.pos.cpu().numpy()
+        self._un_nodes = torch.from_numpy(pos_h[un_nodes].astype(np.int64)).to(dev)  # storage slots
+        self._un_sd = to(un_sd)
+        self._un_X = to(x_un.reshape(-1, self.p))
+        self.y_unobserved = torch.zeros(len(un_nodes), dtype=torch.float64, device=dev)
+        self._zy = torch.empty(len(un_nodes), dtype=torch.float64, device=dev)
 
         # state
-        # (weighted) least squares start; X, y and the weights in the caller's order
-        self.beta = self._XtX_inv @ ((Xh * hh[:, None]).T @ y0.cpu().numpy())
+        # (weighted) least squares start over the observed locations
+        self.beta = self._XtX_inv @ ((X_n * h_n[:, None]).T @ y_n)
         self.sigma2 = float(sigma2)
         self.tau2 = float(tau2)
         lo, hi = self.priors.phi_unif
         self.phi = float(phi) if phi is not None else math.sqrt(lo * hi)
         self.phi_tuning = float(phi_tuning)
         self.yres = self._residual_y(self.beta)
-        self.w = to(np.zeros(n) if w_init is None else w_init)[self.perm].contiguous()  # storage order
+        if w_init is None:
+            w0 = np.zeros(n)
+        else:
+            w0 = np.asarray(w_init, dtype=np.float64).reshape(-1)
+            if w0.shape != (n,):
+                raise ValueError(f"w_init must hold one value per node ({n}: reference points, then the data "
+                                 "locations outside the reference set)")
+        self.w = to(w0)[self.perm].contiguous()  # storage order
         self.iteration = 0
         self.n_accept = 0
         self.n_notpd_reject = 0  # phi proposals rejected because their factor was not positive definite
@@ -174,59 +310,139 @@ class SeqNNGP:
         """log p(w | sigma2, phi) from the sweep's partials of the unit-variance field."""
         return -0.5 * (self.n * math.log(2 * math.pi * sigma2) + sum_logF + quad / sigma2)
 
-    def step(self):
-        n = self.n
-        # 1. phi | w, sigma2: log-normal random walk MH
+    def update_phi(self):
+        """phi | w, sigma2: log-normal random-walk Metropolis-Hastings; the proposal's log
+        density of w is one fused B/F sweep over every node of the DAG."""
         phi_p = self.phi * math.exp(self.phi_tuning * self.rng.standard_normal())
         lo, hi = self.priors.phi_unif
         u = self.rng.random()
-        if lo <= phi_p <= hi:
-            self._sweep_into(phi_p, self._B2, self._Ft2, self._r2)
-            ph = self._part.cpu().numpy()
-        if lo <= phi_p <= hi and ph[2] >= 0:
+        if not lo <= phi_p <= hi:
+            return
+        self._sweep_into(phi_p, self._B2, self._Ft2, self._r2)
+        ph = self._part.cpu().numpy()
+        if ph[2] >= 0:
             # the proposal's latent factor is not positive definite (near-duplicate locations
             # with tau2 = 0 and a large phi): zero density there, so the move is rejected
             self.n_notpd_reject += 1
-        elif lo <= phi_p <= hi:
-            l_new = self.loglik_w(ph[0], ph[1], self.sigma2)
-            l_old = self.loglik_w(self.sum_logF, self.quad, self.sigma2)
-            if math.log(u) < l_new - l_old + math.log(phi_p) - math.log(self.phi):
-                self.phi = phi_p
-                self.B, self._B2 = self._B2, self.B
-                self.Ft, self._Ft2 = self._Ft2, self.Ft
-                self.r, self._r2 = self._r2, self.r
-                self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
-                self.sum_logF, self.quad = float(ph[0]), float(ph[1])
-                self.n_accept += 1
-        # 2. sigma2 | w, phi
+            return
+        l_new = self.loglik_w(ph[0], ph[1], self.sigma2)
+        l_old = self.loglik_w(self.sum_logF, self.quad, self.sigma2)
+        if math.log(u) < l_new - l_old + math.log(phi_p) - math.log(self.phi):
+            self.phi = phi_p
+            self.B, self._B2 = self._B2, self.B
+            self.Ft, self._Ft2 = self._Ft2, self.Ft
+            self.r, self._r2 = self._r2, self.r
+            self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
+            self.sum_logF, self.quad = float(ph[0]), float(ph[1])
+            self.n_accept += 1
+
+    def _sweep_colours(self, c0, c1):
+        if c1 > c0:
+            _lib.gibbs_w_sweep(self.members, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2, self.tau2,
+                               self.yres, self.w, self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z,
+                               noise_w=self.noise_w)
+
+    def update_wt(self):
+        """w_t | w_S, y_t for the data locations outside S (nngp.py:99): the leaves of the DAG,
+        conditionally independent given w_S, all drawn in one parallel colour step
+        (N(B_t w_N(t), sigma2 F_t) prior times the observation's likelihood).  With S = T
+        there are no leaves: w_t is w_s."""
+        self._sweep_colours(self.n_colors_ref, self.n_colors)
+
+    def update_ws(self):
+        """w_s | rest for the reference points (nngp.py:100): colour-ordered parallel sweep of
+        the full conditionals, children on S and leaf children at T included."""
+        self._sweep_colours(0, self.n_colors_ref)
+
+    def update_y_unobserved(self):
+        """Posterior-predictive draws y* = x beta + w + N(0, tau2 / h) at the unobserved
+        locations (nngp.py:101): data locations with NaN y and, for S != T, the reference
+        points without data whose covariates are known (``y_unobserved``, in the order
+        ``unobserved_t`` then ``unobserved_ref``)."""
+        k = self._un_nodes.numel()
+        if k == 0:
+            return
+        # an independent Philox stream: the sweep counter's top bit set
+        _lib.gibbs_normals(self._zy, self.seed, self.iteration | (1 << 63))
+        xb = self._un_X @ torch.as_tensor(self.beta, dtype=torch.float64, device=self.device)
+        torch.addcmul(xb + self.w[self._un_nodes], self._un_sd, self._zy, value=math.sqrt(self.tau2),
+                      out=self.y_unobserved)
+
+    def step(self):
+        """One iteration: phi; sigma2; update_wt; update_ws; tau2; beta; update_y_unobserved."""
+        n = self.n
+        self.update_phi()
+        # sigma2 | w, phi
         a, b = self.priors.sigma2_ig
         self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
-        # 3. w | rest (colour sweep, in place on w and r)
-        _lib.gibbs_normals(self._z, self.seed, self.iteration)  # the sweep's normals, one parallel pass
-        _lib.gibbs_w_sweep(self.members, self.color_off, self._prep, self.m, self.sigma2, self.tau2, self.yres, self.w,
-                           self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z, noise_w=self.noise_w)
+        # w | rest (colour steps, in place on w and r; the sweep's normals in one parallel pass)
+        _lib.gibbs_normals(self._z, self.seed, self.iteration)
+        self.update_wt()
+        self.update_ws()
         st = _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats,
                               noise_w=self.noise_w).cpu().numpy()
         self.quad = float(st[0])
-        # 4. tau2 | y, beta, w (weighted residual sum of squares; held fixed on request)
+        # tau2 | y, beta, w (weighted residual sum of squares over the observed; held fixed on request)
         if not self.fix_tau2:
             a, b = self.priors.tau2_ig
-            self.tau2 = self._ig(a + 0.5 * n, b + 0.5 * float(st[1]))
-        # 5. beta | y, w, tau2 (flat prior; weighted least squares)
+            self.tau2 = self._ig(a + 0.5 * self.n_obs, b + 0.5 * float(st[1]))
+        # beta | y, w, tau2 (flat prior; weighted least squares)
         mean = self._XtX_inv @ st[2:]
         self.beta = mean + math.sqrt(self.tau2) * (self._XtX_inv_chol @ self.rng.standard_normal(self.p))
         self.yres = self._residual_y(self.beta)
+        self.update_y_unobserved()
         self.iteration += 1
+
+    def set_w(self, ws=None, wt=None):
+        """Set the latent state: ``ws`` at the reference points (n_S,), ``wt`` at the data
+        locations (n_T,; with S != T it sets the leaves only, the locations on S take ``ws``);
+        the NNGP residuals are recomputed."""
+        to = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64)).to(self.device)  # noqa: E731
+        wn = self.w_nodes.clone()
+        if ws is not None:
+            wn[: self.n_s] = to(ws).reshape(-1)
+        if wt is not None:
+            wt = to(wt).reshape(-1)
+            if wt.shape != (self.n_t,):
+                raise ValueError(f"wt must hold {self.n_t} values")
+            leaf = self.node_of_t >= self.n_s
+            if self.n_s == self.n_t and self.n == self.n_t and not bool(leaf.any()):
+                wn[self.node_of_t] = wt
+            else:
+                wn[self.node_of_t[leaf]] = wt[leaf]
+        if not bool(torch.isfinite(wn).all()):
+            raise ValueError("w must be finite")
+        self.w = wn[self.perm].contiguous()
+        self._sweep_into(self.phi, self.B, self.Ft, self.r)
+        ph = self._part.cpu().numpy()
+        self.sum_logF, self.quad = float(ph[0]), float(ph[1])
+
+    @property
+    def w_nodes(self) -> torch.Tensor:
+        """w in model node order: the reference points, then the data locations outside S."""
+        return self.w[self.pos]
+
+    @property
+    def w_s(self) -> torch.Tensor:
+        """w at the reference points (the reference's ``ws``)."""
+        return self.w[self.pos[: self.n_s]]
+
+    @property
+    def w_t(self) -> torch.Tensor:
+        """w at the data locations (the reference's ``wt``)."""
+        return self.w[self.pos[self.node_of_t]]
 
     @property
     def w_input_order(self) -> torch.Tensor:
-        """Current latent field w in the caller's location order (the state lives in Z-order storage)."""
-        return self.w[self.pos]
+        """Current latent field w at the data locations, in the caller's order (the state lives in
+        Z-order storage); = :attr:`w_t`."""
+        return self.w_t
 
     def sample(self, n_iter: int, burn: int = 0, thin: int = 1, keep_w_mean: bool = False):
         """Run n_iter iterations; return the thinned post-burn-in draws (numpy)."""
         out = {"beta": [], "sigma2": [], "tau2": [], "phi": []}
         w_sum = torch.zeros_like(self.w) if keep_w_mean else None
+        y_sum = torch.zeros_like(self.y_unobserved)
         kept = 0
         for k in range(n_iter):
             self.step()
@@ -237,9 +453,15 @@ class SeqNNGP:
                 out["phi"].append(self.phi)
                 if keep_w_mean:
                     w_sum += self.w
+                y_sum += self.y_unobserved
                 kept += 1
         res = {k: np.asarray(v) for k, v in out.items()}
         res["phi_accept_rate"] = self.n_accept / max(self.iteration, 1)
         if keep_w_mean:
-            res["w_mean"] = (w_sum / max(kept, 1))[self.pos].cpu().numpy()  # input order
+            wm = w_sum / max(kept, 1)
+            res["w_mean"] = wm[self.pos[self.node_of_t]].cpu().numpy()  # data locations, input order
+            if self.n > self.n_t or self.n_s != self.n_t:
+                res["ws_mean"] = wm[self.pos[: self.n_s]].cpu().numpy()  # reference points
+        if self.y_unobserved.numel():
+            res["y_unobserved_mean"] = (y_sum / max(kept, 1)).cpu().numpy()
         return res

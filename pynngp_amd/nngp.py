@@ -390,17 +390,19 @@ class NNGP:
                 "converged": bool(res.success)}
 
     def oneSample(self, seed: int = 0, X=None, **sampler_kw):
-        """One Gibbs iteration (nngp.py:98-101, whose update_wt / update_ws /
-        update_y_unobserved do not exist in the reference) of the response model
-        y = X beta + w + eps on S = T: delegates to :class:`pynngp_amd.SeqNNGP`, created on
-        the first call with w initialised to ``ws`` and (sigma2, phi, tau2) from ``cov``
-        (``X`` defaults to an intercept).  ``eps`` (nngp.py:9, "measurement uncertainties in
-        y"), when it is one positive sigma per location, makes the noise heteroscedastic:
-        variance tau2 eps_i^2 (see SeqNNGP; pass ``fix_tau2=True`` with tau2 = 1 for exactly
-        eps_i^2).  Afterwards ``ws`` and ``wt`` hold the current w.
+        """One Gibbs iteration of the response model y = X beta + w + eps: the reference's
+        ``update_wt`` / ``update_ws`` / ``update_y_unobserved`` (nngp.py:98-101, which do not
+        exist there), delegated to :class:`pynngp_amd.SeqNNGP`, created on the first call
+        with (sigma2, phi, tau2) from ``cov`` and w initialised from ``ws`` (reference
+        points) and ``wt`` (data locations outside S; NaN -> 0).  'S=T': the field lives on
+        the data locations; tuple refTypes: on S, with each data location outside S a leaf
+        linked to its ``Nt`` (nngp.py:64-71).  ``X`` defaults to an intercept (pass
+        ``X_ref`` for the covariates at S to get predictive draws there).  ``eps``
+        (nngp.py:9, "measurement uncertainties in y"), when it is one positive sigma per
+        location, makes the noise heteroscedastic: variance tau2 eps_i^2 (see SeqNNGP;
+        ``fix_tau2=True`` with tau2 = 1 for exactly eps_i^2).  Afterwards ``ws`` / ``wt``
+        hold the current w at S / T and ``y_unobserved`` the current predictive draws.
         Returns the sampler (its ``beta, sigma2, tau2, phi`` are the other draws)."""
-        if not self._same_sets():
-            raise NotImplementedError("oneSample needs refType 'S=T' (w lives on the observed locations)")
         y = np.asarray(self.y, dtype=np.float64)
         if y.ndim != 1:
             raise ValueError("oneSample needs one response per location (1-D y)")
@@ -413,12 +415,17 @@ class NNGP:
                 ev = np.asarray(self.eps, dtype=np.float64)
                 if ev.shape == y.shape and np.all(np.isfinite(ev)) and np.all(ev > 0):
                     sampler_kw["eps"] = ev
-            self._sampler = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi,
-                                    seed=seed, device=self.device, w_init=np.asarray(self.ws, dtype=np.float64),
-                                    **sampler_kw)
+            ref = None if self._same_sets() else self.s
+            smp = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi, seed=seed,
+                          device=self.device, ref=ref, **sampler_kw)
+            ws = np.asarray(self.ws, dtype=np.float64)
+            smp.set_w(ws=np.where(np.isfinite(ws), ws, 0.0),
+                      wt=None if ref is None else np.where(np.isfinite(self.wt), self.wt, 0.0))
+            self._sampler = smp
         self._sampler.step()
-        self.ws = self._sampler.w_input_order.cpu().numpy()
-        self.wt = self.ws
+        self.ws = self._sampler.w_s.cpu().numpy()
+        self.wt = self._sampler.w_t.cpu().numpy()
+        self.y_unobserved = self._sampler.y_unobserved.cpu().numpy()
         return self._sampler
 
 

@@ -72,3 +72,43 @@ def test_colouring_after_relabelling(c_oracle, n, m):
     off, rev_j = _reverse(nbr)
     colors, nc = _lib.color_moral_graph(nbr, off, rev_j)
     assert G.coloring_is_valid(nbr, colors)
+
+
+@pytest.mark.parametrize("n_s,n_out,m", [(1, 5, 3), (60, 40, 4), (500, 400, 10)])
+def test_reference_dag_colouring(c_oracle, n_s, n_out, m):
+    """S != T: the DAG of reference points plus leaf data locations (nngp.py:49-71) is
+    coloured properly, with every leaf in the one last colour (update_wt's step)."""
+    from pynngp_amd.gibbs import colour_dag
+
+    rng = np.random.default_rng(n_s + n_out)
+    _, nbr = G.reference_dag(rng.uniform(size=(n_s, 2)), rng.uniform(size=(n_out, 2)), m)
+    off, rev_j = _reverse(nbr)
+    colors, nc, nc_ref = colour_dag(nbr, off, rev_j, n_s)
+    assert nc == nc_ref + 1 and np.all(colors[n_s:] == nc_ref) and colors[:n_s].max() == nc_ref - 1
+    assert G.coloring_is_valid(nbr, colors)
+
+
+def test_reference_dag_sweep_invariant_law(c_oracle):
+    """The colour sweep over the reference-set DAG (leaves first: update_wt, then the
+    reference colours: update_ws), with observations on some leaves and on some reference
+    points, leaves the exact posterior N(P^-1 b, P^-1) invariant."""
+    from pynngp_amd.gibbs import colour_dag
+
+    rng = np.random.default_rng(5)
+    n_s, n_out, m = 10, 8, 3
+    coords, nbr = G.reference_dag(rng.uniform(size=(n_s, 2)), rng.uniform(size=(n_out, 2)), m)
+    n = n_s + n_out
+    B, F, _ = c_oracle.c_bf_sweep(coords, nbr, "exponential", (1.0, 4.0, 0.0))
+    h = np.zeros(n)
+    h[[1, 4, 7]] = 1.0  # three reference points carry data
+    h[n_s:] = rng.uniform(0.5, 2.0, n_out)
+    h[n_s + 2] = 0.0  # an unobserved data location
+    P, b, mu, S = G.dag_posterior(nbr, B, F, 1.3, 0.4, h, rng.standard_normal(n))
+    off, rev_j = _reverse(nbr)
+    colors, nc, nc_ref = colour_dag(nbr, off, rev_j, n_s)
+    order = np.where(colors == nc_ref, 0, colors + 1)  # the leaves' colour step first
+    d = G.color_sweep(P, b, np.zeros(n), order, np.zeros(n))
+    A = np.stack([G.color_sweep(P, b, e, order, np.zeros(n)) - d for e in np.eye(n)], 1)
+    C = np.stack([G.color_sweep(P, b, np.zeros(n), order, e) - d for e in np.eye(n)], 1)
+    np.testing.assert_allclose(A @ mu + d, mu, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(A @ S @ A.T + C @ C.T, S, rtol=1e-9, atol=1e-12)

@@ -164,7 +164,7 @@ def test_one_sample_drop_in(dev):
         ws0 = g.ws.copy()
         for _ in range(5):
             s = g.oneSample(seed=4)
-        assert g.ws.shape == (3000,) and g.wt is g.ws and not np.array_equal(g.ws, ws0)
+        assert g.ws.shape == (3000,) and np.array_equal(g.wt, g.ws) and not np.array_equal(g.ws, ws0)
         assert s.iteration == 5 and np.isfinite(s.sigma2) and np.isfinite(s.tau2)
         runs.append(g.ws)
     np.testing.assert_array_equal(runs[0], runs[1])  # bit-reproducible chain
