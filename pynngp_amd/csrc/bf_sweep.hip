@@ -193,6 +193,71 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
     }
 }
 
+// fixed-order fold of bf_pairb's tile records: rec[t] = (mantissa product m_t, sum r^2/F,
+// bad-pivot row, bad-index row), lexp[t] = exponent sum e_t;  sum log F = sum_t log m_t +
+// (sum_t e_t) ln 2 (the exponents summed exactly as integers)
+__global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restrict__ rec,
+                                                          const int32_t* __restrict__ lexp, int64_t n_tiles,
+                                                          double* __restrict__ partials) {
+    __shared__ double sh[16][4];
+    __shared__ long long she[16];
+    const int t = threadIdx.x;
+    double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+    long long e = 0;
+    for (int64_t k0 = t; k0 < n_tiles; k0 += 4 * 1024) {
+        double4 r[4];
+        int32_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = k0 + (int64_t)u * 1024;
+            r[u] = k < n_tiles ? rec[k] : make_double4(1.0, 0.0, INFINITY, INFINITY);
+            x[u] = k < n_tiles ? lexp[k] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a += log(r[u].x);
+            b += r[u].y;
+            c = fmin(c, r[u].z);
+            d = fmin(d, r[u].w);
+            e += x[u];
+        }
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c = wave_min(c);
+    d = wave_min(d);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o);
+    if ((t & 63) == 0) {
+        sh[t >> 6][0] = a;
+        sh[t >> 6][1] = b;
+        sh[t >> 6][2] = c;
+        sh[t >> 6][3] = d;
+        she[t >> 6] = e;
+    }
+    __syncthreads();
+    if (t == 0) {
+        a = 0.0, b = 0.0, c = INFINITY, d = INFINITY, e = 0;
+        for (int w = 0; w < 16; ++w) {
+            a += sh[w][0];
+            b += sh[w][1];
+            c = fmin(c, sh[w][2]);
+            d = fmin(d, sh[w][3]);
+            e += she[w];
+        }
+        partials[0] = fma((double)e, 0.6931471805599453, a);
+        partials[1] = b;
+        partials[2] = c == INFINITY ? -1.0 : c;
+        partials[3] = d == INFINITY ? -1.0 : d;
+    }
+}
+
+hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, hipStream_t s) {
+    hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(1024), 0, s, (const double4*)ws, pairb_lexp(ws, n_rows),
+                       bf_pairb_tiles(n_rows), partials);
+    return hipGetLastError();
+}
+
 // Rank-order combination of all-gathered (world, 4) partials: sums for [0], [1],
 // smallest non-negative (else -1) for the bad-row flags [2], [3].
 __global__ __launch_bounds__(64) void combine_partials_kernel(const double* __restrict__ g, int world,
@@ -248,7 +313,7 @@ static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
 int64_t bf_record_count(int64_t n_rows, int algo, int m) {
     if (n_rows == 0) return 0;
     if (algo == kAlgoLane) return bf_lane_blocks(n_rows);
-    if (algo == kAlgoPairB) return bf_pairb_blocks(n_rows, m);
+    if (algo == kAlgoPairB) return bf_pairb_tiles(n_rows);
     if (algo == kAlgoPair || algo == kAlgoPairBR1) return bf_group_blocks(n_rows, 2);
     if (algo == kAlgoQuad) return bf_group_blocks(n_rows, 4);
     return bf_wave_blocks(n_rows);
@@ -272,7 +337,10 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     } else if (algo == kAlgoPairB) {
         // unit-variance factorisation (nngp_cov_unit), F scaled by sigma2 in the kernel
         ok = bf_pairb_launch(a, nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2), s);
-        nb = bf_pairb_blocks(a.n_rows, a.m);
+        if (!ok) return hipErrorInvalidValue;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || a.partials == nullptr) return e;
+        return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoPairBR1) {
         ok = bf_pairb_r1_launch(a, P, s);
         nb = bf_group_blocks(a.n_rows, 2);

@@ -417,6 +417,47 @@ class SeqNNGP:
         ph = self._part.cpu().numpy()
         self.sum_logF, self.quad = float(ph[0]), float(ph[1])
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save(self, path) -> None:
+        """Checkpoint the chain: w and the maintained residuals r in node order,
+        beta, sigma2, tau2, phi, the partial sums, the iteration counter (the Philox key of
+        every later draw) and the host RNG state, to an ``.npz`` (no pickles).  A sampler
+        built on the same data and :meth:`restore`-d continues the chain bit for bit."""
+        import json
+
+        meta = {"n": self.n, "n_s": self.n_s, "m": self.m, "kind": self.kind, "p": self.p, "seed": self.seed,
+                "iteration": self.iteration, "n_accept": self.n_accept, "n_notpd_reject": self.n_notpd_reject,
+                "sigma2": self.sigma2, "tau2": self.tau2, "phi": self.phi, "sum_logF": self.sum_logF,
+                "quad": self.quad, "rng": self.rng.bit_generator.state}
+        np.savez(path, w=self.w[self.pos].cpu().numpy(), r=self.r[self.pos].cpu().numpy(), beta=np.asarray(self.beta),
+                 y_unobserved=self.y_unobserved.cpu().numpy(), meta=np.array(json.dumps(meta)))
+
+    def restore(self, path) -> "SeqNNGP":
+        """Resume from :meth:`save` (the sampler must be built on the same data and settings)."""
+        import json
+
+        with np.load(path, allow_pickle=False) as z:
+            meta = json.loads(str(z["meta"]))
+            for k in ("n", "n_s", "m", "kind", "p", "seed"):
+                if meta[k] != getattr(self, k):
+                    raise ValueError(f"checkpoint {k}={meta[k]!r} does not match this sampler's {getattr(self, k)!r}")
+            to = lambda a: torch.as_tensor(a).to(self.device)  # noqa: E731
+            self.w = to(z["w"])[self.perm].contiguous()
+            r = to(z["r"])[self.perm].contiguous()
+            self.beta = np.array(z["beta"])
+            self.y_unobserved.copy_(to(z["y_unobserved"]))
+        self.sigma2, self.tau2, self.phi = meta["sigma2"], meta["tau2"], meta["phi"]
+        self.iteration, self.n_accept, self.n_notpd_reject = meta["iteration"], meta["n_accept"], meta["n_notpd_reject"]
+        self.rng.bit_generator.state = meta["rng"]
+        # B, F (and the folded prep) are functions of phi alone; r is the chain's own running value
+        self._sweep_into(self.phi, self.B, self.Ft, self.r)
+        self._check(self._part.cpu().numpy())
+        self.r = r
+        self.sum_logF, self.quad = meta["sum_logF"], meta["quad"]
+        self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
+        self.yres = self._residual_y(self.beta)
+        return self
+
     @property
     def w_nodes(self) -> torch.Tensor:
         """w in model node order: the reference points, then the data locations outside S."""

@@ -133,7 +133,7 @@ def test_reference_set_predicts_held_out(dev):
     s = rng.uniform(size=(1000, 2))
     smp = SeqNNGP(t, y, m=10, ref=s, sigma2=1.0, tau2=0.2, phi=5.0, seed=2, device=dev, phi_tuning=0.1,
                   priors=Priors(phi_unif=(1.0, 30.0)))
-    res = smp.sample(400, burn=150, keep_w_mean=True)
+    res = smp.sample(1500, burn=1000, keep_w_mean=True)  # tau2 and the leaves' w mix slowly
     pred = res["y_unobserved_mean"][: len(hide)]
     assert np.array_equal(smp.unobserved_t, np.sort(hide))
     assert np.corrcoef(pred, y_true[np.sort(hide)])[0, 1] > 0.8
@@ -161,3 +161,31 @@ def test_one_sample_random_reference_set(dev):
         runs.append((g.ws, g.wt, g.y_unobserved))
     for a, b in zip(*runs):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("with_ref", [False, True])
+def test_checkpoint_resume_bit_identical(dev, tmp_path, with_ref):
+    """save() after k iterations + restore() into a fresh sampler continues the chain bit
+    for bit (Philox keyed by (seed, location, iteration); host RNG state restored)."""
+    from pynngp_amd import SeqNNGP
+
+    rng = np.random.default_rng(4)
+    s, t, y = _data(rng, 400, 600, 50, 30)
+    kw = dict(m=8, sigma2=1.0, tau2=0.2, phi=5.0, seed=5, device=dev, phi_tuning=0.2, ref=s if with_ref else None)
+    if not with_ref:
+        y = np.where(np.isfinite(y), y, 0.0)
+    a = SeqNNGP(t, y, **kw)
+    for _ in range(6):
+        a.step()
+    a.save(tmp_path / "ck.npz")
+    for _ in range(6):
+        a.step()
+    b = SeqNNGP(t, y, **kw).restore(tmp_path / "ck.npz")
+    assert b.iteration == 6
+    for _ in range(6):
+        b.step()
+    assert torch.equal(a.w, b.w) and torch.equal(a.r, b.r) and torch.equal(a.y_unobserved, b.y_unobserved)
+    assert (a.phi, a.sigma2, a.tau2, a.n_accept) == (b.phi, b.sigma2, b.tau2, b.n_accept)
+    np.testing.assert_array_equal(a.beta, b.beta)
+    with pytest.raises(ValueError, match="m="):
+        SeqNNGP(t, y, **{**kw, "m": 6}).restore(tmp_path / "ck.npz")
