@@ -164,6 +164,9 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=None,
+                    help="BASELINE.json config preset: 2 = N=1e5, m=15, Matern-3/2 (tau2=0.1); 3 = the headline "
+                         "(default flags); 4 = N=1e7 / world per GPU, m=20, exponential")
     # defaults: the GPU clock settles over the first ~50 ms of sustained load (the sweep
     # kernel goes from ~218 to ~187 us over its first ~200 launches), so the
     # default warm-up is 200 sweeps; both still finish in well under a second
@@ -184,6 +187,10 @@ def main():
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
+    if args.config == 2:
+        args.n, args.m, args.kind, args.theta = 100_000, 15, "matern32", "1.0,17.320508075688772,0.1"
+    elif args.config == 4:
+        args.n, args.m = 10_000_000 // int(os.environ.get("WORLD_SIZE", "1")), 20
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -281,7 +288,8 @@ def main():
                 "workload": "BASELINE config 3: fused B/F + log-lik sweep, N=1,000,000 locations per GPU, m=15, "
                             "exponential covariance" if (args.n == 1_000_000 and args.m == 15
                                                          and args.kind == "exponential") else
-                            f"fused B/F + log-lik sweep, N={args.n} per GPU, m={args.m}, {args.kind}",
+                            (f"BASELINE config {args.config}: " if args.config else "")
+                            + f"fused B/F + log-lik sweep, N={args.n} per GPU, m={args.m}, {args.kind}",
                 "n_per_gpu": args.n,
                 "n_total": n_total,
                 "m": args.m,

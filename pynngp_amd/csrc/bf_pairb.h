@@ -25,21 +25,16 @@
 //
 // Round 2 (profiles/r02b: the kernel keeps the VALU pipe busy, so only fewer
 // instructions per location make it faster):
-//   * persistent grid: each 256-thread block walks a contiguous range of 128-location
-//     tiles (XCD-contiguous logical blocks), so the table fill and the block reduction
-//     are paid once per block, not once per tile;
 //   * unit-variance covariances (nngp_cov_unit: the exponent of 2^n is added to the
 //     table entry's exponent field, one integer op instead of ashr + ldexp), F scaled
 //     by sigma2 at the end (B and the residual are scale-invariant);
-//   * one partial record per 128-location tile, whichever block computes it (so the
-//     fold is bit-reproducible under any schedule): sum log F leaves the kernel as the
+//   * one partial record per 128-location tile: sum log F leaves the kernel as the
 //     tile's mantissa product and exponent sum (frexp), and the ~100-instruction log is
 //     taken once per record by the fold (bf_finalize_pairb), not per lane;
-//     r^2 / F through v_rcp_f64 + two Newton steps instead of the IEEE divide;
-//   * schedules (A/B knob NNGP_PAIRB_MODE): "dyn" -- a persistent grid whose blocks claim
-//     tiles from one counter per XCD (the blocks of XCD x = blockIdx % 8 walk that XCD's
-//     contiguous eighth of the tiles), "static" -- a persistent grid with one contiguous
-//     tile range per block, "grid" -- one tile per block (hardware scheduling).
+//     r^2 / F through v_rcp_f64 + two Newton steps instead of the IEEE divide.
+//   One block per tile, hardware-scheduled: persistent grids (static ranges, ranges with
+//   issue-priority balancing, tiles claimed from per-XCD counters) all measured slower
+//   (profiles/r02j, r02l, r02m).
 // D = coordinate dimension (1..3), KIND = covariance kind (nngp_math.h).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -71,8 +66,8 @@ constexpr int kPairbTile = 128;  // locations per 256-thread tile
 // Tile record fold: wave butterflies (fixed order), then the 4 waves in order by thread 0.
 // lm: product of the lanes' F mantissas (each in [0.5, 1); 128 of them stay above 2^-128),
 // renormalised once; le: their exponent sum.  rec[tile] = (mantissa, sum r^2/F, first
-// bad-pivot row, first bad-index row), lexp[tile] = exponent sum.  sh is double-buffered
-// by tile parity, so one barrier per tile suffices.
+// bad-pivot row, first bad-index row), lexp[tile] = exponent sum.  sh[par] lets a
+// multi-tile caller double-buffer the exchange (one barrier per tile).
 __device__ __forceinline__ void pairb_tile_store(double lm, int le, double qq, double badp, double badi,
                                                  double (*sh)[4][5], int par, double4* __restrict__ rec,
                                                  int32_t* __restrict__ lexp, int64_t tile) {
@@ -125,8 +120,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
                                                 const double* __restrict__ values, const double* __restrict__ qcoords,
                                                 const double* __restrict__ qvalues, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double4* __restrict__ rec, int32_t* __restrict__ lexp,
-                                                uint32_t* __restrict__ tilectr, bool pairb_prio) {
+                                                double4* __restrict__ rec, int32_t* __restrict__ lexp) {
     static_assert(M >= 1 && M <= 24, "pairb instantiated for 1 <= m <= 24");
     static_assert(D >= 1 && D <= 3, "1 <= D <= 3");
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
@@ -135,43 +129,12 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
     __shared__ double etab[NNGP_EXP_TAB_N];
     nngp_exp_table_load_unit(etab);
 
-    __shared__ double sh[2][4][5];
-    __shared__ int64_t s_claim[2];
-    const int64_t n_tiles = (n_rows + kPairbTile - 1) / kPairbTile;
-    int64_t tile, t_end, c0 = 0;
-    uint32_t* ctr = nullptr;
-    if (tilectr != nullptr) {  // dynamic: claim from XCD x's counter (gridDim.x >= 8, checked by the launcher)
-        const int x = (int)(blockIdx.x & 7);
-        c0 = n_tiles * x / 8;
-        t_end = n_tiles * (x + 1) / 8;
-        ctr = tilectr + x * 32;
-        if (threadIdx.x == 0) s_claim[1] = c0 + (int64_t)atomicAdd(ctr, 1u);
-        __syncthreads();
-        tile = s_claim[1];
-    } else if ((int64_t)gridDim.x >= n_tiles) {  // one tile per block
-        tile = xcd_logical_block(blockIdx.x, gridDim.x);
-        t_end = tile + 1;
-    } else {  // static persistent: a contiguous tile range per block
-        const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
-        tile = n_tiles * blk / gridDim.x;
-        t_end = n_tiles * (blk + 1) / gridDim.x;
-    }
+    __shared__ double sh[1][4][5];
+    const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
     const int q = (int)(threadIdx.x & 1);
     const bool q1 = q == 1;
     const bool lead0 = !q1;
-
-    const bool prio = ctr == nullptr && pairb_prio;
-    for (int par = 0; tile < t_end; par ^= 1) {
-        if (prio) {
-            // static ranges: the issue arbiter favours the older of a SIMD's two waves, so one
-            // runs ahead and the other finishes alone at one wave per SIMD; a wave with more of
-            // its range left takes a higher issue priority, which keeps the two in step
-            const int64_t rem = t_end - tile;
-            if (rem > 8) __builtin_amdgcn_s_setprio(3);
-            else if (rem > 4) __builtin_amdgcn_s_setprio(2);
-            else if (rem > 2) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
+    {
         const int64_t r = tile * kPairbTile + (threadIdx.x >> 1);
         const bool live = r < n_rows;
         const int64_t rl = live ? r : n_rows - 1;
@@ -346,73 +309,31 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
         if (Rout != nullptr && lead) Rout[rr] = bad ? NAN : res;
         // this lane's terms of the tile record (lead lanes; a NaN F -- a bad pivot -- propagates
         // into the mantissa product as log(NaN) would; the flag is what callers check)
-        uint32_t claim = 0;
-        if (ctr != nullptr && threadIdx.x == 0) claim = atomicAdd(ctr, 1u);  // the next tile; overlaps the fold
         pairb_tile_store(lead ? __builtin_amdgcn_frexp_mant(F) : 1.0, lead ? __builtin_amdgcn_frexp_exp(F) : 0,
                          lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)i : INFINITY,
-                         (live && bad_index) ? (double)i : INFINITY, sh, par, rec, lexp, tile);
-        if (ctr != nullptr && threadIdx.x == 0) s_claim[par] = c0 + (int64_t)claim;
+                         (live && bad_index) ? (double)i : INFINITY, sh, 0, rec, lexp, tile);
         __syncthreads();
-        if (threadIdx.x == 0) pairb_tile_fold(sh, par, rec, lexp, tile);
-        tile = ctr != nullptr ? s_claim[par] : tile + 1;
+        if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
     }
-}
-
-// Schedules (NNGP_PAIRB_MODE, read once; any schedule gives bit-identical results):
-//   dyn (default) -- persistent grid, tiles claimed from per-XCD counters;
-//   static        -- persistent grid, one contiguous tile range per block;
-//   grid          -- one block per tile.
-// Persistent grids hold 2 blocks of 256 threads per CU (two waves per SIMD) for m <= 17,
-// 1 above; NNGP_PAIRB_BLOCKS overrides that size (A/B knob for DESIGN.md's measurements).
-enum PairbMode { kPairbDyn = 0, kPairbStatic = 1, kPairbGrid = 2, kPairbPrio = 3 };
-
-inline int pairb_mode() {
-    static const int mode = [] {
-        const char* e = getenv("NNGP_PAIRB_MODE");
-        if (e == nullptr || strcmp(e, "dyn") == 0) return (int)kPairbDyn;
-        if (strcmp(e, "prio") == 0) return (int)kPairbPrio;
-        return strcmp(e, "static") == 0 ? (int)kPairbStatic : (int)kPairbGrid;
-    }();
-    return mode;
 }
 
 inline int64_t bf_pairb_tiles(int64_t n_rows) { return (n_rows + kPairbTile - 1) / kPairbTile; }
 
-inline int64_t bf_pairb_blocks(int64_t n_rows, int m) {
-    static const int64_t env_cap = [] {
-        const char* e = getenv("NNGP_PAIRB_BLOCKS");
-        return e != nullptr ? (int64_t)atoll(e) : (int64_t)0;
-    }();
-    const int64_t tiles = bf_pairb_tiles(n_rows);
-    if (pairb_mode() == kPairbGrid) return tiles < 1 ? 1 : tiles;
-    const int64_t cap = env_cap > 0 ? env_cap : (m <= NNGP_PAIRB_TWO_WAVES_MAX ? 512 : 256);
-    return tiles < 1 ? 1 : (tiles > cap ? cap : tiles);
-}
-
-// workspace: tile records (32 B each), tile exponent sums (4 B each), 8 x 128 B tile counters
+// workspace: tile records (32 B each), tile exponent sums (4 B each)
 inline size_t pairb_align(size_t b) { return (b + 255) & ~(size_t)255; }
 inline size_t bf_pairb_workspace_bytes(int64_t n_rows) {
     const int64_t t = bf_pairb_tiles(n_rows);
-    return t > 0 ? pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) + 8 * 128 : 0;
+    return t > 0 ? pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) : 0;
 }
 inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
     return (int32_t*)((char*)ws + pairb_align((size_t)bf_pairb_tiles(n_rows) * 32));
 }
-inline uint32_t* pairb_counters(void* ws, int64_t n_rows) {
-    return (uint32_t*)((char*)pairb_lexp(ws, n_rows) + pairb_align((size_t)bf_pairb_tiles(n_rows) * 4));
-}
 
 template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    const int64_t nb = bf_pairb_blocks(a.n_rows, M);
-    uint32_t* ctr = nullptr;
-    if (pairb_mode() == kPairbDyn && nb >= 8 && nb < bf_pairb_tiles(a.n_rows)) {
-        ctr = pairb_counters(a.bpart, a.n_rows);
-        (void)hipMemsetAsync(ctr, 0, 8 * 128, s);
-    }
-    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)nb), dim3(256), 0, s, a.coords, a.n_points, a.nbr,
-                       a.order, a.n_rows, a.i0, Pc, a.sigma2, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R,
-                       (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), ctr, pairb_mode() == kPairbPrio);
+    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(256), 0, s, a.coords,
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.sigma2, a.values, a.qcoords, a.qvalues, a.B,
+                       a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows));
 }
 
 // one m and dimension, every kind (instantiated by the generated bf_pairb_inst_*.hip units)

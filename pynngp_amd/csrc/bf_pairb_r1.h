@@ -36,25 +36,37 @@
 namespace nngp {
 namespace r1 {
 
+template <int KIND, int VAR>
+__device__ __forceinline__ double cov(const CovParams& P, const double* tab, double d2) {
+    if (VAR & 1) return nngp_cov_unit<KIND>(P, tab, d2);
+    return nngp_cov_d2<KIND>(P, tab, d2);
+}
+
 
 // Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
 // (<= 256 VGPRs): m = 16 / 17 then fit in 248 / 252 VGPRs without spills instead of
 // 264 / 266 (one wave per SIMD).  Beyond it the block needs more registers than that.
 
-template <int M, int KIND>
+// VAR (A/B of the round-2 changes one at a time): bit 0 -- unit-variance covariances
+// (nngp_cov_unit, F scaled by sigma2 at the end); bit 1 -- a tile record with the log
+// deferred to the fold (pairb_tile_store / bf_finalize_pairb) instead of log per lane.
+template <int M, int KIND, int VAR>
 __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0, const CovParams Pc,
                                                 const double* __restrict__ values, const double2* __restrict__ qcoords,
                                                 const double* __restrict__ qvalues, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double* __restrict__ bpart) {
+                                                double* __restrict__ bpart, double sigma2, int32_t* __restrict__ lexp) {
     static_assert(M >= 1 && M <= 24, "pairb instantiated for 1 <= m <= 24");
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
     __shared__ double etab[NNGP_EXP_TAB_N];
-    nngp_exp_table_load(etab, Pc.sigma2);
+    if (VAR & 1)
+        nngp_exp_table_load_unit(etab);
+    else
+        nngp_exp_table_load(etab, Pc.sigma2);
 
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
     const int64_t tid = blk * blockDim.x + threadIdx.x;
@@ -106,11 +118,11 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* _
         for (int s = 0; s < NP; ++s) {
 #pragma unroll
             for (int t = 0; t < s; ++t) {
-                R[s][t][0] = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], ox[t], oy[t]));
-                R[s][t][1] = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], px[t], py[t]));
+                R[s][t][0] = cov<KIND, VAR>(Pc, etab, nngp_d2(ox[s], oy[s], ox[t], oy[t]));
+                R[s][t][1] = cov<KIND, VAR>(Pc, etab, nngp_d2(ox[s], oy[s], px[t], py[t]));
             }
             R[s][s][0] = Pc.diag;
-            const double c = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], px[s], py[s]));
+            const double c = cov<KIND, VAR>(Pc, etab, nngp_d2(ox[s], oy[s], px[s], py[s]));
             R[s][s][1] = q1 ? c : 0.0;
         }
     }
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* _
         res = pr_from0(z[T]);
     }
     bad |= !(F > 0.0);
+    if (VAR & 1) F *= sigma2;
 
     if (Bout != nullptr) {
         // B = L_N^{-T} v, v = row M of L (lane M % 2, local row M / 2).  Lane q ends with
@@ -235,6 +248,15 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* _
     if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
     if (Rout != nullptr && lead) Rout[rr] = bad ? NAN : res;
 
+    if (VAR & 2) {
+        __shared__ double sh[2][4][5];
+        pairb_tile_store(lead ? __builtin_amdgcn_frexp_mant(F) : 1.0, lead ? __builtin_amdgcn_frexp_exp(F) : 0,
+                         lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)i : INFINITY,
+                         (live && bad_index) ? (double)i : INFINITY, sh, 0, (double4*)bpart, lexp, blk);
+        __syncthreads();
+        if (threadIdx.x == 0) pairb_tile_fold(sh, 0, (double4*)bpart, lexp, blk);
+        return;
+    }
     double lf = 0.0, qq = 0.0, badp = INFINITY, badi = INFINITY;
     if (lead) {
         lf = log(F);
@@ -245,11 +267,12 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double2* _
     block_partials_store(lf, qq, badp, badi, bpart, blk);
 }
 
-template <int M, int KIND>
+template <int M, int KIND, int VAR>
 static void launch_pairb_mk(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * 2 + 255) / 256;
-    hipLaunchKernelGGL((bf_pairb<M, KIND>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
+    hipLaunchKernelGGL((bf_pairb<M, KIND, VAR>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, (const double2*)a.qcoords, a.qvalues,
+                       a.B, a.F, a.R, a.bpart, a.sigma2, pairb_lexp(a.bpart, a.n_rows));
 }
 
 

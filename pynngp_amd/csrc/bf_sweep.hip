@@ -342,8 +342,14 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         if (e != hipSuccess || a.partials == nullptr) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoPairBR1) {
-        ok = bf_pairb_r1_launch(a, P, s);
+        const int var = pairb_r1_variant();
+        ok = bf_pairb_r1_launch(a, (var & 1) ? nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2) : P, s);
         nb = bf_group_blocks(a.n_rows, 2);
+        if (ok && (var & 2)) {
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess || a.partials == nullptr) return e;
+            return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
+        }
     } else if (algo == kAlgoPair || algo == kAlgoQuad) {
         const int lanes = algo == kAlgoPair ? 2 : 4;
         ok = a.dim == 2 && a.kind <= 1 && bf_group_launch(a, P, lanes, s);

@@ -71,7 +71,8 @@ double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo) {
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return 0;
     const int a = resolve_algo(algo, m, kind, dim);
-    if (a == nngp::kAlgoPairB) return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + counters
+    if (a == nngp::kAlgoPairB || a == nngp::kAlgoPairBR1)
+        return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + counters
     const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a, m) : 0;
     return align256((size_t)nb * 4 * sizeof(double));
 }
@@ -146,7 +147,8 @@ int nngp_bf_finalize(const void* workspace, int64_t n_rows, int32_t m, int32_t k
     if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
     const int a = resolve_algo(algo, m, kind, dim);
-    hipError_t e = a == nngp::kAlgoPairB && n_rows > 0
+    hipError_t e = (a == nngp::kAlgoPairB || (a == nngp::kAlgoPairBR1 && (nngp::pairb_r1_variant() & 2))) &&
+                           n_rows > 0
                        ? nngp::bf_finalize_pairb_launch((void*)workspace, n_rows, partials, (hipStream_t)stream)
                        : nngp::bf_finalize_launch((const double*)workspace, nngp::bf_record_count(n_rows, a, m),
                                                   partials, (hipStream_t)stream);

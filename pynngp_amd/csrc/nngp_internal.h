@@ -98,6 +98,7 @@ bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
 bool bf_pairb_r1_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
+int pairb_r1_variant();
 // number of 256-thread blocks (= partial records) each kernel launches for n_rows
 int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);

@@ -218,9 +218,12 @@ NNGP_FN double nngp_exp_unit(const CovParams& P, const double* tab, double u) {
     const int32_t hi = (int32_t)(tb >> 32) + (int32_t)((uint32_t)ki << 12);
     const double Ts = __hiloint2double(hi, (int32_t)(tb & 0xffffffffll));  // 2^(j/256) 2^n
 #endif
-    double q = fma(P.q[3], f, P.q[2]);
-    q = fma(q, f, P.q[1]);
-    q = fma(q, f, P.q[0]);
+    // the coefficients as literals (not CovParams fields): the persistent kernels re-materialise
+    // them instead of pinning 8 more SGPRs for the whole tile loop
+    constexpr double Q[4] = NNGP_EXP2_Q;
+    double q = fma(Q[3], f, Q[2]);
+    q = fma(q, f, Q[1]);
+    q = fma(q, f, Q[0]);
     return fma(Ts, f * q, Ts);
 }
 

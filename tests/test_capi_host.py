@@ -47,12 +47,12 @@ def test_version_and_loglik_helper(lib):
 
 def test_workspace_sizes(lib):
     # (n_rows, m, kind, dim, algo): the blocked pair kernel keeps one 32-B record and one 4-B exponent
-    # per 128-location tile plus 1 KiB of tile counters, the lane kernel a record per 256 rows
+    # per 128-location tile, the lane kernel a record per 256 rows
     al = lambda b: (b + 255) // 256 * 256  # noqa: E731
     tiles = (1_000_000 + 127) // 128
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 0) == al(32 * tiles) + al(4 * tiles) + 1024
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 0) == al(32 * tiles) + al(4 * tiles)
     assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 0, 2, 0) >= 4 * 8 * (1_000_000 // 256)
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 3, 2, 0) == al(32 * tiles) + al(4 * tiles) + 1024
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 3, 2, 0) == al(32 * tiles) + al(4 * tiles)
     assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0, 2, 0) == 0
     assert lib.nngp_bf_sweep_workspace_bytes(0, 15, 0, 2, 0) == 0
     assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0, 3, 0) > 0
