@@ -54,10 +54,12 @@ __device__ __forceinline__ double pr_from1(double v) { return dpp_f64<0xF5>(v); 
 __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return q1 ? v1 : v0; }
 
 // Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
-// (<= 256 VGPRs): m = 16 / 17 then fit in 248 / 252 VGPRs without spills instead of
-// 264 / 266 (one wave per SIMD).  Beyond it the block needs more registers than that.
+// (<= 256 VGPRs): m = 16 / 17 fit in 246 / 250 VGPRs without spills; m = 18 / 19 spill 27 / 23
+// dwords to scratch and still run 22 % faster than at one wave per SIMD (282 / 278 VGPRs;
+// same-box A/B, profiles/r02p).  From m = 20 (342 VGPRs) the forced spills (91 dwords) cost
+// more than the second wave gains (+52 % at m = 20, 2-3x at m = 22 / 24).
 #ifndef NNGP_PAIRB_TWO_WAVES_MAX
-#define NNGP_PAIRB_TWO_WAVES_MAX 17
+#define NNGP_PAIRB_TWO_WAVES_MAX 19
 #endif
 #define NNGP_PAIRB_ATTR __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), 2)))
 

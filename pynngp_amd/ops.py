@@ -31,7 +31,9 @@ from . import _lib
 
 _KINDS = tuple(_lib.KIND_CODES)  # code order: exponential, matern32, matern52, gaussian, spherical
 _ALGOS = dict(_lib.ALGO_CODES)
-LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libnngp_torch_ops.so")
+# always the in-tree build; it binds to whichever libnngp_hip.so _lib loaded first (matched by
+# SONAME, so an NNGP_LIB variant build is the one the operators call)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libnngp_torch_ops.so")
 
 _loaded = False
 

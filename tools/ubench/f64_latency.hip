@@ -73,6 +73,24 @@ IND32(i_and, "v_and_b32 %0, %0, %1")
 DEP32(d_and, "v_and_b32 %0, %0, %1")
 DEP32(d_cnd, "v_cndmask_b32 %0, %0, %1, vcc")
 
+IND32(i_rsq32, "v_rsq_f32 %0, %0")
+IND_KERNEL(i_sqrt64, "v_sqrt_f64 %0, %0")
+IND_KERNEL(i_rcp64, "v_rcp_f64 %0, %0")
+// one transcendental + three independent FMAs per group: does v_rsq_f64 overlap plain VALU?
+__global__ void mix_rsq_fma(double* out, long long* cyc) {
+    double a0 = threadIdx.x + 1.0, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, b = 1.0000001, c = 0.5;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    R64(asm volatile("v_rsq_f64 %0, %0" : "+v"(a0)); asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a1) : "v"(b), "v"(c));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a2) : "v"(b), "v"(c));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a3) : "v"(b), "v"(c));
+        asm volatile("v_rsq_f64 %0, %0" : "+v"(a0)); asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a1) : "v"(b), "v"(c));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a2) : "v"(b), "v"(c));
+        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(a3) : "v"(b), "v"(c));)
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = a0 + a1 + a2 + a3;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
     double* out;
     long long* cyc;
@@ -84,7 +102,9 @@ int main() {
     } ks[] = {{"dep v_fma_f64", d_fma, 512}, {"dep v_mul_f64", d_mul, 512}, {"dep v_add_f64", d_add, 512},
               {"dep v_rsq_f64", d_rsq, 512}, {"dep v_min_f64", d_min, 512}, {"dep v_mov_b32_dpp", d_dpp, 512},
               {"ind8 v_fma_f64", i_fma, 512}, {"ind8 v_mul_f64", i_mul, 512}, {"ind8 v_add_f64", i_add, 512},
-              {"ind8 v_rsq_f64", i_rsq, 512}, {"ind8 v_mov_b32_dpp", i_dpp, 512}, {"ind8 v_and_b32", i_and, 512}, {"dep v_and_b32", d_and, 512}, {"dep v_cndmask_b32", d_cnd, 512}};
+              {"ind8 v_rsq_f64", i_rsq, 512}, {"ind8 v_mov_b32_dpp", i_dpp, 512}, {"ind8 v_and_b32", i_and, 512}, {"dep v_and_b32", d_and, 512}, {"dep v_cndmask_b32", d_cnd, 512},
+              {"ind8 v_rsq_f32", i_rsq32, 512}, {"ind8 v_sqrt_f64", i_sqrt64, 512}, {"ind8 v_rcp_f64", i_rcp64, 512},
+              {"mix rsq_f64+3 fma (per group of 4)", mix_rsq_fma, 128}};
     for (auto& k : ks) {
         long long best = -1;
         for (int rep = 0; rep < 5; ++rep) {
