@@ -129,7 +129,8 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
     __shared__ double etab[NNGP_EXP_TAB_N];
-    nngp_exp_table_load_unit(etab);
+    static_assert(NNGP_EXP_TAB_N == 256, "one table entry per thread of the 256-thread block");
+    const double etab_entry = nngp_exp_table_fetch_unit();  // issued before the gathers
 
     __shared__ double sh[1][4][5];
     const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -140,7 +141,10 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
         const int64_t r = tile * kPairbTile + (threadIdx.x >> 1);
         const bool live = r < n_rows;
         const int64_t rl = live ? r : n_rows - 1;
-        const int64_t rr = order != nullptr ? (int64_t)order[rl] : rl;
+        // branch-free (a branch here makes the compiler drain every outstanding load, the
+        // early exp-table fetch included, at the join): without an order, read nbr's word
+        const int32_t ov = (order != nullptr ? order : nbr)[rl];
+        const int64_t rr = order != nullptr ? (int64_t)ov : rl;
         const int64_t i = i0 + rr;
 
         // ---- gathers (branch-free, as bf_group): own rows a = 2s + q
@@ -167,6 +171,10 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             load_point<D>(pc, o[s]);
             z[s] = *pv;
         }
+
+        // the exp table entry was fetched before the gathers; storing it here lets its load and
+        // the barrier overlap the gathers' latency instead of preceding it
+        nngp_exp_table_store_unit(etab, etab_entry);
 
         // ---- unit-variance covariances in own-parity-first order
         double R[NP][NP][2];
