@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="testing only: every rank on cuda:0 with gloo collectives (the N-rank flow on one GPU)")
+    ap.add_argument("--sweep-api", default="ops", choices=["ops", "ctypes"],
+                    help="ops: torch.ops.nngp.bf_sweep_out (default); ctypes: the same C ABI via ctypes (A/B)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
@@ -218,7 +220,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order,
-                          layout=args.layout)
+                          layout=args.layout, api=args.sweep_api)
     if args.layout == "storage":
         # the synthetic field lives in the engine's storage order (an MCMC state would);
         # same iid N(0,1) values, assigned to locations in storage order
@@ -299,6 +301,7 @@ def main():
                 "row_order": "index" if args.no_order else "z-order",
                 "layout": args.layout,
                 "write_BF": want_bf,
+                "sweep_api": "torch.ops.nngp.bf_sweep_out" if args.sweep_api == "ops" else "ctypes",
                 "global_batch": n_total,
                 "parallelism": f"dp{world} (contiguous Z-order location shards; one RCCL all-gather of 4 partials "
                                "per sweep, overlapped with the next sweep)",

@@ -70,9 +70,13 @@ class ShardedLogLik:
 
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
                  algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
-                 spatial_order: bool = True, layout: str = "natural", build_perm: Optional[Callable] = None):
+                 spatial_order: bool = True, layout: str = "natural", build_perm: Optional[Callable] = None,
+                 api: str = "ops"):
         if layout not in ("natural", "storage"):
             raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
+        if api not in ("ops", "ctypes"):
+            raise ValueError(f"api must be 'ops' (torch.ops.nngp) or 'ctypes' (the same C ABI via ctypes), got {api!r}")
+        self.api = api
         self.layout = layout
         if not bool(torch.isfinite(coords).all()):
             raise ValueError("coordinates must be finite (NaN / inf would silently decouple locations)")
@@ -132,6 +136,10 @@ class ShardedLogLik:
         B, F = (self._B, self._F) if want_bf else (None, None)
         p = self._partials if out is None else out
         s2, phi, tau2 = cov.theta
+        if self.api == "ctypes":  # the same C-ABI call without the dispatcher (A/B of the op overhead)
+            _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, s2, phi, tau2, values=values,
+                          want_bf=want_bf, algo=self.algo, B=B, F=F, partials=p, workspace=self._ws, order=self.order)
+            return p
         torch.ops.nngp.bf_sweep_out(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
                                     float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws,
                                     self._algo_code)
