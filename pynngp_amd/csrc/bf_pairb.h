@@ -61,7 +61,15 @@ __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return
 #ifndef NNGP_PAIRB_TWO_WAVES_MAX
 #define NNGP_PAIRB_TWO_WAVES_MAX 19
 #endif
-#define NNGP_PAIRB_ATTR __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), 2)))
+// Three waves per SIMD (<= 168 VGPRs) up to m = NNGP_PAIRB_THREE_WAVES_MAX: m = 12 / 13 fit
+// in 162 / 164 VGPRs (-3.7 % cycles at m = 13); forced at m = 14 / 15 the 31 / 35 spilled
+// dwords cost more (+10 % / +37 %, profiles/r02y).
+#ifndef NNGP_PAIRB_THREE_WAVES_MAX
+#define NNGP_PAIRB_THREE_WAVES_MAX 13
+#endif
+#define NNGP_PAIRB_ATTR                                                                              \
+    __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), \
+                                       (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : 2))))
 
 constexpr int kPairbTile = 128;  // locations per 256-thread tile
 

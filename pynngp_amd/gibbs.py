@@ -99,6 +99,8 @@ class SeqNNGP:
         dev = self.device
         self.kind = kind
         self.m = int(m)
+        if not 1 <= self.m <= _lib.MAX_M:
+            raise ValueError(f"m={m} outside [1, {_lib.MAX_M}]")
         self.priors = priors or Priors()
         self.algo = algo
         self.seed = int(seed)

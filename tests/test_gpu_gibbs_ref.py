@@ -189,3 +189,18 @@ def test_checkpoint_resume_bit_identical(dev, tmp_path, with_ref):
     np.testing.assert_array_equal(a.beta, b.beta)
     with pytest.raises(ValueError, match="m="):
         SeqNNGP(t, y, **{**kw, "m": 6}).restore(tmp_path / "ck.npz")
+
+
+def test_reference_set_rejects_repeated_points(dev):
+    """A reference set with a repeated point (('subset', nRef) draws with replacement,
+    nngp.py:36) makes C_N singular: refused with the offending indices."""
+    from pynngp_amd import SeqNNGP
+
+    rng = np.random.default_rng(2)
+    t = rng.uniform(size=(500, 2))
+    y = rng.standard_normal(500)
+    s = t[[3, 10, 3, 40, 77]]  # point 2 repeats point 0
+    with pytest.raises(ValueError, match="repeats point 0"):
+        SeqNNGP(t, y, m=3, ref=s, device=dev)
+    with pytest.raises(ValueError, match="m=0"):
+        SeqNNGP(t, y, m=0, device=dev)
