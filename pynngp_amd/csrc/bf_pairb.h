@@ -48,10 +48,58 @@
 
 namespace nngp {
 
-__device__ __forceinline__ double pr_swap(double v) { return dpp_f64<0xB1>(v); }   // partner lane's v
-__device__ __forceinline__ double pr_from0(double v) { return dpp_f64<0xA0>(v); }  // lane 0's v
-__device__ __forceinline__ double pr_from1(double v) { return dpp_f64<0xF5>(v); }  // lane 1's v
+// Pair exchanges.  NNGP_PAIRB_SWZ bit 0: the partner swaps go through ds_swizzle (quad-perm
+// mode) on the LDS pipe instead of two v_mov_dpp on the VALU; bit 1: the lane-0 / lane-1
+// broadcasts too.  The kernel is VALU-issue bound, so an exchange issued on the LDS pipe
+// co-issues with the other wave's VALU work.
+#ifndef NNGP_PAIRB_SWZ
+#define NNGP_PAIRB_SWZ 0
+#endif
+// The within-pair covariance split (below) up to m = NNGP_PAIRB_DEDUP_MAX: it keeps the partner
+// coordinates live longer (+20 VGPRs at m = 15), which costs spills past m = 17.
+#ifndef NNGP_PAIRB_DEDUP_MAX
+#define NNGP_PAIRB_DEDUP_MAX 17
+#endif
+// NNGP_PAIRB_NOZ: no value column in the elimination; the residual is r = v_i - B v_N after
+// the back-substitution (B is then always computed): 5 % fewer VALU at m = 15.  Not at m = 19,
+// where it moved the register peak (100 -> 220 B of scratch, 0.394 -> 0.499 ms per 10^6 rows).
+#ifndef NNGP_PAIRB_NOZ
+#define NNGP_PAIRB_NOZ 1
+#endif
+// static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
+#ifdef NNGP_PAIRB_PHASES
+#define NNGP_PHASE(name)                        \
+    __builtin_amdgcn_sched_barrier(0);          \
+    asm volatile("; PHASE_" #name ::: "memory"); \
+    __builtin_amdgcn_sched_barrier(0)
+#else
+#define NNGP_PHASE(name)
+#endif
+template <int CTRL>
+__device__ __forceinline__ double swz_f64(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(u & 0xffffffffll), 0x8000 | CTRL);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(u >> 32), 0x8000 | CTRL);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL, bool SWZ>
+__device__ __forceinline__ double pr_xchg(double v) {
+    if constexpr (SWZ) return swz_f64<CTRL>(v);
+    return dpp_f64<CTRL>(v);
+}
+__device__ __forceinline__ double pr_swap(double v) { return pr_xchg<0xB1, (NNGP_PAIRB_SWZ & 1) != 0>(v); }   // partner lane's v
+__device__ __forceinline__ double pr_from0(double v) { return pr_xchg<0xA0, (NNGP_PAIRB_SWZ & 2) != 0>(v); }  // lane 0's v
+__device__ __forceinline__ double pr_from1(double v) { return pr_xchg<0xF5, (NNGP_PAIRB_SWZ & 2) != 0>(v); }  // lane 1's v
 __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return q1 ? v1 : v0; }
+// the same select as a bit-field insert under an opaque lane mask: a plain select of two entries
+// of one register array becomes an array access at a lane-dependent index, which LLVM lowers
+// to a compare / select chain over the whole array
+__device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) {
+    const long long a = __double_as_longlong(v1), b = __double_as_longlong(v0);
+    const uint32_t lo = ((uint32_t)a & mask1) | ((uint32_t)b & ~mask1);
+    const uint32_t hi = ((uint32_t)(a >> 32) & mask1) | ((uint32_t)(b >> 32) & ~mask1);
+    return __hiloint2double((int)hi, (int)lo);
+}
 
 // Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
 // (<= 256 VGPRs): m = 16 / 17 fit in 246 / 250 VGPRs without spills; m = 18 / 19 spill 27 / 23
@@ -136,6 +184,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
+    constexpr bool NOZ = NNGP_PAIRB_NOZ && M != 19;
     __shared__ double etab[NNGP_EXP_TAB_N];
     static_assert(NNGP_EXP_TAB_N == 256, "one table entry per thread of the 256-thread block");
     const double etab_entry = nngp_exp_table_fetch_unit();  // issued before the gathers
@@ -145,6 +194,9 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
     const int q = (int)(threadIdx.x & 1);
     const bool q1 = q == 1;
     const bool lead0 = !q1;
+    const double wq1 = q1 ? 1.0 : 0.0, wq0 = 1.0 - wq1;
+    uint32_t mask1 = q1 ? 0xffffffffu : 0u;
+    asm volatile("" : "+v"(mask1));  // opaque to the optimizer (see pr_pick)
     {
         const int64_t r = tile * kPairbTile + (threadIdx.x >> 1);
         const bool live = r < n_rows;
@@ -163,7 +215,6 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
         }
         double o[NP][D], z[NP];
-        uint32_t oval = 0;
         bool bad_index = false;
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
@@ -171,7 +222,6 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             const int32_t j = a < M ? jn[s] : -1;
             const bool in_range = j >= 0 && (int64_t)j < n_points;
             bad_index |= j >= 0 && !in_range;
-            oval |= in_range ? (1u << s) : 0u;
             const bool self = a == M;
             const double* pc = self ? qcoords + i * D : (in_range ? coords + (int64_t)j * D : far_point<D>(a));
             const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
@@ -184,6 +234,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
         // the barrier overlap the gathers' latency instead of preceding it
         nngp_exp_table_store_unit(etab, etab_entry);
 
+        NNGP_PHASE(covariances);
         // ---- unit-variance covariances in own-parity-first order
         double R[NP][NP][2];
         {
@@ -200,8 +251,27 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
                     R[s][t][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s], p[t]));
                 }
                 R[s][s][0] = Pc.diag;
-                const double c = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s], p[s]));
-                R[s][s][1] = q1 ? c : 0.0;
+            }
+            // the within-pair entries (2s+1, 2s) are read from lane 1 only (lane 0's R[s][s][1] is
+            // never used): of each two pairs, lane 0 evaluates the first and lane 1 the second, and
+            // lane 0's value moves to lane 1 -- half the evaluations of one per pair in both lanes
+#pragma unroll
+            for (int s0 = 0; s0 < NP; s0 += 2) {
+                const int s1 = s0 + 1;
+                if (M <= NNGP_PAIRB_DEDUP_MAX && s1 < NP) {
+                    double a[D], b[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        a[k] = pr_pick(mask1, o[s1][k], o[s0][k]);
+                        b[k] = pr_pick(mask1, p[s1][k], p[s0][k]);
+                    }
+                    const double c = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(a, b));
+                    R[s1][s1][1] = c;
+                    R[s0][s0][1] = pr_from0(c);
+                } else {
+                    R[s0][s0][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s0], p[s0]));
+                    if (s1 < NP) R[s1][s1][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s1], p[s1]));
+                }
             }
         }
 
@@ -209,6 +279,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
         // After block step t: lane q's R[t][t][0] = 1 / L[2t+q][2t+q], R[t][t][1] = L[2t+1][2t]
         // (both lanes), rows s > t hold their panel entries (L[a][2t+q], L[a][2t+1-q]) and z[t]
         // the forward-solved value of row 2t+q.
+        NNGP_PHASE(elimination);
         bool bad = false;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
@@ -221,17 +292,23 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             const double s11 = fma(-l10, l10, a11);
             bad |= !(s11 > 0.0);
             const double i11 = nngp_rsqrt(s11);
-            const double w0 = pr_from0(z[t]) * i00;
-            const double w1 = fma(-l10, w0, pr_from1(z[t])) * i11;
             R[t][t][0] = pr_sel(q1, i11, i00);
             R[t][t][1] = l10;
-            z[t] = pr_sel(q1, w1, w0);
+            double wS = 0.0, wO = 0.0;
+            if constexpr (!NOZ) {
+                const double w0 = pr_from0(z[t]) * i00;
+                const double w1 = fma(-l10, w0, pr_from1(z[t])) * i11;
+                z[t] = pr_sel(q1, w1, w0);
+                wS = pr_sel(q1, w1, w0);
+                wO = pr_sel(q1, w0, w1);
+            }
             // panel map (L[a][2t], L[a][2t+1]) = (A[a][2t], A[a][2t+1]) U, U = [[i00, u01], [0, i11]],
             // written in own-parity-first coordinates: Y0 = X0 c00 + X1 c10, Y1 = X0 c01 + X1 c11
             const double u01 = -(l10 * i00) * i11;
-            const double c00 = pr_sel(q1, i11, i00), c10 = pr_sel(q1, u01, 0.0);
-            const double c01 = pr_sel(q1, 0.0, u01), c11 = pr_sel(q1, i00, i11);
-            const double wS = pr_sel(q1, w1, w0), wO = pr_sel(q1, w0, w1);
+            // c10 / c01 = u01 in one lane, 0 in the other: one multiply by the lane's 0/1 weight each
+            // instead of a two-dword select
+            const double c00 = pr_sel(q1, i11, i00), c10 = u01 * wq1;
+            const double c01 = u01 * wq0, c11 = pr_sel(q1, i00, i11);
 #pragma unroll
             for (int s = t + 1; s < NP; ++s) {
                 const double x0 = R[s][t][0], x1 = R[s][t][1];
@@ -239,7 +316,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
                 const double y1 = fma(x0, c01, x1 * c11);
                 R[s][t][0] = y0;
                 R[s][t][1] = y1;
-                z[s] = fma(-y0, wS, fma(-y1, wO, z[s]));
+                if constexpr (!NOZ) z[s] = fma(-y0, wS, fma(-y1, wO, z[s]));
             }
             // trailing update: same-parity slots read this lane's panel, other-parity slots the swapped one
 #pragma unroll
@@ -255,6 +332,7 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             }
         }
 
+        NNGP_PHASE(lastpair);
         // ---- last pair: (M-1, M) for odd M (one more column), (M, padding) for even M
         double Fu, res;
         if (M % 2 == 1) {
@@ -265,22 +343,22 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
             const double i00 = nngp_rsqrt(a00);
             const double l10 = a10 * i00;
             Fu = fma(-l10, l10, a11);
-            const double w0 = pr_from0(z[T]) * i00;
-            res = fma(-l10, w0, pr_from1(z[T]));
+            if constexpr (!NOZ) res = fma(-l10, pr_from0(z[T]) * i00, pr_from1(z[T]));
             R[T][T][0] = i00;  // lane 0: 1 / L[M-1][M-1]
             R[T][T][1] = l10;  // L[M][M-1]
         } else {
             Fu = pr_from0(R[T][T][0]);
-            res = pr_from0(z[T]);
+            if constexpr (!NOZ) res = pr_from0(z[T]);
         }
         bad |= !(Fu > 0.0);
         const double F = Fu * sigma2;  // the unit-variance pivot scaled back
 
-        if (Bout != nullptr) {
+        if (NOZ || Bout != nullptr) {
             // B = L_N^{-T} v, v = row M of L (lane M % 2, local row M / 2).  Lane q ends with
             // bown[s] = B_{2s+q}.
             constexpr int SM = M / 2;
             constexpr bool VQ1 = (M % 2) == 1;  // row M sits in lane 1
+            NNGP_PHASE(backsub);
             double bown[NP];
 #pragma unroll
             for (int s = 0; s < NP; ++s) bown[s] = 0.0;
@@ -314,14 +392,32 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
                 const double b0 = fma(-(l10 * iown), b1, bx);  // lane 0: B_{2t}
                 bown[t] = pr_sel(q1, bx, b0);
             }
-            if (live) {
+            NNGP_PHASE(residual);
+            if constexpr (NOZ) {
+                // r = v_i - B v_N (as the oracle states it): this lane's rows a = 2s + q < M, then the pair
+                double acc = 0.0;
+#pragma unroll
+                for (int s = 0; s < NP; ++s) {
+                    if (2 * s >= M) continue;
+                    double bs = bown[s];
+                    if (2 * s + 1 >= M) bs = q1 ? 0.0 : bs;  // lane 1's row here is row M (or padding)
+                    acc = fma(bs, z[s], acc);
+                }
+                const double vi = VQ1 ? pr_from1(z[SM]) : pr_from0(z[SM]);
+                res = vi - (acc + pr_swap(acc));
+            }
+            NNGP_PHASE(stores);
+            if (Bout != nullptr && live) {
+                // padded slots hold exact zeros (far-away points decouple exactly, nngp_math.h)
+                const double bscale = bad ? NAN : 1.0;
 #pragma unroll
                 for (int s = 0; s < NP; ++s) {
                     const int a = 2 * s + q;
-                    if (a < M) Bout[rr * M + a] = bad ? NAN : (((oval >> s) & 1u) ? bown[s] : 0.0);
+                    if (a < M) Bout[rr * M + a] = bown[s] * bscale;
                 }
             }
         }
+        NNGP_PHASE(tail);
         const bool lead = live && lead0;
         if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
         if (Rout != nullptr && lead) Rout[rr] = bad ? NAN : res;

@@ -187,15 +187,21 @@ NNGP_FN double nngp_d2(double ax, double ay, double bx, double by) {
 // the exponent field instead of an ldexp: the LDS table stores 2^(j/256) with (j << 12)
 // pre-subtracted from its high dword, and for k = 256 n + j the high dword of
 // 2^(j/256) 2^n is (stored high dword) + (k << 12) -- one v_lshl_add_u32 instead of an
-// ashr + v_ldexp_f64.  The exponent argument is clamped so that n >= -1021 (results stay
-// normal): a covariance never falls below 2^-1021 (= 0 for every purpose of the
-// factorisation; far-away padding points decouple to within 4.5e-308).
+// ashr + v_ldexp_f64.  The exponent argument is clamped so that n >= -1023 (below).
+//
+// The clamp sits at k = -261888.25 (rounded: -1023 * 256, table entry j = 0): there the high
+// dword is exactly 0 and the covariance is +0.0, so far-away padding points decouple EXACTLY
+// (their rows and columns stay 0 through the elimination and B is 0 in padded slots without a
+// mask; the 1/4 margin absorbs the rounding of phi, d2max and the square root).  Between
+// k = -261887 and -261633 (n = -1023) the exponent field is 0 and the entry reads as a subnormal
+// below 2^-1022 -- a covariance that small is 0 for every purpose of the factorisation.
+#define NNGP_UNIT_CLAMP (1023.0 + 1.0 / 1024.0)
 NNGP_HD CovParams nngp_cov_params_unit(int kind, double phi, double tau2_over_sigma2) {
     CovParams p = nngp_cov_params(kind, 1.0, phi, tau2_over_sigma2);
     if (kind == NNGP_KIND_GAUSSIAN) {
-        p.d2max = 1021.0 / (phi * phi * NNGP_LOG2E);
+        p.d2max = NNGP_UNIT_CLAMP / (phi * phi * NNGP_LOG2E);
     } else if (kind != NNGP_KIND_SPHERICAL) {
-        const double dmax = 1021.0 / (phi * NNGP_LOG2E);
+        const double dmax = NNGP_UNIT_CLAMP / (phi * NNGP_LOG2E);
         p.d2max = dmax * dmax;
     }
     return p;

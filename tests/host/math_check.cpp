@@ -42,11 +42,19 @@ static double cov_any(int kind, bool unit, const CovParams& P, const double* tab
 }
 
 // unit-variance covariance: exactly 1 at coincident points; far-away padding points decouple
-// (below 1e-300 for the exponential kinds -- the clamped exponent keeps them normal, and the
-// Matern polynomials multiply 2^-1021 by <= 2e5 -- and exactly 0 for the spherical kind)
+// exactly (the clamp lands on a zero high dword, nngp_math.h), and every distance near the
+// clamp (exponent below -1022) gives a finite value in [0, 1e-300] (<= 2^-1022 times the
+// Matern polynomial), exactly 0 beyond it
 static int unit_special(int kind, const CovParams& P, const double* tab, double same, double far) {
     const double c0 = cov_any(kind, true, P, tab, same), cf = cov_any(kind, true, P, tab, far);
-    return c0 == 1.0 && cf >= 0.0 && cf <= 1e-300;
+    int ok = c0 == 1.0 && cf == 0.0;
+    const double d2a = P.d2max * 0.999, d2b = P.d2max * 1.02;
+    for (int i = 0; i <= 4000; ++i) {
+        const double d2 = d2a + (d2b - d2a) * i / 4000.0;
+        const double c = cov_any(kind, true, P, tab, d2);
+        ok = ok && c >= 0.0 && c <= 1e-300 && (d2 < P.d2max || c == 0.0);
+    }
+    return ok;
 }
 
 int main() {

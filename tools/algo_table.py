@@ -20,6 +20,7 @@ ap.add_argument("--n", type=int, default=1_000_000)
 ap.add_argument("--ms", default="1-20")
 ap.add_argument("--kind", default="exponential")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--algos", default=None, help="comma-separated subset of kernels to time (default: every one)")
 ap.add_argument("--rounds", type=int, default=6)
 ap.add_argument("--settle-ms", type=float, default=80.0,
                 help="back-to-back sweeps before each m's timing (the GPU clock settles over ~50 ms)")
@@ -41,6 +42,8 @@ for m in range(lo, hi + 1):
     algos += ["quad"] if m in (15, 16, 20) or 25 <= m <= 32 else []
     algos += ["pairb"] if 1 <= m <= 24 else []
     algos += ["wave"]
+    if args.algos:
+        algos = [a for a in algos if a in args.algos.split(",")]
     wss = {a: _lib.bf_workspace(args.n, m, a, dev) for a in algos}
 
     def run(algo):

@@ -9,7 +9,7 @@ mkdir -p gpurun_out/ab
 for rep in $(seq 1 ${REPS:-2}); do
   for v in $VARIANTS; do
     label=${v%%:*}; rest=${v#*:}; lib=${rest%%:*}; algo=${rest#*:}
-    NNGP_LIB=$lib timeout -k 10 120 python bench.py --steps 30 --warmup 5 --cpu-seconds 0 --algo $algo "$@" \
+    NNGP_LIB=$lib timeout -k 10 120 python bench.py --steps ${STEPS:-30} --warmup ${WARMUP:-5} --cpu-seconds 0 --algo $algo "$@" \
       > gpurun_out/ab/$label.$rep.json 2>> gpurun_out/ab/err.log || exit $?
     python3 -c "import json; d=json.load(open('gpurun_out/ab/$label.$rep.json')); print('$label', $rep, round(d['roofline']['kernel_ms'],4), 'ms', round(d['value']/1e9,3), 'Gloc/s')"
   done
