@@ -66,6 +66,10 @@ namespace nngp {
 #ifndef NNGP_PAIRB_NOZ
 #define NNGP_PAIRB_NOZ 1
 #endif
+// (A 2x2-block LDL^T -- one reciprocal of det D_t per block step instead of two pivot square
+// roots, -4.3 % VALU -- was measured and rejected: L = X D_t^{-1} multiplies by entries ~1/delta
+// for a nearly singular pair block where the Cholesky factor's are ~1/sqrt(delta), and F lost
+// accuracy: 2e-9 relative vs the oracle at Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
 #define NNGP_PHASE(name)                        \

@@ -198,21 +198,44 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
 // log(prod_t m_t) + (sum_t e_t) ln 2: the mantissas are multiplied (renormalised by frexp
 // after every product, exponents summed exactly as integers) and ONE log is taken at the
 // end -- a log per record made the single-block fold 10 us at 7,813 records.
-__device__ __forceinline__ void mant_mul(double& m, long long& e, double x) {
-    m *= x;
-    e += __builtin_amdgcn_frexp_exp(m);
+// Row reduction (16 lanes) by four DPP steps -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror -- after which every lane of a row holds the row's result (each step combines
+// a lane with one partner, a op b == b op a, so all 16 lanes agree bit for bit); the four
+// row results are then read from lanes 0, 16, 32, 48 and combined in that order.  DPP
+// moves take a few cycles where a ds_bpermute butterfly step waits on the LDS pipe.
+template <int OP>  // 0: sum, 1: product, 2: min
+__device__ __forceinline__ double fold_op(double a, double b) {
+    return OP == 0 ? a + b : OP == 1 ? a * b : fmin(a, b);
+}
+template <int OP>
+__device__ __forceinline__ double wave_fold_dpp(double v) {
+    v = fold_op<OP>(v, dpp_f64<0xB1>(v));
+    v = fold_op<OP>(v, dpp_f64<0x4E>(v));
+    v = fold_op<OP>(v, dpp_f64<0x141>(v));
+    v = fold_op<OP>(v, dpp_f64<0x140>(v));
+    const long long u = __double_as_longlong(v);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r[k] = __hiloint2double(__builtin_amdgcn_readlane((int)(u >> 32), 16 * k),
+                                __builtin_amdgcn_readlane((int)(u & 0xffffffffll), 16 * k));
+    return fold_op<OP>(fold_op<OP>(r[0], r[1]), fold_op<OP>(r[2], r[3]));
+}
+
+// m in [1/2, 1) and its exponent moved into e (exact: e holds integers far below 2^53)
+__device__ __forceinline__ void mant_norm(double& m, double& e) {
+    e += (double)__builtin_amdgcn_frexp_exp(m);
     m = __builtin_amdgcn_frexp_mant(m);
 }
 
 __global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restrict__ rec,
                                                           const int32_t* __restrict__ lexp, int64_t n_tiles,
                                                           double* __restrict__ partials) {
-    __shared__ double sh[16][4];
-    __shared__ long long she[16];
+    __shared__ double sh[16][5];
     const int t = threadIdx.x;
-    double a = 1.0, b = 0.0, c = INFINITY, d = INFINITY;  // a: mantissa product
-    long long e = 0;
-    // 8 records per thread in flight per round: 8,192 records (N ~ 10^6) in one memory round trip
+    double a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;  // a: mantissa product, e: exponent sum
+    // 8 records per thread in flight per round: 8,192 records (N ~ 10^6) in one memory round trip.
+    // A product of 8 mantissas in [1/2, 1) stays above 2^-8: one renormalisation per round.
     for (int64_t k0 = t; k0 < n_tiles; k0 += 8 * 1024) {
         double4 r[8];
         int32_t x[8];
@@ -222,51 +245,46 @@ __global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restr
             r[u] = k < n_tiles ? rec[k] : make_double4(1.0, 0.0, INFINITY, INFINITY);
             x[u] = k < n_tiles ? lexp[k] : 0;
         }
+        double pm = 1.0;
+        int32_t pe = 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            mant_mul(a, e, r[u].x);
+            pm *= r[u].x;
+            pe += x[u];
             b += r[u].y;
             c = fmin(c, r[u].z);
             d = fmin(d, r[u].w);
-            e += x[u];
         }
+        a *= pm;
+        e += (double)pe;
+        mant_norm(a, e);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ao = __shfl_xor(a, o);
-        e += __shfl_xor(e, o);
-        mant_mul(a, e, ao);
-    }
-    b = wave_sum(b);
-    c = wave_min(c);
-    d = wave_min(d);
+    // one wave: 64 mantissas in [1/2, 1) multiply to no less than 2^-64
+    a = wave_fold_dpp<1>(a);
+    e = wave_fold_dpp<0>(e);
+    mant_norm(a, e);
+    b = wave_fold_dpp<0>(b);
+    c = wave_fold_dpp<2>(c);
+    d = wave_fold_dpp<2>(d);
     if ((t & 63) == 0) {
         sh[t >> 6][0] = a;
-        sh[t >> 6][1] = b;
-        sh[t >> 6][2] = c;
-        sh[t >> 6][3] = d;
-        she[t >> 6] = e;
+        sh[t >> 6][1] = e;
+        sh[t >> 6][2] = b;
+        sh[t >> 6][3] = c;
+        sh[t >> 6][4] = d;
     }
     __syncthreads();
-    if (t < 64) {  // wave 0 folds the 16 wave results with a fixed butterfly
-        const bool h = t < 16;
-        a = h ? sh[t][0] : 1.0;
-        b = h ? sh[t][1] : 0.0;
-        c = h ? sh[t][2] : INFINITY;
-        d = h ? sh[t][3] : INFINITY;
-        e = h ? she[t] : 0;
+    if (t == 0) {  // the 16 wave results in wave order
+        a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            const double ao = __shfl_xor(a, o);
-            e += __shfl_xor(e, o);
-            mant_mul(a, e, ao);
-            b += __shfl_xor(b, o);
-            c = fmin(c, __shfl_xor(c, o));
-            d = fmin(d, __shfl_xor(d, o));
+        for (int w = 0; w < 16; ++w) {
+            a *= sh[w][0];
+            e += sh[w][1];
+            b += sh[w][2];
+            c = fmin(c, sh[w][3]);
+            d = fmin(d, sh[w][4]);
         }
-    }
-    if (t == 0) {
-        partials[0] = fma((double)e, 0.6931471805599453, log(a));
+        partials[0] = fma(e, 0.6931471805599453, log(a));
         partials[1] = b;
         partials[2] = c == INFINITY ? -1.0 : c;
         partials[3] = d == INFINITY ? -1.0 : d;
