@@ -105,3 +105,32 @@ def test_ops_reject_cpu_and_bad_buffers(ops, dev):
     with pytest.raises(RuntimeError, match="partials"):
         torch.ops.nngp.bf_sweep_out(c, nb, None, 0, 0, 1.0, 5.0, 0.1, None, None, None, None,
                                     torch.empty(3, dtype=torch.float64, device=dev), ws, 0)
+
+
+def test_bf_sweep_out_graph_replay_bit_identical(ops, dev):
+    """The bench's launch-bound mode (bench.py --graph): the sweep and its record fold captured
+    once in a hipGraph (torch.cuda.CUDAGraph) and replayed give the direct call's bits."""
+    from pynngp_amd.sweep import Covariance, ShardedLogLik
+
+    coords, y = _field(100_000, 2, 11)
+    c, v = torch.from_numpy(coords).to(dev), torch.from_numpy(y).to(dev)
+    sweep = ShardedLogLik(c, 15, 0, 1, layout="storage")
+    cov = Covariance("matern32", 1.0, 17.320508075688772, 0.1)
+    direct = sweep.local_partials(cov, v, True, "storage").clone()
+    B0, F0 = sweep.B.clone(), sweep.F.clone()
+    out = torch.empty(4, dtype=torch.float64, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        sweep.local_partials(cov, v, True, "storage", out=out)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sweep.local_partials(cov, v, True, "storage", out=out)
+    sweep.B.fill_(np.nan)
+    sweep.F.fill_(np.nan)
+    out.fill_(np.nan)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, direct) and torch.equal(sweep.B, B0) and torch.equal(sweep.F, F0)
