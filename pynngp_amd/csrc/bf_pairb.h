@@ -123,7 +123,15 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
     __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), \
                                        (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : 2))))
 
-constexpr int kPairbTile = 128;  // locations per 256-thread tile
+// Threads per block (one tile of kPairbThreads / 2 locations per block).  256 measured fastest:
+// 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
+// config 3 and +5 % / +1 % at config 2 (same-box A/B).
+#ifndef NNGP_PAIRB_THREADS
+#define NNGP_PAIRB_THREADS 256
+#endif
+constexpr int kPairbThreads = NNGP_PAIRB_THREADS;
+constexpr int kPairbWaves = kPairbThreads / 64;
+constexpr int kPairbTile = kPairbThreads / 2;  // locations per tile
 
 // Tile record fold: wave butterflies (fixed order), then the 4 waves in order by thread 0.
 // lm: product of the lanes' F mantissas (each in [0.5, 1); 128 of them stay above 2^-128),
@@ -131,7 +139,7 @@ constexpr int kPairbTile = 128;  // locations per 256-thread tile
 // bad-pivot row, first bad-index row), lexp[tile] = exponent sum.  sh[par] lets a
 // multi-tile caller double-buffer the exchange (one barrier per tile).
 __device__ __forceinline__ void pairb_tile_store(double lm, int le, double qq, double badp, double badi,
-                                                 double (*sh)[4][5], int par, double4* __restrict__ rec,
+                                                 double (*sh)[kPairbWaves][5], int par, double4* __restrict__ rec,
                                                  int32_t* __restrict__ lexp, int64_t tile) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -153,11 +161,11 @@ __device__ __forceinline__ void pairb_tile_store(double lm, int le, double qq, d
     }
 }
 
-__device__ __forceinline__ void pairb_tile_fold(double (*sh)[4][5], int par, double4* __restrict__ rec,
+__device__ __forceinline__ void pairb_tile_fold(double (*sh)[kPairbWaves][5], int par, double4* __restrict__ rec,
                                                 int32_t* __restrict__ lexp, int64_t tile) {
     double lm = 1.0, le = 0.0, qq = 0.0, bp = INFINITY, bi = INFINITY;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kPairbWaves; ++k) {
         lm *= sh[par][k][0];
         le += sh[par][k][1];
         qq += sh[par][k][2];
@@ -176,7 +184,7 @@ __device__ __forceinline__ double pr_rcp(double x) {
 }
 
 template <int M, int KIND, int D>
-__global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __restrict__ coords, int64_t n_points,
+__global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const double* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0, const CovParams Pc, double sigma2,
                                                 const double* __restrict__ values, const double* __restrict__ qcoords,
@@ -190,10 +198,16 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
     constexpr bool NOZ = NNGP_PAIRB_NOZ && M != 19;
     __shared__ double etab[NNGP_EXP_TAB_N];
-    static_assert(NNGP_EXP_TAB_N == 256, "one table entry per thread of the 256-thread block");
-    const double etab_entry = nngp_exp_table_fetch_unit();  // issued before the gathers
+    // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
+    // entry j - 256 and do not store it)
+    constexpr int kTabPer = kPairbThreads >= NNGP_EXP_TAB_N ? 1 : NNGP_EXP_TAB_N / kPairbThreads;
+    static_assert(kPairbThreads >= NNGP_EXP_TAB_N || kTabPer * kPairbThreads == NNGP_EXP_TAB_N, "table fill");
+    double etab_entry[kTabPer];
+#pragma unroll
+    for (int e = 0; e < kTabPer; ++e)
+        etab_entry[e] = nngp_exp_table_entry_unit(((int)threadIdx.x + e * kPairbThreads) & (NNGP_EXP_TAB_N - 1));
 
-    __shared__ double sh[1][4][5];
+    __shared__ double sh[1][kPairbWaves][5];
     const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
     const int q = (int)(threadIdx.x & 1);
     const bool q1 = q == 1;
@@ -236,7 +250,11 @@ __global__ __launch_bounds__(256) NNGP_PAIRB_ATTR void bf_pairb(const double* __
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
-        nngp_exp_table_store_unit(etab, etab_entry);
+#pragma unroll
+        for (int e = 0; e < kTabPer; ++e)
+            if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
+                etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
+        __syncthreads();
 
         NNGP_PHASE(covariances);
         // ---- unit-variance covariances in own-parity-first order
@@ -449,7 +467,7 @@ inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
 
 template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(256), 0, s, a.coords,
+    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), 0, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.sigma2, a.values, a.qcoords, a.qvalues, a.B,
                        a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows));
 }

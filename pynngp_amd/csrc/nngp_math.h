@@ -256,11 +256,11 @@ NNGP_FN double nngp_cov_unit(const CovParams& P, const double* tab, double d2) {
 // Split fill for a 256-thread block (one entry per thread): fetch the entry early, store it
 // (and synchronise) once other loads are in flight -- vmcnt retires loads in order, so the
 // store waits only for this load, not for loads issued after it.
-NNGP_FN double nngp_exp_table_fetch_unit() {
-    const int j = (int)threadIdx.x & (NNGP_EXP_TAB_N - 1);
+NNGP_FN double nngp_exp_table_entry_unit(int j) {
     const long long b = __double_as_longlong(kExp2Tab[j]);
     return __hiloint2double((int32_t)(b >> 32) - (j << 12), (int32_t)(b & 0xffffffffll));
 }
+NNGP_FN double nngp_exp_table_fetch_unit() { return nngp_exp_table_entry_unit((int)threadIdx.x & (NNGP_EXP_TAB_N - 1)); }
 NNGP_FN void nngp_exp_table_store_unit(double* tab, double v) {
     if (threadIdx.x < NNGP_EXP_TAB_N) tab[threadIdx.x] = v;
     __syncthreads();

@@ -1,0 +1,8 @@
+# A/B of variant libraries on one box (run via gpurun): parity tests of the variant, then
+# interleaved bench runs at the settled clock.  VARIANT=ab/<name>/libnngp_hip.so TAG=<tag>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/$TAG
+NNGP_LIB=$VARIANT timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_bf.py tests/test_gpu_fullsize.py tests/test_gpu_api.py > gpurun_out/$TAG/tests.txt 2>&1 || exit 1
+VARIANTS="cur:pynngp_amd/_build/libnngp_hip.so:auto var:$VARIANT:auto" REPS=${REPS:-4} STEPS=200 WARMUP=200 bash tools/gpu_ab.sh > gpurun_out/$TAG/ab.txt 2>&1 || exit 1
