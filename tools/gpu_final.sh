@@ -1,3 +1,6 @@
+# Final-build GPU check (run via gpurun): the GPU suite, smoke, the bench with the driver's
+# flags (twice) and its defaults, configs 2 and 4, and the rocprofv3 evidence of the default
+# bench (tools/profile.sh -> profiles/<TAG>).   TAG=<tag> bash tools/gpu_final.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
