@@ -70,6 +70,13 @@ namespace nngp {
 // roots, -4.3 % VALU -- was measured and rejected: L = X D_t^{-1} multiplies by entries ~1/delta
 // for a nearly singular pair block where the Cholesky factor's are ~1/sqrt(delta), and F lost
 // accuracy: 2e-9 relative vs the oracle at Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
+// NNGP_PAIRB_SLDL: scalar-pivot LDL^T in the 2x2-blocked layout (reciprocals, unit factor)
+// instead of the Cholesky factor (inverse square roots): -44 VALU per wave at m = 15 (-1.7 %),
+// -0.6 % time (same-box A/B), every GPU parity test unchanged.  Not at m = 19 (no value column
+// path there, NOZ).
+#ifndef NNGP_PAIRB_SLDL
+#define NNGP_PAIRB_SLDL 1
+#endif
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
 #define NNGP_PHASE(name)                        \
@@ -197,6 +204,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
     constexpr bool NOZ = NNGP_PAIRB_NOZ && M != 19;
+    constexpr bool SLDL = NNGP_PAIRB_SLDL && NOZ;
     __shared__ double etab[NNGP_EXP_TAB_N];
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)
@@ -303,6 +311,49 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         // the forward-solved value of row 2t+q.
         NNGP_PHASE(elimination);
         bool bad = false;
+        if constexpr (SLDL) {
+            // 2x2-blocked scalar-pivot LDL^T: per pair t the pivots d00 and e11 = d11 - l d10 (l =
+            // d10 / d00) need a reciprocal each instead of an inverse square root.  Each later row's
+            // panel X becomes W = X L_D^{-T} (its column 2t+1 loses l times column 2t) in place; in
+            // the update of row pair u the partner's side is Q_u = W_u diag(1/d00, 1/e11), which is
+            // also row u's entry of the unit factor and replaces W_u once pair u is done.  Like the
+            // Cholesky form the first column is one product and the second one subtraction away
+            // from X (no 2x2 inverse with 1/det entries, which lost accuracy: see the note above).
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const double d00 = pr_from0(R[t][t][0]);
+                const double d11 = pr_from1(R[t][t][0]);
+                const double d10 = pr_from1(R[t][t][1]);
+                bad |= !(d00 > 0.0);
+                const double r00 = pr_rcp(d00);
+                const double l10 = d10 * r00;
+                const double e11 = fma(-l10, d10, d11);
+                bad |= !(e11 > 0.0);
+                const double r11 = pr_rcp(e11);
+                R[t][t][1] = l10;  // L[2t+1][2t] of the unit factor
+                const double town = pr_sel(q1, r11, r00), toth = pr_sel(q1, r00, r11);
+                const double g1 = -l10 * wq1, g0 = -l10 * wq0;
+#pragma unroll
+                for (int s = t + 1; s < NP; ++s) {
+                    const double x0 = R[s][t][0], x1 = R[s][t][1];
+                    R[s][t][0] = fma(g1, x1, x0);
+                    R[s][t][1] = fma(g0, x0, x1);
+                }
+#pragma unroll
+                for (int u = t + 1; u < NP; ++u) {
+                    const double Q0 = R[u][t][0] * town, Q1 = R[u][t][1] * toth;
+                    const double P0 = pr_swap(Q0), P1 = pr_swap(Q1);
+#pragma unroll
+                    for (int s = u; s < NP; ++s) {
+                        const double w0 = R[s][t][0], w1 = R[s][t][1];
+                        R[s][u][0] = fma(-w0, Q0, fma(-w1, Q1, R[s][u][0]));
+                        R[s][u][1] = fma(-w0, P1, fma(-w1, P0, R[s][u][1]));
+                    }
+                    R[u][t][0] = Q0;
+                    R[u][t][1] = Q1;
+                }
+            }
+        } else {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             const double a00 = pr_from0(R[t][t][0]);
@@ -353,11 +404,21 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 }
             }
         }
+        }
 
         NNGP_PHASE(lastpair);
         // ---- last pair: (M-1, M) for odd M (one more column), (M, padding) for even M
         double Fu, res;
-        if (M % 2 == 1) {
+        if (M % 2 == 1 && SLDL) {
+            const double a00 = pr_from0(R[T][T][0]);
+            const double a11 = pr_from1(R[T][T][0]);
+            const double a10 = pr_from1(R[T][T][1]);
+            bad |= !(a00 > 0.0);
+            const double l10 = a10 * pr_rcp(a00);  // L[M][M-1] of the unit factor = B_{M-1}
+            Fu = fma(-l10, a10, a11);
+            R[T][T][0] = 1.0;
+            R[T][T][1] = l10;
+        } else if (M % 2 == 1) {
             const double a00 = pr_from0(R[T][T][0]);
             const double a11 = pr_from1(R[T][T][0]);
             const double a10 = pr_from1(R[T][T][1]);
@@ -407,11 +468,16 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 } else {
                     v = pr_sel(q1, pr_swap(vrow1), vrow0);
                 }
-                const double iown = R[t][t][0];
-                const double bx = (v - tot) * iown;      // lane 1: B_{2t+1}
-                const double b1 = pr_swap(bx);           // lane 0: B_{2t+1}
                 const double l10 = R[t][t][1];
-                const double b0 = fma(-(l10 * iown), b1, bx);  // lane 0: B_{2t}
+                double bx, b0;
+                if constexpr (SLDL) {  // unit factor: B_{2t+1} = v - tot, B_{2t} = v - tot - l10 B_{2t+1}
+                    bx = v - tot;
+                    b0 = fma(-l10, pr_swap(bx), bx);
+                } else {
+                    const double iown = R[t][t][0];
+                    bx = (v - tot) * iown;                     // lane 1: B_{2t+1}
+                    b0 = fma(-(l10 * iown), pr_swap(bx), bx);  // lane 0: B_{2t}
+                }
                 bown[t] = pr_sel(q1, bx, b0);
             }
             NNGP_PHASE(residual);
