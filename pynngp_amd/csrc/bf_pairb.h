@@ -149,7 +149,7 @@ __device__ __forceinline__ void pairb_tile_store(double lm, int le, double qq, d
                                                  double (*sh)[kPairbWaves][5], int par, double4* __restrict__ rec,
                                                  int32_t* __restrict__ lexp, int64_t tile) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = 32; o > 1; o >>= 1) {  // the terms sit in the even (lead) lanes: lane 0 needs no xor-1 step
         lm *= __shfl_xor(lm, o);
         le += __shfl_xor(le, o);
         qq += __shfl_xor(qq, o);
@@ -241,13 +241,16 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
         }
         double o[NP][D], z[NP];
-        bool bad_index = false;
+        // one unsigned compare per slot (a negative index is out of range as a huge unsigned);
+        // an index >= n_points anywhere in the row shows in the row's largest index
+        const uint32_t n32 = n_points < (int64_t)INT32_MAX ? (uint32_t)n_points : (uint32_t)INT32_MAX;
+        int32_t jmax = -1;
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
             const int a = 2 * s + q;
             const int32_t j = a < M ? jn[s] : -1;
-            const bool in_range = j >= 0 && (int64_t)j < n_points;
-            bad_index |= j >= 0 && !in_range;
+            jmax = max(jmax, j);
+            const bool in_range = (uint32_t)j < n32;
             const bool self = a == M;
             const double* pc = self ? qcoords + i * D : (in_range ? coords + (int64_t)j * D : far_point<D>(a));
             const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
@@ -255,6 +258,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             load_point<D>(pc, o[s]);
             z[s] = *pv;
         }
+        const bool bad_index = (int64_t)jmax >= n_points;
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
