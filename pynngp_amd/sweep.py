@@ -115,6 +115,9 @@ class ShardedLogLik:
                 self.order, self._nbr_sweep = _lib.row_order(coords, self.lo, self.hi - self.lo, self.nbr)
         if compute is None:
             ops.load()  # sweeps go through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
+            # the resolved overload: calling it skips the packet's overload resolution per sweep
+            # (host issue time is what bounds a sweep of ~10^5 rows)
+            self._sweep_op = torch.ops.nngp.bf_sweep_out.default
             self._algo_code = ops.algo_code(algo)
             self._ws = _lib.bf_workspace(self.hi - self.lo, self.m, algo, coords.device, dim=coords.shape[1])
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
@@ -140,9 +143,8 @@ class ShardedLogLik:
             _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, s2, phi, tau2, values=values,
                           want_bf=want_bf, algo=self.algo, B=B, F=F, partials=p, workspace=self._ws, order=self.order)
             return p
-        torch.ops.nngp.bf_sweep_out(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
-                                    float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws,
-                                    self._algo_code)
+        self._sweep_op(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
+                       float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws, self._algo_code)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
