@@ -183,11 +183,12 @@ __device__ __forceinline__ void pairb_tile_fold(double (*sh)[kPairbWaves][5], in
     lexp[tile] = (int32_t)le + __builtin_amdgcn_frexp_exp(lm);
 }
 
-// 1/x to ~1 ulp for a positive normal x: v_rcp_f64 (~2^-26) and two Newton steps
+// 1/x to ~1 ulp for a positive normal x: v_rcp_f64 (~2^-26) and one second-order correction
+// y (1 + e + e^2), e = 1 - x y (3 ops; the e^3 term is below 2^-78; two Newton steps are 4)
 __device__ __forceinline__ double pr_rcp(double x) {
-    double y = __builtin_amdgcn_rcp(x);
-    y = fma(fma(-x, y, 1.0), y, y);
-    return fma(fma(-x, y, 1.0), y, y);
+    const double y = __builtin_amdgcn_rcp(x);
+    const double e = fma(-x, y, 1.0);
+    return fma(y, fma(e, e, e), y);
 }
 
 template <int M, int KIND, int D>
