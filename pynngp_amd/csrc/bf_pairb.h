@@ -31,7 +31,10 @@
 //   * one partial record per 128-location tile: sum log F leaves the kernel as the
 //     tile's mantissa product and exponent sum (frexp), and the ~100-instruction log is
 //     taken once per record by the fold (bf_finalize_pairb), not per lane;
-//     r^2 / F through v_rcp_f64 + two Newton steps instead of the IEEE divide.
+//     r^2 / F through v_rcp_f64 + a refinement (pr_rcp) instead of the IEEE divide.
+//   Second pass: no value column (r = v_i - B v_N), within-pair covariances split across the
+//   pair, exact-zero far points, scalar-pivot LDL^T (reciprocal pivots, unit factor); see
+//   DESIGN.md 4.1 for each step's measured effect and the variants rejected.
 //   One block per tile, hardware-scheduled: persistent grids (static ranges, ranges with
 //   issue-priority balancing, tiles claimed from per-XCD counters) all measured slower
 //   (profiles/r02j, r02l, r02m).
