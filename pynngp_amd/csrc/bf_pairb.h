@@ -64,8 +64,9 @@ namespace nngp {
 #define NNGP_PAIRB_DEDUP_MAX 17
 #endif
 // NNGP_PAIRB_NOZ: no value column in the elimination; the residual is r = v_i - B v_N after
-// the back-substitution (B is then always computed): 5 % fewer VALU at m = 15.  Not at m = 19,
-// where it moved the register peak (100 -> 220 B of scratch, 0.394 -> 0.499 ms per 10^6 rows).
+// the back-substitution (B is then always computed): 5 % fewer VALU at m = 15.  Not at m = 19
+// with two waves per SIMD, where it moved the register peak (100 -> 220 B of scratch, 0.394 ->
+// 0.499 ms per 10^6 rows).
 #ifndef NNGP_PAIRB_NOZ
 #define NNGP_PAIRB_NOZ 1
 #endif
@@ -79,6 +80,10 @@ namespace nngp {
 // path there, NOZ).
 #ifndef NNGP_PAIRB_SLDL
 #define NNGP_PAIRB_SLDL 1
+#endif
+// ... except where the two-wave register budget is tight (m = 18: 80 -> 216 B of scratch)
+#ifndef NNGP_PAIRB_SLDL_MAX
+#define NNGP_PAIRB_SLDL_MAX 17
 #endif
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
@@ -116,12 +121,14 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 }
 
 // Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
-// (<= 256 VGPRs): m = 16 / 17 fit in 246 / 250 VGPRs without spills; m = 18 / 19 spill 27 / 23
-// dwords to scratch and still run 22 % faster than at one wave per SIMD (282 / 278 VGPRs;
-// same-box A/B, profiles/r02p).  From m = 20 (342 VGPRs) the forced spills (91 dwords) cost
-// more than the second wave gains (+52 % at m = 20, 2-3x at m = 22 / 24).
+// (<= 256 VGPRs): m = 16 / 17 fit without spills; m = 18 spills 20 dwords to scratch and still
+// runs ~30 % faster than at one wave per SIMD (0.314 vs 0.435 ms per 10^6 rows, profiles/r02ap);
+// m = 19 spilled 60 dwords in the final build and runs faster at one wave (0.476 vs 0.546 ms;
+// it was 23 dwords and 22 % faster at two waves in profiles/r02p).  From m = 20 (342 VGPRs) the
+// forced spills (91 dwords) cost more than the second wave gains (+52 % at m = 20, 2-3x at
+// m = 22 / 24).
 #ifndef NNGP_PAIRB_TWO_WAVES_MAX
-#define NNGP_PAIRB_TWO_WAVES_MAX 19
+#define NNGP_PAIRB_TWO_WAVES_MAX 18
 #endif
 // Three waves per SIMD (<= 168 VGPRs) up to m = NNGP_PAIRB_THREE_WAVES_MAX: m = 12 / 13 fit
 // in 162 / 164 VGPRs (-3.7 % cycles at m = 13); forced at m = 14 / 15 the 31 / 35 spilled
@@ -207,8 +214,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
-    constexpr bool NOZ = NNGP_PAIRB_NOZ && M != 19;
-    constexpr bool SLDL = NNGP_PAIRB_SLDL && NOZ;
+    constexpr bool NOZ = NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX);
+    constexpr bool SLDL = NNGP_PAIRB_SLDL && NOZ && (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
     __shared__ double etab[NNGP_EXP_TAB_N];
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)

@@ -28,17 +28,17 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order
-// (tools/algo_table.py, profiles/r02q/algo_table_m1_24.jsonl): for the
-// configurations' 2-D exponential / Matern-3/2 fields one lane per location while the joint
-// block still leaves room for latency hiding (m <= 9), the 2x2-blocked two-lane kernel for
-// 10 <= m <= 24, four lanes for 25..32, one wavefront per location above.  Other kinds and
-// dimensions are instantiated for the blocked pair kernel (m <= 24) and the wavefront kernel.
+// (tools/algo_table.py, profiles/r02ap/algo_lane_pairb_m1_24.jsonl): the
+// 2x2-blocked two-lane kernel for 1 <= m <= 24 (since its round-2 instruction cuts it ties the
+// one-lane kernel at m = 1, 2 and is faster from m = 3), four lanes for 25..32 on the
+// configurations' 2-D exponential / Matern-3/2 fields, one wavefront per location above.  Other
+// kinds and dimensions are instantiated for the blocked pair kernel (m <= 24) and the
+// wavefront kernel.
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     if (algo != NNGP_ALGO_AUTO) return algo;
     const bool classic = dim == 2 && (kind == NNGP_COV_EXPONENTIAL || kind == NNGP_COV_MATERN32);
     if (classic) {
-        if (m >= 1 && m <= 9) return nngp::kAlgoLane;
-        if (m >= 10 && m <= 24) return nngp::kAlgoPairB;
+        if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
         if (m >= 25 && m <= 32) return nngp::kAlgoQuad;  // ~10x bf_wave (tools/algo_table.py)
         return nngp::kAlgoWave;
     }
