@@ -47,12 +47,12 @@ extern "C" {
 
 /* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE, PAIR and
  * QUAD serve 2-D exponential / Matern-3/2 only, PAIRB and WAVE every kind and dimension */
-#define NNGP_ALGO_AUTO 0  /* 2-D exp / Matern-3/2: lane m <= 10, pairb 11..24, quad 25..32, wave; else pairb / wave */
+#define NNGP_ALGO_AUTO 0  /* pairb m <= 24; 2-D exp / Matern-3/2: quad 25..32; wave above                 */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
 #define NNGP_ALGO_PAIR 3  /* two lanes per location (10 <= m <= 20)                          */
 #define NNGP_ALGO_QUAD 4  /* four lanes per location (m in 15, 16, 20, 25..32)               */
-#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked, persistent (1 <= m <= 24) */
+#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 24)              */
 #define NNGP_ALGO_PAIRB_R1 7 /* the round-1 pair kernel (m = 15, exponential, 2-D): same-box A/B only */
 
 #define NNGP_MAX_M 63
