@@ -254,7 +254,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         double o[NP][D], z[NP];
         // one unsigned compare per slot (a negative index is out of range as a huge unsigned);
         // an index >= n_points anywhere in the row shows in the row's largest index
-        const uint32_t n32 = n_points < (int64_t)INT32_MAX ? (uint32_t)n_points : (uint32_t)INT32_MAX;
+        // (n_points >= 2^31: every non-negative int32 index is in range)
+        const uint32_t n32 = n_points < (int64_t)0x80000000ll ? (uint32_t)n_points : 0x80000000u;
         int32_t jmax = -1;
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
