@@ -249,6 +249,201 @@ int oracle_knn_prior_kdtree_rebuild(const double *coords, int64_t n, int32_t dim
     return 0;
 }
 
+/* ---------------------------------------------------------------------------
+ * An exact prior-kNN for large N that shares nothing with the GPU's grid search
+ * (pynngp_amd/csrc/knn.hip): kd-trees over DOUBLING PREFIXES s[0:2^k].  Query i
+ * searches the tree of the smallest prefix that holds s[0:i] (2^k >= i, so at least
+ * half of that tree's points are prior points) and skips every j >= i.  Same key as
+ * nngp.py:49-62 through sklearn (rdist unfused, ascending; ties by lower index, the
+ * documented divergence), same kd-tree code as the per-i rebuild above; the node-box
+ * bound prunes only with '>' so keys tied with the k-th are still visited.  The trees
+ * total ~2N points (O(N log N) to build instead of the reference's O(N^2 log N)), so
+ * every row of config 4 (N = 1e7, m = 20) is checkable in seconds.
+ * ------------------------------------------------------------------------- */
+static void kd_query_prior(const KdTree *t, int64_t id, const double *q, int64_t i, int64_t k, double *bd,
+                           int64_t *bi, int64_t *cnt) {
+    const KdNode *nd = &t->nodes[id];
+    if (*cnt == k && kd_min_rdist(t, id, q) > bd[k - 1]) return;
+    if (nd->left < 0) {
+        for (int64_t a = nd->start; a < nd->end; ++a) {
+            const int64_t j = t->idx[a];
+            if (j < i) kd_push(bd, bi, cnt, k, rdist(q, t->pts + j * t->dim, t->dim), j);
+        }
+        return;
+    }
+    const double dl = kd_min_rdist(t, nd->left, q), dr = kd_min_rdist(t, nd->right, q);
+    const int64_t first = dl <= dr ? nd->left : nd->right, second = dl <= dr ? nd->right : nd->left;
+    kd_query_prior(t, first, q, i, k, bd, bi, cnt);
+    kd_query_prior(t, second, q, i, k, bd, bi, cnt);
+}
+
+static int kd_alloc(KdTree *t, const double *pts, int dim, int64_t size) {
+    const int64_t nn = 2 * size / 20 + 8;
+    t->pts = pts;
+    t->dim = dim;
+    t->n_nodes = 0;
+    t->idx = (int64_t *)malloc(sizeof(int64_t) * (size_t)(size > 0 ? size : 1));
+    t->nodes = (KdNode *)malloc(sizeof(KdNode) * (size_t)nn);
+    t->lo = (double *)malloc(sizeof(double) * (size_t)dim * (size_t)nn);
+    t->hi = (double *)malloc(sizeof(double) * (size_t)dim * (size_t)nn);
+    return t->idx && t->nodes && t->lo && t->hi;
+}
+
+static void kd_free(KdTree *t) {
+    free(t->idx);
+    free(t->nodes);
+    free(t->lo);
+    free(t->hi);
+}
+
+static int64_t kd_size(int k, int64_t n) { return ((int64_t)1 << k) > n ? n : ((int64_t)1 << k); }
+
+/* smallest k with 2^k >= i (i >= 1) */
+static int ceil_log2(int64_t i) {
+    int k = 0;
+    while (((int64_t)1 << k) < i) ++k;
+    return k;
+}
+
+/* nodes of the kd_build subtree over `size` points (sizes at one depth are floor / ceil of
+ * one value, so the pair (c(a), c(a+1)) recurses on a / 2 alone) */
+static void kd_count_pair(int64_t a, int64_t *ca, int64_t *ca1) {
+    if (a + 1 <= 40) {
+        *ca = 1;
+        *ca1 = 1;
+        return;
+    }
+    if (a <= 40) { /* a = 40: c(41) = 1 + c(20) + c(21) */
+        *ca = 1;
+        *ca1 = 3;
+        return;
+    }
+    int64_t ch, ch1;
+    kd_count_pair(a / 2, &ch, &ch1);
+    if (a % 2 == 0) {
+        *ca = 1 + 2 * ch;
+        *ca1 = 1 + ch + ch1;
+    } else {
+        *ca = 1 + ch + ch1;
+        *ca1 = 1 + 2 * ch1;
+    }
+}
+
+static int64_t kd_count(int64_t size) {
+    int64_t c, c1;
+    kd_count_pair(size, &c, &c1);
+    return c;
+}
+
+/* kd_build with the same tree and node numbering (pre-order: left child id + 1, right child
+ * id + 1 + nodes of the left subtree), subtrees of large nodes built as OpenMP tasks */
+static void kd_build_at(KdTree *t, int64_t id, int64_t start, int64_t end) {
+    KdNode *nd = &t->nodes[id];
+    nd->start = start;
+    nd->end = end;
+    nd->left = nd->right = -1;
+    double *lo = t->lo + id * t->dim, *hi = t->hi + id * t->dim;
+    for (int k = 0; k < t->dim; ++k) {
+        lo[k] = INFINITY;
+        hi[k] = -INFINITY;
+    }
+    for (int64_t a = start; a < end; ++a)
+        for (int k = 0; k < t->dim; ++k) {
+            const double v = t->pts[t->idx[a] * t->dim + k];
+            if (v < lo[k]) lo[k] = v;
+            if (v > hi[k]) hi[k] = v;
+        }
+    if (end - start <= 40) return;
+    int ks = 0;
+    for (int k = 1; k < t->dim; ++k)
+        if (hi[k] - lo[k] > hi[ks] - lo[ks]) ks = k;
+    const int64_t mid = start + (end - start) / 2;
+    kd_select(t->pts, t->dim, ks, t->idx, start, end, mid);
+    const int64_t l = id + 1, r = id + 1 + kd_count(mid - start);
+    nd->left = l;
+    nd->right = r;
+    if (end - start > 65536) {
+#pragma omp task
+        kd_build_at(t, l, start, mid);
+#pragma omp task
+        kd_build_at(t, r, mid, end);
+#pragma omp taskwait
+    } else {
+        kd_build_at(t, l, start, mid);
+        kd_build_at(t, r, mid, end);
+    }
+}
+
+static void knn_prior_row(const KdTree *t, const double *coords, int dim, int64_t i, int32_t m, double *bd,
+                          int64_t *bi, int32_t *row) {
+    const int64_t k = i < m ? i : m;
+    int64_t cnt = 0;
+    kd_query_prior(t, 0, coords + i * dim, i, k, bd, bi, &cnt);
+    for (int64_t s = 0; s < m; ++s) row[s] = s < cnt ? (int32_t)bi[s] : -1;
+}
+
+int oracle_knn_prior_prefix_kdtree(const double *coords, int64_t n, int32_t dim, int32_t m, int64_t q0, int64_t q1,
+                                   int32_t *nbr) {
+    if (m < 0 || dim < 1 || q0 < 0 || q1 > n || q0 > q1) return -1;
+    if (m == 0 || q1 == q0) return 0;
+    const int64_t first = q0 > 1 ? q0 : 1; /* row 0 has no prior point */
+    const int klo = ceil_log2(first), khi = q1 - 1 >= first ? ceil_log2(q1 - 1) : klo;
+    const int nlev = khi - klo + 1;
+    KdTree *trees = (KdTree *)calloc((size_t)nlev, sizeof(KdTree));
+    if (trees == NULL) return -2;
+    int rc = 0;
+    for (int l = 0; l < nlev; ++l) {
+        if (!kd_alloc(&trees[l], coords, dim, kd_size(klo + l, n))) rc = 1;
+    }
+    /* one task tree per prefix, the large nodes' subtrees as tasks of their own */
+#pragma omp parallel
+#pragma omp single
+    for (int l = nlev - 1; l >= 0 && rc == 0; --l) {
+#pragma omp task firstprivate(l)
+        {
+            KdTree *t = &trees[l];
+            const int64_t size = kd_size(klo + l, n);
+            for (int64_t a = 0; a < size; ++a) t->idx[a] = a;
+            kd_build_at(t, 0, 0, size);
+            t->n_nodes = kd_count(size);
+        }
+    }
+    if (rc == 0) {
+#pragma omp parallel
+        {
+            double *bd = (double *)malloc(sizeof(double) * (size_t)m);
+            int64_t *bi = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+            /* query i (not a power of two) is a point of the tree it searches: visiting the
+             * queries in that tree's leaf order (spatial order) keeps consecutive queries on the
+             * same paths and leaves.  i = 2^k searches tree k without being one of its points,
+             * and row 0 has no prior point: both are done on their own. */
+            for (int l = 0; l < nlev; ++l) {
+                const KdTree *t = &trees[l];
+                const int64_t size = kd_size(klo + l, n);
+#pragma omp for schedule(dynamic, 256) nowait
+                for (int64_t a = 0; a < size; ++a) {
+                    const int64_t i = t->idx[a];
+                    if (i < q0 || i >= q1 || i < 1 || (i & (i - 1)) == 0 || ceil_log2(i) != klo + l) continue;
+                    knn_prior_row(t, coords, dim, i, m, bd, bi, nbr + (i - q0) * m);
+                }
+            }
+#pragma omp for schedule(dynamic, 1)
+            for (int k = 0; k < 63; ++k) {
+                const int64_t i = (int64_t)1 << k;
+                if (i >= q0 && i < q1) knn_prior_row(&trees[k - klo], coords, dim, i, m, bd, bi, nbr + (i - q0) * m);
+            }
+#pragma omp single
+            if (q0 == 0)
+                for (int64_t s = 0; s < m; ++s) nbr[s] = -1;
+            free(bd);
+            free(bi);
+        }
+    }
+    for (int l = 0; l < nlev; ++l) kd_free(&trees[l]);
+    free(trees);
+    return rc ? -2 : 0;
+}
+
 static inline double cov_eval(int kind, double d, double sigma2, double phi) {
     const double u = phi * d;
     switch (kind) {

@@ -259,6 +259,8 @@ def load_c_oracle():
     lib.oracle_knn_prior_rows.restype = ctypes.c_int
     lib.oracle_knn_prior_kdtree_rebuild.argtypes = [P, I64, I32, I32, I64, I64, P]
     lib.oracle_knn_prior_kdtree_rebuild.restype = ctypes.c_int
+    lib.oracle_knn_prior_prefix_kdtree.argtypes = [P, I64, I32, I32, I64, I64, P]
+    lib.oracle_knn_prior_prefix_kdtree.restype = ctypes.c_int
     lib.oracle_bf_sweep.argtypes = [P, P, I64, I32, I32, I32, P, P, P, P, P, I64, I64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
     lib.oracle_num_threads.restype = ctypes.c_int
@@ -301,6 +303,22 @@ def c_knn_prior_kdtree_rebuild(coords, m, q0=0, q1=None):
     rc = lib.oracle_knn_prior_kdtree_rebuild(_ptr(coords), n, _dim(coords), m, q0, q1, _ptr(out))
     if rc != 0:
         raise RuntimeError(f"oracle_knn_prior_kdtree_rebuild failed: {rc}")
+    return out
+
+
+def c_knn_prior_prefix_kdtree(coords, m, q0=0, q1=None):
+    """Exact prior sets through kd-trees over doubling prefixes s[0:2^k] (query i searches the
+    smallest prefix holding s[0:i] and skips j >= i), OpenMP over queries: an independent
+    check of the GPU grid search that is fast enough for every row at N = 1e7.  Same output
+    as c_knn_prior (nngp.py:49-62 key; ties by lower index)."""
+    lib = load_c_oracle()
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    n = coords.shape[0]
+    q1 = n if q1 is None else q1
+    out = np.full((q1 - q0, m), -1, dtype=np.int32)
+    rc = lib.oracle_knn_prior_prefix_kdtree(_ptr(coords), n, _dim(coords), m, q0, q1, _ptr(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle_knn_prior_prefix_kdtree failed: {rc}")
     return out
 
 

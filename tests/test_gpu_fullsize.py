@@ -6,9 +6,11 @@ Configs (BASELINE.json "configs", SURVEY.md 8(d) inputs):
   4: N = 1e7, m = 20, exponential (phi = 30), tau2 = 0, seed 1   (8 shards at N = 1e7)
 For each: the GPU neighbour sets against the C oracle's brute force
 (oracle/nngp_oracle.c: nngp.py:49-62 restated, sklearn's unfused rdist, ties by
-lower index) -- every row at configs 2 and 3, >= 12,000 rows at config 4 (the first
-and last 1,000 plus 10,000 random ones; all 1e7 rows would take ~1 h of brute
-force) -- then B and F of EVERY row and the whole-field log-likelihood against the
+lower index) -- every row at configs 2 and 3; at config 4 EVERY row against the
+independent doubling-prefix kd-tree search (oracle_knn_prior_prefix_kdtree: trees over
+s[0:2^k], pinned to the brute force in tests/test_oracle.py; ~6 s on 16 threads where the
+brute force would take ~1 h) plus 12,000 rows against the brute force itself -- then B and
+F of EVERY row and the whole-field log-likelihood against the
 C oracle's sweep on the GPU's neighbour sets.  Config 3 also runs through the
 benchmark's own path (ShardedLogLik, Z-order storage layout) and config 4 through its
 8-shard decomposition.  Tolerances as tests/test_gpu_bf.py:
@@ -115,8 +117,8 @@ def test_config3_bench_path_all_rows(lib, dev, c_oracle):
 
 
 def test_config4_rows_and_shards(lib, dev, c_oracle):
-    """N = 1e7, m = 20: >= 12,000 neighbour rows bit-exact vs brute force; B / F of every
-    row and the log-likelihood vs the oracle; the 8-shard storage decomposition's
+    """N = 1e7, m = 20: every neighbour row bit-exact vs the prefix kd-tree search and 12,000
+    rows vs the brute force; B / F of every row and the log-likelihood vs the oracle; the 8-shard storage decomposition's
     rank-order sum equals the oracle's log-likelihood too."""
     from pynngp_amd import Covariance, ShardedLogLik
 
@@ -130,6 +132,9 @@ def test_config4_rows_and_shards(lib, dev, c_oracle):
     rng = np.random.default_rng(44)
     rows = np.unique(np.concatenate([np.arange(1000), n - 1000 + np.arange(1000), rng.integers(0, n, 10_000)]))
     np.testing.assert_array_equal(nbr[rows], c_oracle.c_knn_prior_rows(coords, m, rows))
+    kd = c_oracle.c_knn_prior_prefix_kdtree(coords, m)
+    np.testing.assert_array_equal(nbr, kd)  # all 1e7 rows
+    del kd
     B, F, p = lib.bf_sweep(c, nb, 0, kind, *theta, values=v)
     Bo, Fo, po = c_oracle.c_bf_sweep(coords, nbr, kind, theta, y)
     llo = c_oracle.loglik_from_partials(po, n)
