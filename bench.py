@@ -176,7 +176,7 @@ def main():
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=list(_lib.KIND_CODES))
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
-    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "pair", "quad", "pairb", "pairb_r1"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "quad", "pairb"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
     ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order; natural layout)")
     ap.add_argument("--layout", default="storage", choices=["storage", "natural"],
@@ -188,6 +188,9 @@ def main():
                     help="ops: torch.ops.nngp.bf_sweep_out (default); ctypes: the same C ABI via ctypes (A/B)")
     ap.add_argument("--event-stride", type=int, default=10,
                     help="bracket every S-th timed sweep with HIP events for kernel_ms (1 = every sweep)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="exchange the partials through torch.distributed even on one rank (a one-rank RCCL group "
+                         "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
@@ -206,6 +209,15 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = "RANK" in os.environ and "MASTER_ADDR" in os.environ  # launched by torch.distributed.run
+    if not distributed and args.force_collective:
+        # a one-rank RCCL group of our own (127.0.0.1, a free port): the collective path on one GPU
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        distributed = True
     if distributed:
         if args.rehearse_on_one_gpu:
             dist.init_process_group("gloo")
@@ -222,7 +234,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order,
-                          layout=args.layout, api=args.sweep_api)
+                          layout=args.layout, api=args.sweep_api, collective=distributed)
     if args.layout == "storage":
         # the synthetic field lives in the engine's storage order (an MCMC state would);
         # same iid N(0,1) values, assigned to locations in storage order
@@ -341,6 +353,8 @@ def main():
             "neighbor_build_s": knn_s,
             "loglik": ll,
             "bad_rows": [int(p[2]), int(p[3])],
+            "collective": "torch.distributed all_gather_into_tensor (" + dist.get_backend() + ") + rank-order fold"
+                          if distributed else "none (one rank)",
             "lib": os.path.relpath(_lib.LIB_PATH, ROOT),
         }
         if world == 1 and args.cpu_seconds > 0:

@@ -45,15 +45,17 @@ extern "C" {
 #define NNGP_COV_GAUSSIAN 3    /* sigma2 exp(-u^2)                                  */
 #define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
 
-/* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE, PAIR and
- * QUAD serve 2-D exponential / Matern-3/2 only, PAIRB and WAVE every kind and dimension */
-#define NNGP_ALGO_AUTO 0  /* pairb m <= 24; 2-D exp / Matern-3/2: quad 25..32; wave above                 */
+/* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE and QUAD
+ * serve 2-D exponential / Matern-3/2 only, PAIRB and WAVE every kind and dimension.  (3 and 7
+ * were comparison-only kernels of earlier builds; they are rejected as unknown.) */
+#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 32; wave above                              */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
-#define NNGP_ALGO_PAIR 3  /* two lanes per location (10 <= m <= 20)                          */
-#define NNGP_ALGO_QUAD 4  /* four lanes per location (m in 15, 16, 20, 25..32)               */
-#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 24)              */
-#define NNGP_ALGO_PAIRB_R1 7 /* the round-1 pair kernel (m = 15, exponential, 2-D): same-box A/B only */
+#define NNGP_ALGO_QUAD 4  /* four lanes per location (25 <= m <= 32)                         */
+#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 32)              */
+
+/* the kernel NNGP_ALGO_AUTO (or an explicit code, returned as is) resolves to for (m, kind, dim) */
+int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim);
 
 #define NNGP_MAX_M 63
 #define NNGP_MAX_DIM 3
@@ -112,7 +114,10 @@ int nngp_knn_query(const double *ref, int64_t n_ref, int32_t dim, const double *
  *   partials[0] = sum_i log F_i
  *   partials[1] = sum_i (v_i - B_i v_N(i))^2 / F_i        (0 when values == NULL)
  *   partials[2] = first location index whose Cholesky pivot or F_i is not > 0, else -1
- *   partials[3] = first location index with a neighbour index >= n_points, else -1
+ *   partials[3] = first location index with an invalid neighbour index (>= n_points, or
+ *                 negative other than the -1 padding), else -1; such a row's slot is
+ *                 decoupled (a far-away point), so its B / F / log-lik terms are finite but
+ *                 meaningless: callers check the flag (nngp_check_partials)
  *   log-lik = -1/2 (n_rows log 2 pi + partials[0] + partials[1]).
  * Rows flagged in partials[2] get B = F = NaN.  The sum order is fixed, so the
  * partials are bit-reproducible run to run.
@@ -132,9 +137,11 @@ int nngp_bf_sweep(const double *coords, int64_t n_points, int32_t dim, const int
                   const double *values, double *B, double *F, double *R, double *partials, void *workspace,
                   size_t workspace_bytes, int32_t algo, void *stream);
 /* The deferred fold of a sweep run with partials == NULL (fixed order: the same
- * bits as the in-line fold). */
-int nngp_bf_finalize(const void *workspace, int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo,
-                     double *partials, void *stream);
+ * bits as the in-line fold).  n_rows, m, kind, dim and algo must be the sweep's (they select
+ * the kernel, hence the record layout); workspace_bytes is checked against the size that
+ * sweep needed, so a mismatched call fails with NNGP_EINVAL instead of reading past it. */
+int nngp_bf_finalize(const void *workspace, size_t workspace_bytes, int64_t n_rows, int32_t m, int32_t kind,
+                     int32_t dim, int32_t algo, double *partials, void *stream);
 
 /* ---------------------------------------------------------------------------
  * B/F of query locations t against a reference set S (prediction / kriging at

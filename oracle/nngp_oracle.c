@@ -462,7 +462,8 @@ static inline double pdist(const double *a, const double *b, int dim) { return s
  * v = L^-1 c, B = L^-T v, F = C_ii - v.v, r = v_i - B.v_N.
  * partials[0] = sum log F, partials[1] = sum r^2/F (index order),
  * partials[2] = first row index whose pivot or F is not > 0 (or -1).
- * A slot is valid iff its index is >= 0; invalid slots give B = 0.
+ * A slot is valid iff its index is >= 0; -1 slots give B = 0; an index >= n or below -1
+ * marks the row bad (B = F = NaN, partials[2]).
  */
 int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t dim, int32_t m, int32_t kind,
                     const double *theta, const double *values, double *Bout, double *Fout, double *partials,
@@ -492,6 +493,8 @@ int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t
                 if (row[s] >= 0) {
                     if (row[s] >= n) bad = 1;
                     slot[k++] = s;
+                } else if (row[s] != -1) {
+                    bad = 1; /* only -1 pads a row */
                 }
             const double *xi = coords + dim * i;
             double F = sigma2 + tau2;

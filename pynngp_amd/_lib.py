@@ -27,6 +27,7 @@ SYMBOLS = (
     "nngp_bf_sweep",
     "nngp_bf_cross",
     "nngp_bf_finalize",
+    "nngp_resolve_algo",
     "nngp_loglik_from_partials",
     "nngp_check_partials",
     "nngp_row_order_workspace_bytes",
@@ -44,7 +45,7 @@ SYMBOLS = (
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4}
-ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "pair": 3, "quad": 4, "pairb": 5, "pairb_r1": 7}
+ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
 
@@ -89,8 +90,10 @@ def load() -> ctypes.CDLL:
     lib.nngp_row_order.argtypes = [P, I64, I32, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
-    lib.nngp_bf_finalize.argtypes = [P, I64, I32, I32, I32, I32, P, P]
+    lib.nngp_bf_finalize.argtypes = [P, ctypes.c_size_t, I64, I32, I32, I32, I32, P, P]
     lib.nngp_bf_finalize.restype = ctypes.c_int
+    lib.nngp_resolve_algo.argtypes = [I32, I32, I32, I32]
+    lib.nngp_resolve_algo.restype = I32
     lib.nngp_combine_partials.restype = ctypes.c_int
     U64 = ctypes.c_uint64
     lib.nngp_reverse_workspace_bytes.argtypes = [I64, I32]
@@ -122,6 +125,13 @@ def load() -> ctypes.CDLL:
 
 def version() -> str:
     return load().nngp_version().decode()
+
+
+def resolve_algo(algo: str, m: int, kind: str, dim: int) -> str:
+    """The kernel ``algo`` ("auto" or explicit) runs as for (m, kind, dim) (nngp_resolve_algo)."""
+    code = load().nngp_resolve_algo(ALGO_CODES[algo], int(m), KIND_CODES[kind], int(dim))
+    names = {v: k for k, v in ALGO_CODES.items()}
+    return names.get(code, str(code))
 
 
 def _check(rc: int, what: str) -> None:
@@ -310,15 +320,19 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     return B, F, partials
 
 
-def bf_finalize(workspace: torch.Tensor, rows: int, m: int, algo: str = "auto",
-                out: Optional[torch.Tensor] = None, kind: str = "exponential", dim: int = 2) -> torch.Tensor:
+def bf_finalize(workspace: torch.Tensor, rows: int, m: int, kind: str, dim: int, algo: str = "auto",
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fold the block records a ``bf_sweep(..., defer=True)`` left in ``workspace`` into
-    ``out`` (float64 (4,)), on torch's current stream (nngp_bf_finalize); ``kind`` / ``dim``
-    as the sweep's (they select the kernel, hence the record layout, under ``algo="auto"``)."""
+    ``out`` (float64 (4,)), on torch's current stream (nngp_bf_finalize).  ``rows``, ``m``,
+    ``kind``, ``dim`` and ``algo`` must be the sweep's: they select the kernel, hence the record
+    layout (the library checks the workspace size against them)."""
     dev = _require_gpu(workspace, out)
     out = torch.empty(4, dtype=torch.float64, device=dev) if out is None else out
-    _check(load().nngp_bf_finalize(_ptr(workspace), int(rows), int(m), KIND_CODES[kind], int(dim), ALGO_CODES[algo],
-                                   _ptr(out), _stream(dev)), "nngp_bf_finalize")
+    if not workspace.is_contiguous():
+        raise ValueError("workspace must be contiguous")
+    _check(load().nngp_bf_finalize(_ptr(workspace), workspace.numel() * workspace.element_size(), int(rows), int(m),
+                                   KIND_CODES[kind], int(dim), ALGO_CODES[algo], _ptr(out), _stream(dev)),
+           "nngp_bf_finalize")
     return out
 
 

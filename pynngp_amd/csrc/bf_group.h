@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
         const int a = P * s + q;
         const int32_t j = a < M ? jn[s] : -1;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
-        bad_index |= j >= 0 && !in_range;
+        bad_index |= j != -1 && !in_range;
         oval[s] = in_range;
         const bool self = a == M;
         const double2* pc = self ? qcoords + i : (in_range ? coords + j : kFarPoints + (a & 63));

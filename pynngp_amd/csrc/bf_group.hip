@@ -1,33 +1,23 @@
-// Dispatch for the P-lanes-per-location sweep kernels (template in bf_group.h,
-// instantiations in bf_pair_*.hip / bf_quad.hip).
+// Dispatch for the four-lanes-per-location sweep kernels at m = 25..32 (template in bf_group.h,
+// instantiations in bf_quad_b.hip / bf_quad_c.hip; 2-D exponential and Matern-3/2 only).  The
+// two-lane bf_group and the m <= 20 four-lane instantiations were comparison points of the
+// blocked pair kernel (bf_pairb.h) and are no longer built into the library.
 #include "bf_group.h"
 
 namespace nngp {
 
-bool bf_pair_launch_a(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pair_launch_b(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pair_launch_c(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_pair_launch_d(const BfArgs&, const CovParams&, hipStream_t);
-bool bf_quad_launch(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch_b(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch_c(const BfArgs&, const CovParams&, hipStream_t);
 
 int64_t bf_group_blocks(int64_t n_rows, int P) { return (n_rows * P + 255) / 256; }
 
 bool bf_group_supported(int m, int P) {
-    if (P == 2) return m >= 10 && m <= 20;
-    if (P == 4) return m == 15 || m == 16 || m == 20 || (m >= 25 && m <= 32);
-    return false;
+    return P == 4 && m >= 25 && m <= 32;
 }
 
 bool bf_group_launch(const BfArgs& a, const CovParams& Pc, int P, hipStream_t s) {
     if (!bf_group_supported(a.m, P)) return false;
-    if (P == 4) return a.m <= 20 ? bf_quad_launch(a, Pc, s) : a.m <= 28 ? bf_quad_launch_b(a, Pc, s)
-                                                                          : bf_quad_launch_c(a, Pc, s);
-    if (a.m <= 13) return bf_pair_launch_a(a, Pc, s);
-    if (a.m <= 16) return bf_pair_launch_b(a, Pc, s);
-    if (a.m <= 18) return bf_pair_launch_c(a, Pc, s);
-    return bf_pair_launch_d(a, Pc, s);
+    return a.m <= 28 ? bf_quad_launch_b(a, Pc, s) : bf_quad_launch_c(a, Pc, s);
 }
 
 }  // namespace nngp

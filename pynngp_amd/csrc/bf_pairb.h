@@ -208,9 +208,11 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 const double* __restrict__ values, const double* __restrict__ qcoords,
                                                 const double* __restrict__ qvalues, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double4* __restrict__ rec, int32_t* __restrict__ lexp) {
-    static_assert(M >= 1 && M <= 24, "pairb instantiated for 1 <= m <= 24");
-    static_assert(D >= 1 && D <= 3, "1 <= D <= 3");
+                                                double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim) {
+    static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
+    static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
+    constexpr int DA = point_arity<D>();  // coordinates held per point
+    const int ds = D == 0 ? dim : D;      // row stride of coords / qcoords
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
@@ -251,26 +253,29 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const int a = 2 * s + q;
             jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
         }
-        double o[NP][D], z[NP];
+        double o[NP][DA], z[NP];
         // one unsigned compare per slot (a negative index is out of range as a huge unsigned);
-        // an index >= n_points anywhere in the row shows in the row's largest index
-        // (n_points >= 2^31: every non-negative int32 index is in range)
+        // an index >= n_points anywhere in the row shows in the row's largest index, one below -1
+        // (only -1 pads a row) in its smallest (n_points >= 2^31: every non-negative int32 index is
+        // in range)
         const uint32_t n32 = n_points < (int64_t)0x80000000ll ? (uint32_t)n_points : 0x80000000u;
-        int32_t jmax = -1;
+        int32_t jmax = -1, jmin = -1;
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
             const int a = 2 * s + q;
             const int32_t j = a < M ? jn[s] : -1;
             jmax = max(jmax, j);
+            jmin = min(jmin, j);
             const bool in_range = (uint32_t)j < n32;
             const bool self = a == M;
-            const double* pc = self ? qcoords + i * D : (in_range ? coords + (int64_t)j * D : far_point<D>(a));
+            const double* pc = self ? qcoords + i * ds : (in_range ? coords + (int64_t)j * ds : far_point<DA>(a));
             const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                     : ((values != nullptr && in_range) ? values + j : kZeroValue);
-            load_point<D>(pc, o[s]);
+            if constexpr (D == 0) load_point_rt(pc, dim, o[s]);
+            else load_point<D>(pc, o[s]);
             z[s] = *pv;
         }
-        const bool bad_index = (int64_t)jmax >= n_points;
+        const bool bad_index = (int64_t)jmax >= n_points || jmin < -1;
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
@@ -284,17 +289,17 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         // ---- unit-variance covariances in own-parity-first order
         double R[NP][NP][2];
         {
-            double p[NP][D];
+            double p[NP][DA];
 #pragma unroll
             for (int t = 0; t < NP; ++t)
 #pragma unroll
-                for (int k = 0; k < D; ++k) p[t][k] = pr_swap(o[t][k]);
+                for (int k = 0; k < DA; ++k) p[t][k] = pr_swap(o[t][k]);
 #pragma unroll
             for (int s = 0; s < NP; ++s) {
 #pragma unroll
                 for (int t = 0; t < s; ++t) {
-                    R[s][t][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s], o[t]));
-                    R[s][t][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s], p[t]));
+                    R[s][t][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], o[t]));
+                    R[s][t][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], p[t]));
                 }
                 R[s][s][0] = Pc.diag;
             }
@@ -305,18 +310,18 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             for (int s0 = 0; s0 < NP; s0 += 2) {
                 const int s1 = s0 + 1;
                 if (M <= NNGP_PAIRB_DEDUP_MAX && s1 < NP) {
-                    double a[D], b[D];
+                    double a[DA], b[DA];
 #pragma unroll
-                    for (int k = 0; k < D; ++k) {
+                    for (int k = 0; k < DA; ++k) {
                         a[k] = pr_pick(mask1, o[s1][k], o[s0][k]);
                         b[k] = pr_pick(mask1, p[s1][k], p[s0][k]);
                     }
-                    const double c = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(a, b));
+                    const double c = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(a, b));
                     R[s1][s1][1] = c;
                     R[s0][s0][1] = pr_from0(c);
                 } else {
-                    R[s0][s0][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s0], p[s0]));
-                    if (s1 < NP) R[s1][s1][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<D>(o[s1], p[s1]));
+                    R[s0][s0][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s0], p[s0]));
+                    if (s1 < NP) R[s1][s1][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s1], p[s1]));
                 }
             }
         }
@@ -551,7 +556,17 @@ template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), 0, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.sigma2, a.values, a.qcoords, a.qvalues, a.B,
-                       a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows));
+                       a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), a.dim);
+}
+
+// m = 25..32: one instantiation per m for every kind and dimension (runtime kind NNGP_KIND_GENERIC,
+// runtime dimension D = 0): these fully unrolled kernels take 0.5-2.5 min each to compile, and the
+// extra work per covariance (the kind's polynomial, padded coordinates) is a few percent of theirs
+template <int M>
+static bool launch_pairb_generic_if(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
+    if (a.m != M) return false;
+    launch_pairb_mkd<M, NNGP_KIND_GENERIC, 0>(a, Pc, s);
+    return true;
 }
 
 // one m and dimension, every kind (instantiated by the generated bf_pairb_inst_*.hip units)

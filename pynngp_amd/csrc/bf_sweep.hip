@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void bf_lane(const double2* __restrict__ coord
     for (int a = 0; a < M; ++a) {
         const int32_t j = jn[a];
         const bool v = j >= 0 && (int64_t)j < n_points;
-        bad_index |= j >= 0 && !v;
+        bad_index |= j != -1 && !v;
         valid[a] = v;
         const double2 x = *(v ? coords + j : kFarPoints + a);
         px[a] = x.x;
@@ -353,7 +353,6 @@ int64_t bf_record_count(int64_t n_rows, int algo, int m) {
     if (n_rows == 0) return 0;
     if (algo == kAlgoLane) return bf_lane_blocks(n_rows);
     if (algo == kAlgoPairB) return bf_pairb_tiles(n_rows);
-    if (algo == kAlgoPair || algo == kAlgoPairBR1) return bf_group_blocks(n_rows, 2);
     if (algo == kAlgoQuad) return bf_group_blocks(n_rows, 4);
     return bf_wave_blocks(n_rows);
 }
@@ -380,19 +379,9 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || a.partials == nullptr) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
-    } else if (algo == kAlgoPairBR1) {
-        const int var = pairb_r1_variant();
-        ok = bf_pairb_r1_launch(a, (var & 1) ? nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2) : P, s);
-        nb = bf_group_blocks(a.n_rows, 2);
-        if (ok && (var & 2)) {
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess || a.partials == nullptr) return e;
-            return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
-        }
-    } else if (algo == kAlgoPair || algo == kAlgoQuad) {
-        const int lanes = algo == kAlgoPair ? 2 : 4;
-        ok = a.dim == 2 && a.kind <= 1 && bf_group_launch(a, P, lanes, s);
-        nb = bf_group_blocks(a.n_rows, lanes);
+    } else if (algo == kAlgoQuad) {
+        ok = a.dim == 2 && a.kind <= 1 && bf_group_launch(a, P, 4, s);
+        nb = bf_group_blocks(a.n_rows, 4);
     } else {
         nb = bf_wave_blocks(a.n_rows);
         ok = bf_wave_launch(a, P, nb, s);

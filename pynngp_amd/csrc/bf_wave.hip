@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords
         const int32_t j = (lane < M) ? jr : -1;
         const bool is_self = lane == M;
         const bool in_range = j >= 0 && (int64_t)j < n_points;
-        const bool bad_index = j >= 0 && !in_range;
+        const bool bad_index = j != -1 && !in_range;
         const double* pc = is_self ? qcoords + i * dim
                                    : (in_range ? coords + (int64_t)j * dim : far_point<1>(lane));  // far: (x, 0, 0)
         const double* pv = is_self ? (qvalues != nullptr ? qvalues + i : kZeroValue)

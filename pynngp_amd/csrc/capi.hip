@@ -27,22 +27,15 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order
-// (tools/algo_table.py, profiles/r02ap/algo_lane_pairb_m1_24.jsonl): the
-// 2x2-blocked two-lane kernel for 1 <= m <= 24 (since its round-2 instruction cuts it ties the
-// one-lane kernel at m = 1, 2 and is faster from m = 3), four lanes for 25..32 on the
-// configurations' 2-D exponential / Matern-3/2 fields, one wavefront per location above.  Other
-// kinds and dimensions are instantiated for the blocked pair kernel (m <= 24) and the
-// wavefront kernel.
+// NNGP_ALGO_AUTO: the 2x2-blocked two-lane kernel (bf_pairb.h) for 1 <= m <= 32 -- fastest per m,
+// measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py; profiles/r02ap for m <= 24, since
+// its round-2 cuts it ties the one-lane kernel at m = 1, 2 and is faster from m = 3; m = 25..32:
+// DESIGN.md 4.3), every kind and dimension; one wavefront per location above.
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
+    (void)kind;
+    (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
-    const bool classic = dim == 2 && (kind == NNGP_COV_EXPONENTIAL || kind == NNGP_COV_MATERN32);
-    if (classic) {
-        if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
-        if (m >= 25 && m <= 32) return nngp::kAlgoQuad;  // ~10x bf_wave (tools/algo_table.py)
-        return nngp::kAlgoWave;
-    }
-    if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
+    if (m >= 1 && m <= 32) return nngp::kAlgoPairB;
     return nngp::kAlgoWave;
 }
 
@@ -54,6 +47,8 @@ extern "C" {
 const char* nngp_version(void) { return "pynngp_amd 0.1.0 gfx950"; }
 
 const char* nngp_last_error(void) { return g_err; }
+
+int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) { return resolve_algo(algo, m, kind, dim); }
 
 int nngp_check_partials(const double* p, int64_t* first_bad_row, int64_t* first_bad_index) {
     if (p == nullptr) return fail(NNGP_EINVAL, "partials must be non-null");
@@ -71,8 +66,7 @@ double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo) {
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return 0;
     const int a = resolve_algo(algo, m, kind, dim);
-    if (a == nngp::kAlgoPairB || a == nngp::kAlgoPairBR1)
-        return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + counters
+    if (a == nngp::kAlgoPairB) return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + exponent sums
     const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a, m) : 0;
     return align256((size_t)nb * 4 * sizeof(double));
 }
@@ -98,17 +92,16 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
     int a = resolve_algo(algo, m, kind, dim);
-    if (a < nngp::kAlgoLane || a > nngp::kAlgoPairBR1 || a == 6) return fail(NNGP_EINVAL, "unknown algo %d", algo);
-    if (a == nngp::kAlgoPairBR1 && !(m == 15 && kind == NNGP_COV_EXPONENTIAL && dim == 2))
-        return fail(NNGP_EUNSUP, "the round-1 A/B kernel is instantiated for m = 15, exponential, 2-D only");
+    if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
+        return fail(NNGP_EINVAL, "unknown algo %d", algo);
     const bool classic = dim == 2 && kind <= NNGP_COV_MATERN32;
-    if ((a == nngp::kAlgoLane || a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !classic)
-        return fail(NNGP_EUNSUP, "the lane / pair / quad kernels serve 2-D exponential and Matern-3/2 only "
+    if ((a == nngp::kAlgoLane || a == nngp::kAlgoQuad) && !classic)
+        return fail(NNGP_EUNSUP, "the lane / quad kernels serve 2-D exponential and Matern-3/2 only "
                                  "(kind=%d, dim=%d): use NNGP_ALGO_AUTO, PAIRB or WAVE", kind, dim);
     if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
         return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
-    if ((a == nngp::kAlgoPair || a == nngp::kAlgoQuad) && !nngp::bf_group_supported(m, a == nngp::kAlgoPair ? 2 : 4))
-        return fail(NNGP_EUNSUP, "no %s-lane kernel instantiated for m=%d", a == nngp::kAlgoPair ? "2" : "4", m);
+    if (a == nngp::kAlgoQuad && !nngp::bf_group_supported(m, 4))
+        return fail(NNGP_EUNSUP, "no 4-lane kernel instantiated for m=%d (25..32)", m);
     if (a == nngp::kAlgoPairB && !nngp::bf_pairb_supported(m))
         return fail(NNGP_EUNSUP, "no blocked pair kernel instantiated for m=%d", m);
     const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo);
@@ -142,13 +135,21 @@ int nngp_bf_cross(const double* ref, int64_t n_ref, int32_t dim, const double* q
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
-int nngp_bf_finalize(const void* workspace, int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo,
-                     double* partials, void* stream) {
+int nngp_bf_finalize(const void* workspace, size_t workspace_bytes, int64_t n_rows, int32_t m, int32_t kind,
+                     int32_t dim, int32_t algo, double* partials, void* stream) {
     if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
+    if (dim < 1 || dim > NNGP_MAX_DIM || kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_SPHERICAL)
+        return fail(NNGP_EINVAL, "bad kind %d or dim %d", kind, dim);
     const int a = resolve_algo(algo, m, kind, dim);
-    hipError_t e = (a == nngp::kAlgoPairB || (a == nngp::kAlgoPairBR1 && (nngp::pairb_r1_variant() & 2))) &&
-                           n_rows > 0
+    if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
+        return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo);
+    if (workspace_bytes < need)
+        return fail(NNGP_EINVAL, "workspace of %zu bytes is smaller than the %zu the sweep (n_rows=%lld, m=%d, "
+                                 "kind=%d, dim=%d, algo=%d) needs", workspace_bytes, need, (long long)n_rows, m, kind,
+                    dim, algo);
+    hipError_t e = a == nngp::kAlgoPairB && n_rows > 0
                        ? nngp::bf_finalize_pairb_launch((void*)workspace, n_rows, partials, (hipStream_t)stream)
                        : nngp::bf_finalize_launch((const double*)workspace, nngp::bf_record_count(n_rows, a, m),
                                                   partials, (hipStream_t)stream);

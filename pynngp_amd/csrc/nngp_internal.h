@@ -25,12 +25,17 @@ static __device__ double kFarPoints3[64 * 3] = {1e150, 0.0, 0.0, 2e150, 0.0, 0.0
 // ---------------------------------------------------------------- D-dimensional points
 // Ordinates are fp64 (n, D) row-major (the reference's KDTree takes any dimension,
 // nngp.py:55-61).  D = 2 loads a point with one 16-byte load.
+// D = 0: the dimension is a runtime argument (1..3) and points are held as 3 coordinates, the
+// missing ones 0 (the m = 25..32 kernels: one instantiation for every dimension).  The 3-D far
+// points serve every runtime dimension (their first coordinate is the far one).
 template <int D>
 __device__ __forceinline__ const double* far_point(int a) {
     if constexpr (D == 1) return kFarPoints1 + (a & 63);
     else if constexpr (D == 2) return (const double*)(kFarPoints + (a & 63));
     else return kFarPoints3 + 3 * (a & 63);
 }
+template <int D>
+constexpr int point_arity() { return D == 0 ? 3 : D; }
 
 template <int D>
 __device__ __forceinline__ void load_point(const double* __restrict__ p, double (&x)[D]) {
@@ -42,6 +47,13 @@ __device__ __forceinline__ void load_point(const double* __restrict__ p, double 
 #pragma unroll
         for (int k = 0; k < D; ++k) x[k] = p[k];
     }
+}
+
+// a point of runtime dimension dim (1..3) as 3 coordinates (the missing ones read 0 from a table,
+// branch-free)
+__device__ __forceinline__ void load_point_rt(const double* __restrict__ p, int dim, double (&x)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = *(k < dim ? p + k : kZeroValue);
 }
 
 // squared distance for the covariance, floored at 2^-1000 (nngp_d2's order for D = 2:
@@ -60,10 +72,9 @@ __device__ __forceinline__ double point_d2(const double (&a)[D], const double (&
 constexpr int kAlgoAuto = 0;
 constexpr int kAlgoLane = 1;
 constexpr int kAlgoWave = 2;
-constexpr int kAlgoPair = 3;  // bf_group, 2 lanes per location
-constexpr int kAlgoQuad = 4;  // bf_group, 4 lanes per location
-constexpr int kAlgoPairB = 5; // bf_pairb, 2 lanes per location, 2x2-blocked elimination
-constexpr int kAlgoPairBR1 = 7;  // the round-1 bf_pairb (m = 15, exponential, 2-D), kept for same-box A/B
+// (3 was the two-lane bf_group and 7 the round-1 bf_pairb: comparison kernels, no longer built)
+constexpr int kAlgoQuad = 4;  // bf_group, 4 lanes per location (m = 25..32, 2-D exponential / Matern-3/2)
+constexpr int kAlgoPairB = 5; // bf_pairb, 2 lanes per location, 2x2-blocked elimination (m = 1..32)
 constexpr int kLaneMaxM = 16;
 
 struct BfArgs {
@@ -97,8 +108,6 @@ bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t
 bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
-bool bf_pairb_r1_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
-int pairb_r1_variant();
 // number of 256-thread blocks (= partial records) each kernel launches for n_rows
 int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);

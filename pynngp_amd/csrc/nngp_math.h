@@ -62,6 +62,10 @@ static __device__ const double kExp2Tab[256] = NNGP_EXP2_TAB;
 #define NNGP_KIND_GAUSSIAN 3     // sigma2 e^-u^2          (no square root: the exponent is phi^2 d^2)
 #define NNGP_KIND_SPHERICAL 4    // sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0   (no exponential)
 #define NNGP_N_KINDS 5
+// Runtime kind (the m = 25..32 kernels, one instantiation for all five kinds): every kind as
+// p(u) e, p(u) = 1 + c1 u + c2 u^2 + c3 u^3 with u = min(phi d, umax), e = 2^(nphi256 g / 256) with
+// g = d (g = d^2 for the gaussian kind; nphi256 = 0, i.e. e = 1, for the spherical kind).
+#define NNGP_KIND_GENERIC 5
 
 // Covariance parameters, built once on the host (nngp_cov_params) and passed by value.
 struct CovParams {
@@ -72,6 +76,9 @@ struct CovParams {
     double phi;
     double diag;     // sigma2 + tau2
     double sigma2;
+    double c[3];     // NNGP_KIND_GENERIC: polynomial coefficients c1, c2, c3 of the kind
+    double umax;     // NNGP_KIND_GENERIC: u = phi d is clamped at umax (1 for the spherical kind)
+    int gauss;       // NNGP_KIND_GENERIC: the exponent's variable is d^2 (gaussian), else d
 };
 
 NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double tau2) {
@@ -94,6 +101,11 @@ NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double ta
     p.phi = phi;
     p.diag = sigma2 + tau2;
     p.sigma2 = sigma2;
+    p.c[0] = kind == NNGP_KIND_MATERN32 || kind == NNGP_KIND_MATERN52 ? 1.0 : kind == NNGP_KIND_SPHERICAL ? -1.5 : 0.0;
+    p.c[1] = kind == NNGP_KIND_MATERN52 ? 1.0 / 3.0 : 0.0;
+    p.c[2] = kind == NNGP_KIND_SPHERICAL ? 0.5 : 0.0;
+    p.umax = kind == NNGP_KIND_SPHERICAL ? 1.0 : 1e300;
+    p.gauss = kind == NNGP_KIND_GAUSSIAN;
     return p;
 }
 
@@ -242,6 +254,13 @@ NNGP_FN double nngp_cov_unit(const CovParams& P, const double* tab, double d2) {
     if (KIND == NNGP_KIND_SPHERICAL) {
         const double u = fmin(P.phi * d, 1.0);
         return fma(u, fma(0.5 * u, u, -1.5), 1.0);
+    }
+    if (KIND == NNGP_KIND_GENERIC) {
+        // exponential: p = 1 exactly; Matern-5/2 and spherical: the same polynomial operations as
+        // their own kinds below; Matern-3/2: (1 + u) e, one more rounding than e + u e
+        const double e = nngp_exp_unit(P, tab, P.gauss ? x : d);
+        const double u = fmin(P.phi * d, P.umax);
+        return fma(u, fma(u, fma(u, P.c[2], P.c[1]), P.c[0]), 1.0) * e;
     }
     const double e = nngp_exp_unit(P, tab, d);
     if (KIND == NNGP_KIND_MATERN32) return fma(P.phi * d, e, e);

@@ -16,13 +16,16 @@
 // log-likelihood oneSample needs (nngp.py:98-101); bf_cross <- B_t / F_t at t not in S.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include "../../include/nngp.h"
 
 namespace {
 
-void* stream() { return (void*)at::hip::getCurrentHIPStream().stream(); }
+// Every op runs on the current stream of ITS TENSORS' device, under a device guard for that
+// device (a tensor on cuda:1 while cuda:0 is current must not launch on cuda:0's stream).
+void* stream(const at::Tensor& t) { return (void*)at::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 void check_rc(int rc, const char* what) { TORCH_CHECK(rc == NNGP_OK, what, " failed (", rc, "): ", nngp_last_error()); }
 
@@ -62,31 +65,34 @@ at::Tensor workspace(int64_t bytes, const at::Tensor& like) {
 // ---------------------------------------------------------------- neighbour sets
 at::Tensor knn_prior(const at::Tensor& coords, int64_t m, int64_t q0, int64_t q1) {
     check_coords(coords, "coords");
+    const at::OptionalDeviceGuard guard(coords.device());
     const int64_t n = coords.size(0), d = coords.size(1);
     TORCH_CHECK(0 <= q0 && q0 <= q1 && q1 <= n, "query rows [", q0, ", ", q1, ") outside [0, ", n, ")");
     auto out = at::empty({q1 - q0, m}, coords.options().dtype(at::kInt));
     auto ws = workspace((int64_t)nngp_knn_workspace_bytes(n, (int32_t)d, (int32_t)m), coords);
     check_rc(nngp_knn_prior(coords.data_ptr<double>(), n, (int32_t)d, (int32_t)m, q0, q1, out.data_ptr<int32_t>(),
-                            ws.data_ptr(), ws.numel(), stream()),
+                            ws.data_ptr(), ws.numel(), stream(coords)),
              "nngp_knn_prior");
     return out;
 }
 
 at::Tensor knn_prior_rows(const at::Tensor& coords, int64_t m, const at::Tensor& rows) {
     check_coords(coords, "coords");
+    const at::OptionalDeviceGuard guard(coords.device());
     TORCH_CHECK(rows.scalar_type() == at::kInt && rows.dim() == 1 && rows.is_contiguous(), "rows must be int32 (n_rows,)");
     check_same_device(coords, rows, "rows");
     const int64_t n = coords.size(0), d = coords.size(1);
     auto out = at::empty({rows.size(0), m}, coords.options().dtype(at::kInt));
     auto ws = workspace((int64_t)nngp_knn_workspace_bytes(n, (int32_t)d, (int32_t)m), coords);
     check_rc(nngp_knn_prior_rows(coords.data_ptr<double>(), n, (int32_t)d, (int32_t)m, rows.data_ptr<int32_t>(),
-                                 rows.size(0), out.data_ptr<int32_t>(), ws.data_ptr(), ws.numel(), stream()),
+                                 rows.size(0), out.data_ptr<int32_t>(), ws.data_ptr(), ws.numel(), stream(coords)),
              "nngp_knn_prior_rows");
     return out;
 }
 
 at::Tensor knn_query(const at::Tensor& ref, const at::Tensor& query, int64_t k) {
     check_coords(ref, "ref");
+    const at::OptionalDeviceGuard guard(ref.device());
     check_coords(query, "query");
     check_same_device(ref, query, "query");
     TORCH_CHECK(ref.size(1) == query.size(1), "ref and query have different dimensions");
@@ -94,7 +100,7 @@ at::Tensor knn_query(const at::Tensor& ref, const at::Tensor& query, int64_t k) 
     auto out = at::empty({query.size(0), k}, ref.options().dtype(at::kInt));
     auto ws = workspace((int64_t)nngp_knn_workspace_bytes(ref.size(0), (int32_t)d, (int32_t)k), ref);
     check_rc(nngp_knn_query(ref.data_ptr<double>(), ref.size(0), (int32_t)d, query.data_ptr<double>(), query.size(0),
-                            (int32_t)k, out.data_ptr<int32_t>(), ws.data_ptr(), ws.numel(), stream()),
+                            (int32_t)k, out.data_ptr<int32_t>(), ws.data_ptr(), ws.numel(), stream(ref)),
              "nngp_knn_query");
     return out;
 }
@@ -107,6 +113,7 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
                   const c10::optional<at::Tensor>& R, const at::Tensor& partials, const at::Tensor& ws,
                   int64_t algo) {
     check_coords(coords, "coords");
+    const at::OptionalDeviceGuard guard(coords.device());
     check_nbr(nbr, coords);
     const int64_t rows = nbr.size(0), m = nbr.size(1), n = coords.size(0), d = coords.size(1);
     if (order.has_value()) {
@@ -124,7 +131,7 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
     check_rc(nngp_bf_sweep(coords.data_ptr<double>(), n, (int32_t)d, nbr.data_ptr<int32_t>(), ptr<int32_t>(order), rows,
                            (int32_t)m, i0, (int32_t)kind, sigma2, phi, tau2, ptr<double>(values), ptr<double>(B),
                            ptr<double>(F), ptr<double>(R), partials.data_ptr<double>(), ws.data_ptr(),
-                           (size_t)ws.nbytes(), (int32_t)algo, stream()),
+                           (size_t)ws.nbytes(), (int32_t)algo, stream(coords)),
              "nngp_bf_sweep");
 }
 
@@ -133,6 +140,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_sweep(const at::Tensor& coords
                                                         const c10::optional<at::Tensor>& values, bool want_bf,
                                                         int64_t algo, const c10::optional<at::Tensor>& order) {
     check_coords(coords, "coords");
+    const at::OptionalDeviceGuard guard(coords.device());
     check_nbr(nbr, coords);
     const int64_t rows = nbr.size(0), m = nbr.size(1);
     auto f64 = coords.options();
@@ -152,6 +160,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
                                                         double tau2, const c10::optional<at::Tensor>& ref_values,
                                                         int64_t algo) {
     check_coords(ref, "ref");
+    const at::OptionalDeviceGuard guard(ref.device());
     check_coords(query, "query");
     check_same_device(ref, query, "query");
     TORCH_CHECK(ref.size(1) == query.size(1), "ref and query have different dimensions");
@@ -167,7 +176,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
                            nbr.data_ptr<int32_t>(), nullptr, rows, (int32_t)m, 0, (int32_t)kind, sigma2, phi, tau2,
                            ptr<double>(ref_values), nullptr, B.data_ptr<double>(), F.data_ptr<double>(),
                            ref_values.has_value() ? R.data_ptr<double>() : nullptr, p.data_ptr<double>(),
-                           ws.data_ptr(), ws.nbytes(), (int32_t)algo, stream()),
+                           ws.data_ptr(), ws.nbytes(), (int32_t)algo, stream(ref)),
              "nngp_bf_cross");
     // R = 0 - B_t v_N: the kriging mean is -R (zeros without reference values)
     at::Tensor mean = ref_values.has_value() ? R.neg() : at::zeros({rows}, f64);
@@ -177,6 +186,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
 std::tuple<at::Tensor, at::Tensor> row_order(const at::Tensor& coords, int64_t i0, int64_t rows,
                                              const c10::optional<at::Tensor>& nbr) {
     check_coords(coords, "coords");
+    const at::OptionalDeviceGuard guard(coords.device());
     const int64_t n = coords.size(0);
     TORCH_CHECK(0 <= i0 && 0 <= rows && i0 + rows <= n, "rows [", i0, ", ", i0 + rows, ") outside [0, ", n, ")");
     int64_t m = 0;
@@ -190,7 +200,7 @@ std::tuple<at::Tensor, at::Tensor> row_order(const at::Tensor& coords, int64_t i
     auto ws = workspace((int64_t)nngp_row_order_workspace_bytes(rows), coords);
     check_rc(nngp_row_order(coords.data_ptr<double>(), n, (int32_t)coords.size(1), ptr<int32_t>(nbr), (int32_t)m, i0,
                             rows, order.data_ptr<int32_t>(), nbr.has_value() ? srt.data_ptr<int32_t>() : nullptr,
-                            ws.data_ptr(), ws.nbytes(), stream()),
+                            ws.data_ptr(), ws.nbytes(), stream(coords)),
              "nngp_row_order");
     return {order, srt};
 }
@@ -199,9 +209,10 @@ void combine_partials_out(const at::Tensor& gathered, const at::Tensor& out) {
     TORCH_CHECK(gathered.is_cuda() && gathered.scalar_type() == at::kDouble && gathered.dim() == 2 &&
                     gathered.size(1) == 4 && gathered.is_contiguous(),
                 "gathered must be a contiguous float64 (world, 4) GPU tensor");
+    const at::OptionalDeviceGuard guard(gathered.device());
     check_f64(out, {4}, gathered, "out");
     check_rc(nngp_combine_partials(gathered.data_ptr<double>(), (int32_t)gathered.size(0), out.data_ptr<double>(),
-                                   stream()),
+                                   stream(gathered)),
              "nngp_combine_partials");
 }
 

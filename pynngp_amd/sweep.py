@@ -31,16 +31,27 @@ def shard_range(n: int, rank: int, world: int):
     return (n * rank) // world, (n * (rank + 1)) // world
 
 
-def combine_partials(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
+def _collective_default(collective: Optional[bool]) -> bool:
+    """Exchange partials through torch.distributed whenever a process group exists (so a
+    one-rank RCCL group runs the same all-gather + fold as N ranks), unless told otherwise."""
+    if collective is not None:
+        return bool(collective)
+    return dist.is_available() and dist.is_initialized()
+
+
+def combine_partials(local: torch.Tensor, world: int, group=None, force: bool = False) -> torch.Tensor:
     """All-gather the (4,) partials and reduce them in rank order.
 
     [0], [1] are summed; [2], [3] (first bad row or -1) take the smallest non-negative.
+    One rank returns ``local`` itself unless ``force`` (then the collective and the fold run
+    exactly as with N ranks: the path a one-GPU box can test).
     """
-    if world == 1:
+    if world == 1 and not force:
         return local
     gathered = torch.empty((world, 4), dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(gathered, local.reshape(1, 4), group=group)
     if gathered.device.type == "cuda":
+        ops.load()  # torch.ops.nngp.combine_partials_out lives in libnngp_torch_ops.so
         out = torch.empty(4, dtype=local.dtype, device=local.device)
         torch.ops.nngp.combine_partials_out(gathered, out)  # one tiny HIP kernel, rank order
         return out
@@ -71,7 +82,7 @@ class ShardedLogLik:
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
                  algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
                  spatial_order: bool = True, layout: str = "natural", build_perm: Optional[Callable] = None,
-                 api: str = "ops"):
+                 api: str = "ops", collective: Optional[bool] = None):
         if layout not in ("natural", "storage"):
             raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
         if api not in ("ops", "ctypes"):
@@ -84,6 +95,9 @@ class ShardedLogLik:
         self.n = coords.shape[0]
         self.m = int(m)
         self.rank, self.world, self.group = rank, world, group
+        # partials go through the all-gather whenever torch.distributed is initialised (also at
+        # world 1), or as ``collective`` says
+        self.collective = _collective_default(collective)
         self.lo, self.hi = shard_range(self.n, rank, world)
         self.algo = algo
         self._compute = compute
@@ -150,7 +164,8 @@ class ShardedLogLik:
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,
                  values_layout: str = "input") -> torch.Tensor:
         """Global partials (all ranks), stream-ordered."""
-        return combine_partials(self.local_partials(cov, values, want_bf, values_layout), self.world, self.group)
+        return combine_partials(self.local_partials(cov, values, want_bf, values_layout), self.world, self.group,
+                                force=self.collective)
 
     def loglik(self, cov: Covariance, values: torch.Tensor, want_bf: bool = False,
                values_layout: str = "input") -> float:
@@ -214,6 +229,9 @@ class PipelinedCombine:
         dev = sweep.coords.device
         self.sweep = sweep
         self.world = sweep.world
+        self.active = self.world > 1 or getattr(sweep, "collective", False)
+        if dev.type == "cuda":
+            ops.load()  # torch.ops.nngp.combine_partials_out lives in libnngp_torch_ops.so
         self.local = torch.empty((slots, 4), dtype=torch.float64, device=dev)
         self.gathered = torch.empty((slots, self.world, 4), dtype=torch.float64, device=dev)
         self.results = torch.empty((slots, 4), dtype=torch.float64, device=dev)
@@ -222,7 +240,7 @@ class PipelinedCombine:
 
     def exchange(self, k: int) -> None:
         self.k = max(self.k, k + 1)
-        if self.world == 1:
+        if not self.active:
             return
         work = dist.all_gather_into_tensor(self.gathered[k], self.local[k].reshape(1, 4),
                                            group=self.sweep.group, async_op=True)
@@ -235,7 +253,7 @@ class PipelinedCombine:
             torch.ops.nngp.combine_partials_out(self.gathered[k], self.results[k])
 
     def finish(self) -> torch.Tensor:
-        if self.world == 1:
+        if not self.active:
             return self.local[: self.k]
         if self.side is not None:
             torch.cuda.current_stream(self.side.device).wait_stream(self.side)

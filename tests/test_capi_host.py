@@ -80,8 +80,11 @@ def _sweep(lib, **kw):
     (dict(dim=0), -4, "dim=0"),
     (dict(dim=4), -4, "dim=4"),
     (dict(algo=1, m=8, kind=2), -4, "2-D exponential and Matern-3/2 only"),
-    (dict(algo=3, m=15, dim=3), -4, "2-D exponential and Matern-3/2 only"),
-    (dict(algo=5, m=25), -4, "blocked pair kernel"),
+    (dict(algo=4, m=26, dim=3), -4, "2-D exponential and Matern-3/2 only"),
+    (dict(algo=4, m=20), -4, "4-lane kernel"),
+    (dict(algo=3, m=15), -1, "unknown algo"),  # the removed comparison kernels
+    (dict(algo=7, m=15), -1, "unknown algo"),
+    (dict(algo=5, m=33), -4, "blocked pair kernel"),
     (dict(sigma2=0.0), -1, "theta"),
     (dict(phi=float("nan")), -1, "theta"),
     (dict(tau2=-1.0), -1, "theta"),
@@ -150,3 +153,25 @@ def test_check_partials_codes(lib):
     assert run([1.0, 2.0, 1234.0, -1.0]) == (-2, 1234, -1)
     assert b"1234" in lib.nngp_last_error()
     assert run([1.0, 2.0, 5.0, 99.0]) == (-1, 5, 99)
+
+
+def test_resolve_algo_table(lib):
+    """auto: the blocked pair kernel for 1 <= m <= 32 at every kind and dimension, the wavefront
+    kernel above; explicit codes pass through."""
+    for m in (1, 15, 20, 24, 25, 32):
+        for kind in range(5):
+            for dim in (1, 2, 3):
+                assert lib.nngp_resolve_algo(0, m, kind, dim) == 5
+    assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
+    assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
+    assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1
+
+
+def test_finalize_checks_workspace(lib):
+    P = ctypes.c_void_p
+    need = lib.nngp_bf_sweep_workspace_bytes(100_000, 15, 0, 2, 0)
+    assert lib.nngp_bf_finalize(P(256), need - 256, 100_000, 15, 0, 2, 0, P(512), None) == -1
+    assert "smaller" in lib.nngp_last_error().decode()
+    assert lib.nngp_bf_finalize(P(256), need, 100_000, 15, 9, 2, 0, P(512), None) == -1
+    assert lib.nngp_bf_finalize(P(256), need, 100_000, 15, 0, 2, 3, P(512), None) == -1
+    assert lib.nngp_bf_finalize(None, need, 100_000, 15, 0, 2, 0, P(512), None) == -1

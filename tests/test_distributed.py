@@ -82,7 +82,9 @@ def _worker_storage(rank, world, port, n, m, out):
     # pipelined exchange (throughput mode): three independent sweeps, each fully combined
     from pynngp_amd.sweep import PipelinedCombine
 
+    assert sweep.collective  # a process group exists: even one rank exchanges through it
     pipe = PipelinedCombine(sweep, 3)
+    assert pipe.active
     for k, c in enumerate([cov, cov.replace(phi=4.0), cov]):
         sweep.local_partials(c, values, out=pipe.local[k])
         pipe.exchange(k)
@@ -92,7 +94,7 @@ def _worker_storage(rank, world, port, n, m, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_gloo_storage_layout_matches_single(world):
     """Relabelled storage shards (any global permutation, identical on every rank) give
     the input-order log-likelihood, and the shards' rows cover every location once."""
@@ -152,3 +154,13 @@ def test_gloo_sharded_loglik_matches_single(world):
     assert abs(lls[0] - want) <= 1e-12 * abs(want)
     assert [(out[r][1], out[r][2]) for r in range(world)] == [shard_range(n, r, world) for r in range(world)]
     assert out[0][3] == [0.0, 0.0, 6.0, 9.0]
+
+
+def test_no_group_no_collective():
+    """Without a process group a one-rank sweep skips the exchange (the plain bench path)."""
+    assert not dist.is_initialized()
+    coords = torch.from_numpy(np.random.default_rng(1).uniform(size=(300, 2)))
+    sw = ShardedLogLik(coords, 5, 0, 1, build_nbr=_oracle_build, compute=_oracle_compute)
+    assert not sw.collective
+    p = torch.tensor([1.0, 2.0, -1.0, -1.0], dtype=torch.float64)
+    assert combine_partials(p, 1) is p

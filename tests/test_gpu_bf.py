@@ -69,21 +69,18 @@ CASES = [
     ("spherical", (1.0, 10.0, 0.05), 15),
     ("spherical", (1.2, 25.0, 0.0), 20),
 ]
-CLASSIC = ("exponential", "matern32")  # the kinds the lane / pair / quad kernels serve
+CLASSIC = ("exponential", "matern32")  # the kinds the lane / quad kernels serve
+ALL_KINDS = ("exponential", "matern32", "matern52", "gaussian", "spherical")
 
 
-PAIR_M = tuple(range(10, 21))  # instantiated for the 2-lane kernel
-QUAD_M = (15, 16, 20) + tuple(range(25, 33))  # and for the 4-lane kernel
-GROUP_M = QUAD_M
-PAIRB_M = tuple(range(1, 25))  # and for the 2x2-blocked 2-lane kernel
+QUAD_M = tuple(range(25, 33))  # instantiated for the 4-lane kernel
+PAIRB_M = tuple(range(1, 33))  # and for the 2x2-blocked 2-lane kernel (25..32: runtime kind and dimension)
 
 
-@pytest.mark.parametrize("algo", ["lane", "wave", "pair", "quad", "pairb"])
+@pytest.mark.parametrize("algo", ["lane", "wave", "pairb"])
 @pytest.mark.parametrize("kind,theta,m", CASES)
 def test_bf_vs_oracle(lib, dev, c_oracle, kind, theta, m, algo):
-    if ((algo == "pair" and m not in PAIR_M) or (algo == "quad" and m not in QUAD_M)
-            or (algo == "pairb" and m not in PAIRB_M) or (algo == "lane" and m > 16)
-            or (algo in ("lane", "pair", "quad") and kind not in CLASSIC)):
+    if (algo == "lane" and m > 16) or (algo == "lane" and kind not in CLASSIC):
         pytest.skip("not instantiated")
     coords, y = _field(6000, m)
     nbr = c_oracle.c_knn_prior(coords, m)
@@ -96,29 +93,45 @@ def test_bf_large_m(lib, dev, c_oracle, m):
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 8.0, 0.05), y, "auto")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, "wave")
-    for algo, ms in (("pair", PAIR_M), ("quad", QUAD_M), ("pairb", PAIRB_M)):
+    for algo, ms in (("quad", QUAD_M), ("pairb", PAIRB_M)):
         if m in ms:
             _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.0, 10.0, 0.1), y, algo)
             _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 30.0, 0.0), y, algo)
 
 
-@pytest.mark.parametrize("m", list(range(10, 21)))
-def test_bf_pair_all_m(lib, dev, c_oracle, m):
-    coords, y = _field(2500, 200 + m)
-    nbr = c_oracle.c_knn_prior(coords, m)
-    _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.0), y, "pair")
-    _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "pair")
-
-
 @pytest.mark.parametrize("m", list(range(25, 33)))
 def test_bf_quad_all_m(lib, dev, c_oracle, m):
-    """4-lane kernel at every m it serves by default (25..32), duplicates included."""
+    """4-lane kernel at every m it is instantiated for (25..32), duplicates included."""
     coords, y = _field(2500, 400 + m)
     coords[1000:1010] = coords[500]
     nbr = c_oracle.c_knn_prior(coords, m)
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 20.0, 0.3), y, "quad")
     _check(dev, lib, c_oracle, coords, nbr, "matern32", (1.3, 15.0, 0.2), y, "quad")
     _check(dev, lib, c_oracle, coords, nbr, "exponential", (0.8, 30.0, 0.01), None, "auto")
+
+
+@pytest.mark.parametrize("m", list(range(25, 33)))
+@pytest.mark.parametrize("kind,theta", [("exponential", (1.0, 20.0, 0.3)), ("matern32", (1.3, 15.0, 0.2)),
+                                        ("matern52", (1.0, 12.0, 0.1)), ("gaussian", (1.0, 6.0, 0.2)),
+                                        ("spherical", (1.0, 8.0, 0.05))])
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_bf_pairb_generic_m25_32(lib, dev, c_oracle, m, kind, theta, dim):
+    """m = 25..32 (one runtime-kind, runtime-dimension pairb kernel per m), every kind and
+    dimension, under algo "auto" (which must pick it, never the wavefront kernel)."""
+    rng = np.random.default_rng(500 + m + 7 * dim)
+    coords = rng.uniform(0.0, 1.0, (1500, dim))
+    coords[700:705] = coords[300]
+    y = rng.standard_normal(1500)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, "auto")
+
+
+def test_auto_never_wave_below_33(lib):
+    for m in range(1, 33):
+        for kind in ALL_KINDS:
+            for dim in (1, 2, 3):
+                assert lib.resolve_algo("auto", m, kind, dim) == "pairb", (m, kind, dim)
+    assert lib.resolve_algo("auto", 33, "exponential", 2) == "wave"
 
 
 @pytest.mark.parametrize("m", list(PAIRB_M))
@@ -189,7 +202,7 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     sing = nbr.copy()
     sing[1234, 1] = sing[1234, 0]  # repeated neighbour: C_N singular, second pivot exactly 0 (sigma2 = 1)
     sing[1500, 1] = sing[1500, 0]
-    for algo in ["lane", "wave", "pair", "pairb"]:
+    for algo in ["lane", "wave", "pairb"]:
         B, F, p = lib.bf_sweep(c, torch.from_numpy(sing).to(dev), 0, "exponential", 1.0, 5.0, 0.0, algo=algo)
         _, _, po = c_oracle.c_bf_sweep(coords, sing, "exponential", (1.0, 5.0, 0.0), None)
         assert p[2].item() == 1234 == po[2]
@@ -202,6 +215,27 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     assert p[3].item() == 1234
 
 
+@pytest.mark.parametrize("algo,m", [("lane", 10), ("wave", 10), ("pairb", 10), ("pairb", 15), ("pairb", 20),
+                                    ("pairb", 27), ("quad", 26)])
+@pytest.mark.parametrize("bad_value", [-2, -7, -2147483648, 2000, 2147483647])
+def test_bf_flags_every_invalid_index(lib, dev, c_oracle, algo, m, bad_value):
+    """Any neighbour index < -1 or >= n_points sets partials[3] to the first such row, for every
+    kernel (-1 is the only padding value); the C oracle marks the same row bad."""
+    coords, _ = _field(2000, 5)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    bad = nbr.copy()
+    bad[1234, m // 2] = bad_value  # a middle row, a middle slot
+    bad[1500, 0] = bad_value
+    c = torch.from_numpy(coords).to(dev)
+    _, _, p = lib.bf_sweep(c, torch.from_numpy(bad).to(dev), 0, "exponential", 1.0, 5.0, 0.1, algo=algo)
+    assert p[3].item() == 1234
+    _, Fo, po = c_oracle.c_bf_sweep(coords, bad, "exponential", (1.0, 5.0, 0.1), None)
+    assert po[2] == 1234 and np.isnan(Fo[1234]) and np.isnan(Fo[1500])
+    # -1 padding alone is never flagged
+    _, _, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "exponential", 1.0, 5.0, 0.1, algo=algo)
+    assert p[3].item() == -1
+
+
 def test_bf_full_size_properties(lib, dev, c_oracle):
     """Config 3 size (N=1e6, m=15): lane == wave, sampled rows vs oracle, F in (0, sigma2]."""
     n, m = 1_000_000, 15
@@ -212,7 +246,7 @@ def test_bf_full_size_properties(lib, dev, c_oracle):
     theta = (1.0, 30.0, 0.0)
     B, F, p = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo="lane")
     ll = c_oracle.loglik_from_partials(p.cpu().numpy(), n)
-    for algo in ("wave", "pair", "quad", "pairb"):
+    for algo in ("wave", "pairb"):
         Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "exponential", *theta, values=v, algo=algo)
         assert torch.allclose(F, Fw, rtol=1e-12, atol=0)
         assert torch.allclose(B, Bw, rtol=0, atol=1e-10)
@@ -246,7 +280,7 @@ def test_bf_op_registered(dev, c_oracle):
     assert abs(p2[0].item() - po[0]) <= 1e-12 * abs(po[0])
 
 
-@pytest.mark.parametrize("algo", ["lane", "pair", "quad", "wave", "pairb"])
+@pytest.mark.parametrize("algo", ["lane", "wave", "pairb"])
 def test_bf_row_order_bit_identical(lib, dev, c_oracle, algo):
     """Visiting rows in Z-order (nngp_row_order) changes nothing per row."""
     coords, y = _field(30000, 12)
@@ -331,7 +365,7 @@ def test_bf_tiny_fields(lib, dev, c_oracle):
     for n, m in [(1, 4), (2, 4), (5, 15), (16, 15), (3, 20)]:
         coords, y = _field(n, 40 + n)
         nbr = c_oracle.c_knn_prior(coords, m)
-        for algo in ("auto", "wave") + (("pairb",) if m <= 20 else ()):
+        for algo in ("auto", "wave", "pairb"):
             _check(dev, lib, c_oracle, coords, nbr, "exponential", (1.0, 5.0, 0.1), y, algo)
 
 
@@ -339,7 +373,7 @@ def test_bf_tiny_fields(lib, dev, c_oracle):
 def test_deferred_finalize_same_bits(lib, dev, c_oracle, algo):
     """nngp_bf_sweep with partials = NULL + nngp_bf_finalize (the pipelined benchmark's
     path) gives exactly the in-line partials, for every record layout."""
-    m = {"auto": 15, "lane": 10, "wave": 15, "quad": 16}[algo]
+    m = {"auto": 15, "lane": 10, "wave": 15, "quad": 26}[algo]
     coords, y = _field(20000, 77)
     nbr = torch.from_numpy(c_oracle.c_knn_prior(coords, m)).to(dev)
     c, v = torch.from_numpy(coords).to(dev), torch.from_numpy(y).to(dev)
@@ -347,5 +381,9 @@ def test_deferred_finalize_same_bits(lib, dev, c_oracle, algo):
     ws = lib.bf_workspace(nbr.shape[0], m, algo, dev)
     _, _, none = lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 20.0, 0.1, values=v, algo=algo, workspace=ws, defer=True)
     assert none is None
-    q = lib.bf_finalize(ws, nbr.shape[0], m, algo)
+    q = lib.bf_finalize(ws, nbr.shape[0], m, "exponential", 2, algo)
     assert torch.equal(p, q)
+    # a finalize whose (m, kind, dim, algo) do not match the sweep's record layout is refused
+    if algo == "wave":
+        with pytest.raises(lib.NNGPExtensionError):
+            lib.bf_finalize(ws[:256], nbr.shape[0], 15, "exponential", 2, "pairb")

@@ -6,6 +6,8 @@
 #   smoke            __graft_entry__.smoke()
 #   bench[:args]     python bench.py <args>  (one JSON line -> bench_<n>.json)
 #   ubench           tools/ubench/f64_latency (prebuilt in-tree)
+#   valumix          tools/ubench/valu_mix (prebuilt): VALU cycles per SIMD by class and waves per SIMD
+#   valuclass[:args] / valubusy[:args]   VALU class-count and VALU-busy counter passes over bench.py
 #   sq[:args]        SQ counter pass over bench.py <args> (per-kernel CSV)
 #   sqmem[:args]     memory-pipeline counter pass over bench.py <args>
 #   trace[:args]     rocprofv3 --kernel-trace --stats over bench.py <args>
@@ -53,6 +55,17 @@ for step in "$@"; do
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace_$n -o run -- python3 bench.py --cpu-seconds 0 $arg > $out/trace_$n.json 2> $out/trace_$n.err || { tail -5 $out/trace_$n.err; exit 1; }
       python3 tools/pmc_summary.py $out/trace_$n ;;
+    valuclass)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES \
+        --output-format csv -d $out/valuclass_$n -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 $arg > $out/valuclass_$n.json 2> $out/valuclass_$n.err || { tail -5 $out/valuclass_$n.err; exit 1; }
+      python3 tools/pmc_summary.py $out/valuclass_$n ;;
+    valubusy)
+      timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_CVT SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE \
+        --output-format csv -d $out/valubusy_$n -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 $arg > $out/valubusy_$n.json 2> $out/valubusy_$n.err || { tail -5 $out/valubusy_$n.err; exit 1; }
+      python3 tools/pmc_summary.py $out/valubusy_$n ;;
+    valumix)
+      timeout -k 10 120 tools/ubench/valu_mix > $out/valu_mix.txt 2>&1 || exit 1
+      cat $out/valu_mix.txt ;;
     fetch)
       timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch_$n -o run -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 $arg > $out/fetch_$n.json 2> $out/fetch_$n.err || exit 1
       python3 tools/pmc_summary.py $out/fetch_$n ;;

@@ -1,0 +1,109 @@
+// Microbenchmark: VALU issue cost per SIMD on gfx950 by instruction class and by waves per
+// SIMD (W = 1..4), the numbers the class-weighted issue bound of the B/F sweep needs
+// (is a 32-bit op -- DPP move, bfi, lshl_add -- 2 cycles across waves
+// while fp64 is 4?).  Each kernel runs 8 independent chains (ILP 8) of a 16-instruction
+// body; every wave times itself with s_memtime (shader clock, so DVFS does not enter) and
+// the report is cycles per wave-instruction per SIMD = elapsed / (W * instructions per
+// wave), median over waves.  Blocks of 256 threads (one wave per SIMD of a CU), 256 * W
+// blocks, so every SIMD holds W waves for the whole run.
+//   hipcc --offload-arch=gfx950 -O3 tools/ubench/valu_mix.hip -o tools/ubench/valu_mix
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+
+#define D8(I) I(d0) I(d1) I(d2) I(d3) I(d4) I(d5) I(d6) I(d7)
+#define F8(I) I(f0) I(f1) I(f2) I(f3) I(f4) I(f5) I(f6) I(f7)
+
+#define FMA64(x) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x) : "v"(b), "v"(c));
+#define MUL64(x) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(x) : "v"(b));
+#define RSQ64(x) asm volatile("v_rsq_f64 %0, %0" : "+v"(x));
+#define RCP64(x) asm volatile("v_rcp_f64 %0, %0" : "+v"(x));
+#define DPP32(x) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(x));
+#define AND32(x) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(k));
+#define LSHLADD32(x) asm volatile("v_lshl_add_u32 %0, %0, 4, %1" : "+v"(x) : "v"(k));
+#define BFI32(x) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(x) : "v"(k), "v"(k2));
+#define FMA32(x) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(fb), "v"(fc));
+#define CND32(x) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(k));
+
+// 16-instruction bodies
+#define BODY_fma64 D8(FMA64) D8(FMA64)
+#define BODY_mul64 D8(MUL64) D8(MUL64)
+#define BODY_rsq64 D8(RSQ64) D8(RSQ64)
+#define BODY_rcp64 D8(RCP64) D8(RCP64)
+#define BODY_dpp32 F8(DPP32) F8(DPP32)
+#define BODY_and32 F8(AND32) F8(AND32)
+#define BODY_lshladd32 F8(LSHLADD32) F8(LSHLADD32)
+#define BODY_bfi32 F8(BFI32) F8(BFI32)
+#define BODY_fma32 F8(FMA32) F8(FMA32)
+#define BODY_cnd32 F8(CND32) F8(CND32)
+// mixes (16 instructions each)
+#define BODY_fma64_dpp32 D8(FMA64) F8(DPP32)
+#define BODY_fma64_and32 D8(FMA64) F8(AND32)
+#define BODY_fma64_bfi32 D8(FMA64) F8(BFI32)
+#define BODY_fma64x3_dpp32 FMA64(d0) FMA64(d1) FMA64(d2) DPP32(f0) FMA64(d3) FMA64(d4) FMA64(d5) DPP32(f1) \
+    FMA64(d6) FMA64(d7) FMA64(d0) DPP32(f2) FMA64(d1) FMA64(d2) FMA64(d3) DPP32(f3)
+#define BODY_rsq64_fma64x7 RSQ64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d4) FMA64(d5) FMA64(d6) FMA64(d7) \
+    RSQ64(d1) FMA64(d0) FMA64(d2) FMA64(d3) FMA64(d4) FMA64(d5) FMA64(d6) FMA64(d7)
+// dependent pairs: 4 chains of fma64 (ILP 4) and 2 chains (ILP 2)
+#define BODY_fma64_ilp4 FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) \
+    FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3)
+#define BODY_fma64_ilp2 FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1) \
+    FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1) FMA64(d0) FMA64(d1)
+#define BODY_fma64_ilp1 FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) \
+    FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0)
+
+#define KERNEL(NAME)                                                                                    \
+    __global__ __launch_bounds__(256) void k_##NAME(long long* cyc, double* out, int iters) {          \
+        double d0 = threadIdx.x, d1 = d0 + 1, d2 = d0 + 2, d3 = d0 + 3, d4 = d0 + 4, d5 = d0 + 5,       \
+               d6 = d0 + 6, d7 = d0 + 7, b = 1.0000001, c = 0.5;                                       \
+        float f0 = threadIdx.x, f1 = f0 + 1, f2 = f0 + 2, f3 = f0 + 3, f4 = f0 + 4, f5 = f0 + 5,        \
+              f6 = f0 + 6, f7 = f0 + 7, fb = 1.0000001f, fc = 0.5f;                                     \
+        int k = 0x0f0f0f0f, k2 = (int)threadIdx.x;                                                      \
+        asm volatile("s_mov_b64 vcc, -1" ::: "vcc");                                                    \
+        __syncthreads();                                                                                \
+        const long long t0 = __builtin_readcyclecounter();                                              \
+        for (int i = 0; i < iters; ++i) { BODY_##NAME }                                                 \
+        const long long t1 = __builtin_readcyclecounter();                                              \
+        if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;                \
+        out[blockIdx.x * 256 + threadIdx.x] = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7 +                  \
+                                              (double)(f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7) + k + k2; \
+    }
+
+KERNEL(fma64) KERNEL(mul64) KERNEL(rsq64) KERNEL(rcp64) KERNEL(dpp32) KERNEL(and32) KERNEL(lshladd32)
+KERNEL(bfi32) KERNEL(fma32) KERNEL(cnd32) KERNEL(fma64_dpp32) KERNEL(fma64_and32) KERNEL(fma64_bfi32)
+KERNEL(fma64x3_dpp32) KERNEL(rsq64_fma64x7) KERNEL(fma64_ilp4) KERNEL(fma64_ilp2) KERNEL(fma64_ilp1)
+
+int main() {
+    struct K { const char* n; void (*f)(long long*, double*, int); } ks[] = {
+        {"fma64", k_fma64}, {"mul64", k_mul64}, {"rsq64", k_rsq64}, {"rcp64", k_rcp64},
+        {"dpp32", k_dpp32}, {"and32", k_and32}, {"lshladd32", k_lshladd32}, {"bfi32", k_bfi32},
+        {"fma32", k_fma32}, {"cnd32", k_cnd32}, {"fma64+dpp32 (1:1)", k_fma64_dpp32},
+        {"fma64+and32 (1:1)", k_fma64_and32}, {"fma64+bfi32 (1:1)", k_fma64_bfi32},
+        {"fma64x3+dpp32 (3:1)", k_fma64x3_dpp32}, {"rsq64+fma64x7 (1:7)", k_rsq64_fma64x7},
+        {"fma64 ILP4", k_fma64_ilp4}, {"fma64 ILP2", k_fma64_ilp2}, {"fma64 ILP1", k_fma64_ilp1}};
+    const int cus = 256, iters = 2048;
+    long long* cyc;
+    double* out;
+    hipMalloc(&cyc, cus * 4 * 4 * sizeof(long long));
+    hipMalloc(&out, cus * 4 * 256 * sizeof(double));
+    std::vector<long long> h(cus * 4 * 4);
+    printf("cycles per wave-instruction per SIMD (s_memtime; median over waves; 16 instr x %d iters per wave)\n", iters);
+    printf("%-22s %8s %8s %8s %8s\n", "body", "W=1", "W=2", "W=3", "W=4");
+    for (auto& k : ks) {
+        printf("%-22s", k.n);
+        for (int W = 1; W <= 4; ++W) {
+            const int blocks = cus * W;
+            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, cyc, out, 64);  // warm
+            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, cyc, out, iters);
+            hipMemcpy(h.data(), cyc, (size_t)blocks * 4 * sizeof(long long), hipMemcpyDeviceToHost);
+            std::vector<long long> v(h.begin(), h.begin() + blocks * 4);
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            const double per = (double)v[v.size() / 2] / ((double)W * iters * 16);
+            printf(" %8.2f", per);
+        }
+        printf("\n");
+    }
+    return 0;
+}
