@@ -156,6 +156,133 @@ def cpu_baseline(coords, values, nbr_host, kind, theta, budget_s, F_gpu):
     }
 
 
+def synth_gibbs_field(n, seed, sigma2, phi, tau2, beta, dev, features=2048):
+    """Synthetic response data for the Gibbs preset: y = X beta + w + e on uniform [0,1]^2
+    coordinates, w a stationary exponential-covariance GP field (sigma2, phi) drawn with random
+    Fourier features (2-D exponential spectral density: omega = phi z / |g|, z ~ N(0, I_2),
+    g ~ N(0, 1)), e ~ N(0, tau2), X = [1, N(0,1)].  Generated on the GPU in chunks; a
+    spatially structured field keeps the chain in the regime config 5 describes."""
+    rng = np.random.default_rng(seed)
+    coords = rng.uniform(0.0, 1.0, (n, 2))
+    omega = phi * rng.standard_normal((2, features)) / np.abs(rng.standard_normal(features))
+    bias = rng.uniform(0.0, 2 * np.pi, features)
+    x1 = rng.standard_normal(n)
+    noise = rng.standard_normal(n)
+    c = torch.from_numpy(coords).to(dev)
+    om, b = torch.from_numpy(omega).to(dev), torch.from_numpy(bias).to(dev)
+    w = torch.empty(n, dtype=torch.float64, device=dev)
+    for a in range(0, n, 65536):
+        w[a:a + 65536] = torch.cos(c[a:a + 65536] @ om + b).sum(dim=1)
+    w *= np.sqrt(2.0 * sigma2 / features)
+    wh = w.cpu().numpy()
+    X = np.column_stack([np.ones(n), x1])
+    y = X @ np.asarray(beta) + wh + np.sqrt(tau2) * noise
+    return coords, X, y, wh
+
+
+def run_gibbs(args, dev, rank, world, distributed, json_fd):
+    """BASELINE config 5: the Gibbs sampler (SeqNNGP) at N = 1e6, m = 15 -- one chain per GPU
+    ("replicas only": the w sweep's per-colour halo exchange would cost more than the sweep at this
+    N); a step = one full iteration (phi MH with its fused B/F sweep, sigma2, the
+    colour-ordered w sweep, tau2, beta)."""
+    from pynngp_amd import Priors, SeqNNGP
+
+    n = args.n
+    m = args.m
+    sigma2, phi, tau2, beta = 1.0, 30.0, 0.1, (1.0, -0.5)
+    coords, X, y, _ = synth_gibbs_field(n, 5, sigma2, phi, tau2, beta, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
+                seed=1 + rank, device=dev)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    for _ in range(args.warmup):
+        g.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the fused B/F sweep of one phi proposal, timed on its own (HIP events on the launch stream),
+    # and the colour-ordered w sweep: their shares of an iteration
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record(stream)
+    for _ in range(reps):
+        g._sweep_into(g.phi, g._B2, g._Ft2, g._r2)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    sweep_ms = e0.elapsed_time(e1) / reps
+    w_save, r_save = g.w.clone(), g.r.clone()
+    e0.record(stream)
+    for _ in range(reps):
+        g.update_wt()
+        g.update_ws()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wsweep_ms = e0.elapsed_time(e1) / reps
+    g.w.copy_(w_save)
+    g.r.copy_(r_save)
+    ms_iter = 1e3 * elapsed / args.steps
+    if rank == 0:
+        bpl = bytes_per_location(m) + 8  # + the residual r written for the sampler
+        achieved = bpl * n / (sweep_ms * 1e-3)
+        out = {
+            "metric": "NNGP Gibbs sampler iterations/sec (BASELINE config 5: N=1M, m=15, 1,000 sweeps; one chain "
+                      "per GPU)",
+            "value": world * args.steps / elapsed,
+            "unit": "chain-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_iter,
+            "iterations_per_s_per_chain": args.steps / elapsed,
+            "locations_per_s": world * n * args.steps / elapsed,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: uniform [0,1]^2 coords, y = X beta + w + e, w an exponential GP field (sigma2=1, "
+                    "phi=30; random Fourier features), tau2=0.1, beta=(1, -0.5)",
+            "config": {
+                "workload": f"BASELINE config 5: SeqNNGP Gibbs sampler, N={n} per chain, m={m}, exponential, "
+                            f"{args.steps} timed iterations after {args.warmup} warm-up",
+                "n_per_gpu": n, "m": m, "kind": "exponential", "chains": world,
+                "parallelism": f"replicas x{world} (one independent chain per GPU)",
+            },
+            "breakdown": {
+                "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
+                "w_sweep_ms": wsweep_ms, "w_sweep_share": wsweep_ms / ms_iter, "n_colors": int(g.n_colors),
+                "phi_accept_rate": g.n_accept / max(1, g.iteration), "setup_s": setup_s,
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": "fused B/F + residual sweep of a phi proposal",
+                "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                "traffic": None, "algorithmic_bytes_per_location": bpl, "kernel_ms": sweep_ms, "kernel_rows": n,
+            },
+            "state": {"phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "beta": list(map(float, g.beta))},
+            "lib": os.path.relpath(_lib.LIB_PATH, ROOT),
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            F_gpu = g.Ft.cpu().numpy()
+            out["cpu_baseline"] = cpu_baseline(g.coords.cpu().numpy(), g.w.cpu().numpy(), g.nbr.cpu().numpy(),
+                                               "exponential", (1.0, g.phi, 0.0), args.cpu_seconds, F_gpu)
+            out["cpu_baseline"]["sample"] += " -- the B/F + log-lik sweep of one phi proposal (no CPU Gibbs sampler)"
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+
+
 def main():
     # The result must be the only line on stdout: libraries (RCCL prints a version
     # banner at communicator creation) write to fd 1 too, so point fd 1 at stderr
@@ -164,14 +291,15 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=None,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
                     help="BASELINE.json config preset: 2 = N=1e5, m=15, Matern-3/2 (tau2=0.1); 3 = the headline "
-                         "(default flags); 4 = N=1e7 / world per GPU, m=20, exponential")
+                         "(default flags); 4 = N=1e7 / world per GPU, m=20, exponential; 5 = the Gibbs sampler "
+                         "(SeqNNGP, N=1e6, m=15, 1,000 iterations after 100 warm-up, one chain per GPU)")
     # defaults: the GPU clock settles over the first ~50 ms of sustained load (the sweep
     # kernel goes from ~218 to ~187 us over its first ~200 launches), so the
     # default warm-up is 200 sweeps; both still finish in well under a second
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 200; config 5: 1,000 iterations)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200; config 5: 100)")
     ap.add_argument("--n", "--n-per-gpu", dest="n", type=int, default=1_000_000, help="locations per GPU")
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=list(_lib.KIND_CODES))
@@ -194,6 +322,10 @@ def main():
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 1000 if args.config == 5 else 200
+    if args.warmup is None:
+        args.warmup = 100 if args.config == 5 else 200
     if args.config == 2:
         args.n, args.m, args.kind, args.theta = 100_000, 15, "matern32", "1.0,17.320508075688772,0.1"
     elif args.config == 4:
@@ -223,6 +355,12 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+
+    if args.config == 5:
+        run_gibbs(args, dev, rank, world, distributed, json_fd)
+        if distributed:
+            dist.destroy_process_group()
+        return
 
     sigma2, phi, tau2 = (float(x) for x in args.theta.split(","))
     cov = Covariance(args.kind, sigma2, phi, tau2)

@@ -420,6 +420,24 @@ class SeqNNGP:
         self.sum_logF, self.quad = float(ph[0]), float(ph[1])
 
     # ------------------------------------------------------------------ checkpoint / resume
+    def _settings(self) -> dict:
+        return {"algo": self.algo, "phi_tuning": self.phi_tuning, "fix_tau2": self.fix_tau2,
+                "priors": {k: list(v) for k, v in dataclasses.asdict(self.priors).items()},
+                "n_t": self.n_t, "n_obs": self.n_obs, "n_colors": int(self.n_colors)}
+
+    def _fingerprint(self) -> str:
+        """sha256 over the sampler's data (coordinates, responses, covariates, noise weights,
+        neighbour sets, all in storage order) and settings: a checkpoint resumes only into a
+        sampler built on the same inputs."""
+        import hashlib
+        import json
+
+        h = hashlib.sha256()
+        for t in (self.coords, self.y, self.X, self.nbr, self.noise_w):
+            h.update(b"none" if t is None else t.contiguous().cpu().numpy().tobytes())
+        h.update(json.dumps(self._settings(), sort_keys=True).encode())
+        return h.hexdigest()
+
     def save(self, path) -> None:
         """Checkpoint the chain: w and the maintained residuals r in node order,
         beta, sigma2, tau2, phi, the partial sums, the iteration counter (the Philox key of
@@ -430,12 +448,17 @@ class SeqNNGP:
         meta = {"n": self.n, "n_s": self.n_s, "m": self.m, "kind": self.kind, "p": self.p, "seed": self.seed,
                 "iteration": self.iteration, "n_accept": self.n_accept, "n_notpd_reject": self.n_notpd_reject,
                 "sigma2": self.sigma2, "tau2": self.tau2, "phi": self.phi, "sum_logF": self.sum_logF,
-                "quad": self.quad, "rng": self.rng.bit_generator.state}
+                "quad": self.quad, "rng": self.rng.bit_generator.state, "settings": self._settings(),
+                "fingerprint": self._fingerprint()}
         np.savez(path, w=self.w[self.pos].cpu().numpy(), r=self.r[self.pos].cpu().numpy(), beta=np.asarray(self.beta),
                  y_unobserved=self.y_unobserved.cpu().numpy(), meta=np.array(json.dumps(meta)))
 
     def restore(self, path) -> "SeqNNGP":
-        """Resume from :meth:`save` (the sampler must be built on the same data and settings)."""
+        """Resume from :meth:`save`.  The sampler must be built on the same data and settings:
+        sizes, kind and seed are compared one by one, then a fingerprint of the coordinates,
+        responses, covariates, noise weights, neighbour sets, algo, phi_tuning, fix_tau2 and
+        priors; any mismatch raises ValueError (the running residuals r would otherwise be
+        inconsistent with w and B)."""
         import json
 
         with np.load(path, allow_pickle=False) as z:
@@ -443,6 +466,13 @@ class SeqNNGP:
             for k in ("n", "n_s", "m", "kind", "p", "seed"):
                 if meta[k] != getattr(self, k):
                     raise ValueError(f"checkpoint {k}={meta[k]!r} does not match this sampler's {getattr(self, k)!r}")
+            mine = self._settings()
+            for k, v in meta.get("settings", {}).items():
+                if mine.get(k) != v:
+                    raise ValueError(f"checkpoint setting {k}={v!r} does not match this sampler's {mine.get(k)!r}")
+            if meta.get("fingerprint") != self._fingerprint():
+                raise ValueError("checkpoint was written by a sampler built on different data (coordinates, "
+                                 "responses, covariates, noise weights or neighbour sets) or settings")
             to = lambda a: torch.as_tensor(a).to(self.device)  # noqa: E731
             self.w = to(z["w"])[self.perm].contiguous()
             r = to(z["r"])[self.perm].contiguous()

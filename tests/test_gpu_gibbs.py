@@ -287,3 +287,43 @@ def test_seqnngp_config5_scale_stationary(dev):
     assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.9
     print(f"N=1e6 chain: sigma2 {res['sigma2'].mean():.4f} tau2 {res['tau2'].mean():.4f} "
           f"phi {res['phi'].mean():.3f} beta {res['beta'].mean(0)} accept {res['phi_accept_rate']:.2f}")
+
+
+@pytest.mark.timeout(300)
+def test_seqnngp_config5_cold_start_1000_sweeps(dev):
+    """Config 5 as BASELINE states it (N = 1e6, m = 15, 1,000 Gibbs sweeps) from a COLD start:
+    w from the reference's initialiser (_init_ws, nngp.py:45-47: the uniform 5-NN mean of y),
+    sigma2 and tau2 started 2x too large and phi 2x too small.  The field is drawn exactly from
+    the NNGP at the generating values (oracle_nngp_simulate).  After 500 burn-in sweeps the
+    posterior means must sit near the generating values: tau2 and the slope within 10 % / 0.02,
+    the microergodic sigma2 * phi (the combination an exponential field identifies in a fixed
+    domain) within 10 %, sigma2 and phi each within 30 %, and the latent mean must track w."""
+    from oracle import nngp_oracle as O
+    from pynngp_amd import Priors, SeqNNGP, _lib
+
+    n, m = 1_000_000, 15
+    sigma2, phi, tau2, beta = 1.0, 30.0, 0.1, np.array([1.0, -0.5])
+    rng = np.random.default_rng(56)
+    c = rng.uniform(size=(n, 2))
+    ct = torch.from_numpy(c).to(dev)
+    nbr = _lib.knn_prior(ct, m)
+    B, F, _ = _lib.bf_sweep(ct, nbr, 0, "exponential", sigma2, phi, 0.0)
+    w = O.c_nngp_simulate(nbr.cpu().numpy(), B.cpu().numpy(), F.cpu().numpy(), rng.standard_normal(n))
+    X = np.column_stack([np.ones(n), rng.standard_normal(n)])
+    y = X @ beta + w + np.sqrt(tau2) * rng.standard_normal(n)
+    # the reference's ws: KNeighborsRegressor(n_neighbors=5, weights='uniform').fit(t, y).predict(s), S = T
+    idx = _lib.knn_query(ct, ct, 5).long()
+    w0 = torch.from_numpy(y).to(dev)[idx].mean(dim=1).cpu().numpy()
+    pri = Priors(sigma2_ig=(2.0, 1.0), tau2_ig=(2.0, 0.1), phi_unif=(1.0, 100.0))
+    s = SeqNNGP(c, y, X, m=m, priors=pri, sigma2=2 * sigma2, tau2=2 * tau2, phi=phi / 2, phi_tuning=0.01, seed=10,
+                device=dev, w_init=w0)
+    res = s.sample(1000, burn=500, keep_w_mean=True)
+    s2, ph, t2 = res["sigma2"].mean(), res["phi"].mean(), res["tau2"].mean()
+    print(f"cold start, N=1e6, 1000 sweeps: sigma2 {s2:.4f} phi {ph:.3f} sigma2*phi {(res['sigma2'] * res['phi']).mean():.3f} "
+          f"tau2 {t2:.4f} beta {res['beta'].mean(0)} accept {res['phi_accept_rate']:.2f}")
+    assert 0.02 < res["phi_accept_rate"] < 0.95
+    assert abs(t2 / tau2 - 1) < 0.10
+    assert abs(res["beta"][:, 1].mean() - beta[1]) < 0.02
+    assert abs((res["sigma2"] * res["phi"]).mean() / (sigma2 * phi) - 1) < 0.10
+    assert abs(s2 / sigma2 - 1) < 0.30 and abs(ph / phi - 1) < 0.30
+    assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.9

@@ -189,6 +189,17 @@ def test_checkpoint_resume_bit_identical(dev, tmp_path, with_ref):
     np.testing.assert_array_equal(a.beta, b.beta)
     with pytest.raises(ValueError, match="m="):
         SeqNNGP(t, y, **{**kw, "m": 6}).restore(tmp_path / "ck.npz")
+    # same sizes, different data or settings: refused (the running residuals would not match)
+    y2 = y.copy()
+    y2[np.nonzero(np.isfinite(y2))[0][0]] += 1.0
+    with pytest.raises(ValueError, match="different data"):
+        SeqNNGP(t, y2, **kw).restore(tmp_path / "ck.npz")
+    t2 = t.copy()
+    t2[5] += 1e-3
+    with pytest.raises(ValueError, match="different data"):
+        SeqNNGP(t2, y, **kw).restore(tmp_path / "ck.npz")
+    with pytest.raises(ValueError, match="phi_tuning"):
+        SeqNNGP(t, y, **{**kw, "phi_tuning": 0.3}).restore(tmp_path / "ck.npz")
 
 
 def test_reference_set_rejects_repeated_points(dev):

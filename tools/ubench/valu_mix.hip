@@ -3,9 +3,10 @@
 // (is a 32-bit op -- DPP move, bfi, lshl_add -- 2 cycles across waves
 // while fp64 is 4?).  Each kernel runs 8 independent chains (ILP 8) of a 16-instruction
 // body; every wave times itself with s_memtime (shader clock, so DVFS does not enter) and
-// the report is cycles per wave-instruction per SIMD = elapsed / (W * instructions per
-// wave), median over waves.  Blocks of 256 threads (one wave per SIMD of a CU), 256 * W
-// blocks, so every SIMD holds W waves for the whole run.
+// the report is cycles per wave-instruction per SIMD = block elapsed (first start to last end
+// of its waves) / (W * instructions per wave), median over blocks.  One block of 256 W threads
+// per CU (each block allocates 96 KB of LDS, so no CU holds two): the block's waves are dealt
+// round-robin over the CU's 4 SIMDs, so every SIMD holds exactly W waves for the whole run.
 //   hipcc --offload-arch=gfx950 -O3 tools/ubench/valu_mix.hip -o tools/ubench/valu_mix
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -55,7 +56,8 @@
     FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0) FMA64(d0)
 
 #define KERNEL(NAME)                                                                                    \
-    __global__ __launch_bounds__(256) void k_##NAME(long long* cyc, double* out, int iters) {          \
+    __global__ __launch_bounds__(1024) void k_##NAME(long long* cyc, double* out, int iters) {         \
+        extern __shared__ double lds_pad[];                                                             \
         double d0 = threadIdx.x, d1 = d0 + 1, d2 = d0 + 2, d3 = d0 + 3, d4 = d0 + 4, d5 = d0 + 5,       \
                d6 = d0 + 6, d7 = d0 + 7, b = 1.0000001, c = 0.5;                                       \
         float f0 = threadIdx.x, f1 = f0 + 1, f2 = f0 + 2, f3 = f0 + 3, f4 = f0 + 4, f5 = f0 + 5,        \
@@ -66,8 +68,12 @@
         const long long t0 = __builtin_readcyclecounter();                                              \
         for (int i = 0; i < iters; ++i) { BODY_##NAME }                                                 \
         const long long t1 = __builtin_readcyclecounter();                                              \
-        if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;                \
-        out[blockIdx.x * 256 + threadIdx.x] = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7 +                  \
+        if ((threadIdx.x & 63) == 0) {                                                                  \
+            cyc[2 * (blockIdx.x * 16 + (threadIdx.x >> 6))] = t0;                                       \
+            cyc[2 * (blockIdx.x * 16 + (threadIdx.x >> 6)) + 1] = t1;                                   \
+        }                                                                                               \
+        if (threadIdx.x == 0) lds_pad[0] = d0;                                                          \
+        out[blockIdx.x * 1024 + threadIdx.x] = d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7 +                 \
                                               (double)(f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7) + k + k2; \
     }
 
@@ -84,24 +90,34 @@ int main() {
         {"fma64x3+dpp32 (3:1)", k_fma64x3_dpp32}, {"rsq64+fma64x7 (1:7)", k_rsq64_fma64x7},
         {"fma64 ILP4", k_fma64_ilp4}, {"fma64 ILP2", k_fma64_ilp2}, {"fma64 ILP1", k_fma64_ilp1}};
     const int cus = 256, iters = 2048;
+    const size_t lds = 96 * 1024;
     long long* cyc;
     double* out;
-    hipMalloc(&cyc, cus * 4 * 4 * sizeof(long long));
-    hipMalloc(&out, cus * 4 * 256 * sizeof(double));
-    std::vector<long long> h(cus * 4 * 4);
-    printf("cycles per wave-instruction per SIMD (s_memtime; median over waves; 16 instr x %d iters per wave)\n", iters);
+    (void)hipMalloc(&cyc, cus * 16 * 2 * sizeof(long long));
+    (void)hipMalloc(&out, cus * 1024 * sizeof(double));
+    std::vector<long long> h(cus * 16 * 2);
+    printf("cycles per wave-instruction per SIMD (s_memtime; one block per CU, W waves per SIMD; median over "
+           "blocks; 16 instr x %d iters per wave)\n", iters);
     printf("%-22s %8s %8s %8s %8s\n", "body", "W=1", "W=2", "W=3", "W=4");
     for (auto& k : ks) {
+        (void)hipFuncSetAttribute((const void*)k.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         printf("%-22s", k.n);
         for (int W = 1; W <= 4; ++W) {
-            const int blocks = cus * W;
-            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, cyc, out, 64);  // warm
-            hipLaunchKernelGGL(k.f, dim3(blocks), dim3(256), 0, 0, cyc, out, iters);
-            hipMemcpy(h.data(), cyc, (size_t)blocks * 4 * sizeof(long long), hipMemcpyDeviceToHost);
-            std::vector<long long> v(h.begin(), h.begin() + blocks * 4);
-            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
-            const double per = (double)v[v.size() / 2] / ((double)W * iters * 16);
-            printf(" %8.2f", per);
+            const int threads = 256 * W, waves = 4 * W;
+            hipLaunchKernelGGL(k.f, dim3(cus), dim3(threads), lds, 0, cyc, out, 64);  // warm
+            hipLaunchKernelGGL(k.f, dim3(cus), dim3(threads), lds, 0, cyc, out, iters);
+            (void)hipMemcpy(h.data(), cyc, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+            std::vector<double> per;
+            for (int b = 0; b < cus; ++b) {
+                long long lo = h[2 * (b * 16)], hi = h[2 * (b * 16) + 1];
+                for (int w = 1; w < waves; ++w) {
+                    lo = std::min(lo, h[2 * (b * 16 + w)]);
+                    hi = std::max(hi, h[2 * (b * 16 + w) + 1]);
+                }
+                per.push_back((double)(hi - lo) / ((double)W * iters * 16));
+            }
+            std::nth_element(per.begin(), per.begin() + per.size() / 2, per.end());
+            printf(" %8.2f", per[per.size() / 2]);
         }
         printf("\n");
     }
