@@ -45,14 +45,14 @@ extern "C" {
 #define NNGP_COV_GAUSSIAN 3    /* sigma2 exp(-u^2)                                  */
 #define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
 
-/* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE and QUAD
- * serve 2-D exponential / Matern-3/2 only, PAIRB and WAVE every kind and dimension.  (3 and 7
- * were comparison-only kernels of earlier builds; they are rejected as unknown.) */
-#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 32; wave above                              */
+/* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE serves 2-D
+ * exponential / Matern-3/2 only, PAIRB, QUAD and WAVE every kind and dimension.  (3 and 7 were
+ * comparison-only kernels of earlier builds; they are rejected as unknown.) */
+#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above              */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
 #define NNGP_ALGO_QUAD 4  /* four lanes per location (25 <= m <= 32)                         */
-#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 32)              */
+#define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 24)              */
 
 /* the kernel NNGP_ALGO_AUTO (or an explicit code, returned as is) resolves to for (m, kind, dim) */
 int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim);

@@ -62,15 +62,21 @@ __device__ __forceinline__ double grp_sum(double v) {
     return v;
 }
 
-template <int M, int KIND, int P>
-__global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coords, int64_t n_points,
+// D = 2: 2-D ordinates (one 16-byte load per point); D = 0: runtime dimension 1..3 held as three
+// coordinates, with KIND = NNGP_KIND_GENERIC the runtime-kind covariance (nngp_math.h) -- the
+// m = 25..32 kernels for every kind and dimension
+template <int M, int KIND, int P, int D = 2>
+__global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0,
-                                                const CovParams Pc, const double* __restrict__ values, const double2* __restrict__ qcoords, const double* __restrict__ qvalues,
+                                                const CovParams Pc, const double* __restrict__ values, const double* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                 double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double* __restrict__ bpart) {
+                                                double* __restrict__ bpart, int dim) {
+    static_assert(D == 0 || D == 2, "bf_group: 2-D or runtime dimension");
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
+    constexpr int DA = point_arity<D>();
+    const int ds = D == 0 ? dim : 2;
     __shared__ double etab[NNGP_EXP_TAB_N];
     nngp_exp_table_load(etab, Pc.sigma2);
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -92,7 +98,7 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
         const int a = P * s + q;
         jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
     }
-    double ox[S], oy[S], z[S];
+    double o[S][DA], z[S];
     bool oval[S];
     bool bad_index = false;
 #pragma unroll
@@ -103,24 +109,22 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
         bad_index |= j != -1 && !in_range;
         oval[s] = in_range;
         const bool self = a == M;
-        const double2* pc = self ? qcoords + i : (in_range ? coords + j : kFarPoints + (a & 63));
+        const double* pc = self ? qcoords + i * ds : (in_range ? coords + (int64_t)j * ds : far_point<DA>(a));
         const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                 : ((values != nullptr && in_range) ? values + j : kZeroValue);
-        const double2 x = *pc;
-        ox[s] = x.x;
-        oy[s] = x.y;
+        if constexpr (D == 0) load_point_rt(pc, dim, o[s]);
+        else load_point<D>(pc, o[s]);
         z[s] = *pv;
     }
 
     // ---- joint block rows: R[s][b], b < min(P*s + P, NR)
     double R[S][NR];
     {
-        double X[NR], Y[NR];
+        double X[NR][DA];
 #pragma unroll
-        for (int b = 0; b < NR; ++b) {
-            X[b] = grp_bcast<P>(ox[b / P], b % P);
-            Y[b] = grp_bcast<P>(oy[b / P], b % P);
-        }
+        for (int b = 0; b < NR; ++b)
+#pragma unroll
+            for (int k = 0; k < DA; ++k) X[b][k] = grp_bcast<P>(o[b / P][k], b % P);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int a = P * s + q;
@@ -128,9 +132,9 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
             for (int b = 0; b < NR; ++b) {
                 if (b >= P * s + P) continue;  // beyond this local row's width
                 if (b < P * s) {
-                    R[s][b] = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], X[b], Y[b]));
+                    R[s][b] = nngp_cov_d2<KIND>(Pc, etab, point_d2<DA>(o[s], X[b]));
                 } else if (b < P * s + P - 1) {  // diagonal block: lane-dependent
-                    const double c = nngp_cov_d2<KIND>(Pc, etab, nngp_d2(ox[s], oy[s], X[b], Y[b]));
+                    const double c = nngp_cov_d2<KIND>(Pc, etab, point_d2<DA>(o[s], X[b]));
                     R[s][b] = b < a ? c : (b == a ? Pc.diag : 0.0);
                 } else {
                     R[s][b] = b == a ? Pc.diag : 0.0;
@@ -216,21 +220,24 @@ __global__ __launch_bounds__(256) void bf_group(const double2* __restrict__ coor
     block_partials_store(lf, qq, badp, badi, bpart, blk);
 }
 
-template <int M, int KIND, int P>
+template <int M, int KIND, int P, int D = 2>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
-    hipLaunchKernelGGL((bf_group<M, KIND, P>), dim3((unsigned)blocks), dim3(256), 0, s, (const double2*)a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.values, (const double2*)a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart);
+    hipLaunchKernelGGL((bf_group<M, KIND, P, D>), dim3((unsigned)blocks), dim3(256), 0, s, a.coords, a.n_points, a.nbr,
+                       a.order, a.n_rows, a.i0, Pc, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart, a.dim);
 }
 
-// instantiate both kinds for one (M, P); returns false for other m
+// one (M, P): the 2-D exponential / Matern-3/2 kernels, and one runtime-kind, runtime-dimension
+// kernel for the other kinds and dimensions; returns false for other m
 template <int M, int P>
 static bool launch_group_if(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     if (a.m != M) return false;
-    if (a.kind == 1)
+    if (a.dim == 2 && a.kind == 1)
         launch_group_mkp<M, 1, P>(a, Pc, s);
-    else
+    else if (a.dim == 2 && a.kind == 0)
         launch_group_mkp<M, 0, P>(a, Pc, s);
+    else
+        launch_group_mkp<M, NNGP_KIND_GENERIC, P, 0>(a, Pc, s);
     return true;
 }
 

@@ -1,5 +1,6 @@
 // Dispatch for the four-lanes-per-location sweep kernels at m = 25..32 (template in bf_group.h,
-// instantiations in bf_quad_b.hip / bf_quad_c.hip; 2-D exponential and Matern-3/2 only).  The
+// instantiations in bf_quad_b.hip / bf_quad_c.hip: 2-D exponential and Matern-3/2, and one runtime-
+// kind, runtime-dimension kernel per m for the rest).  The
 // two-lane bf_group and the m <= 20 four-lane instantiations were comparison points of the
 // blocked pair kernel (bf_pairb.h) and are no longer built into the library.
 #include "bf_group.h"

@@ -85,6 +85,33 @@ namespace nngp {
 #ifndef NNGP_PAIRB_SLDL_MAX
 #define NNGP_PAIRB_SLDL_MAX 17
 #endif
+// NNGP_PAIRB_ZLDS_MIN: from this m the neighbour values wait in LDS between the gathers and the
+// residual (they are read only there): NP doubles of registers per lane less where the two-wave
+// register budget is tight.
+#ifndef NNGP_PAIRB_ZLDS_MIN
+#define NNGP_PAIRB_ZLDS_MIN 99
+#endif
+// Left-looking elimination (bit m of NNGP_PAIRB_LEFT_MASK): column pair by column pair, each
+// column's covariances evaluated when it is reached and updated from the finished columns, so the
+// trailing block and every coordinate are never live at once; the finished factor rows
+// 0..KL-1 wait in LDS for the back-substitution.  The register peak is the factor's later rows
+// instead of the whole joint block plus coordinates: m = 19, 20, 22 run at two waves per SIMD
+// (right-looking: one; 0.352 / 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows,
+// profiles/r03e); from m = NNGP_PAIRB_LEFT_ONE_WAVE_MIN the left-looking kernel runs at one wave
+// with more rows in LDS (its peak no longer fits 256 registers).
+#ifndef NNGP_PAIRB_LEFT_MASK
+#define NNGP_PAIRB_LEFT_MASK ((1ull << 19) | (1ull << 20) | (1ull << 22))
+#endif
+#ifndef NNGP_PAIRB_LEFT_ONE_WAVE_MIN
+#define NNGP_PAIRB_LEFT_ONE_WAVE_MIN 23
+#endif
+#ifndef NNGP_PAIRB_LEFT_LDS_ROWS  // factor rows in LDS at two waves per SIMD (5: 123 KB of 160 per CU)
+#define NNGP_PAIRB_LEFT_LDS_ROWS 5
+#endif
+#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_1W  // ... and at one wave per SIMD (8: 147 KB)
+#define NNGP_PAIRB_LEFT_LDS_ROWS_1W 8
+#endif
+constexpr bool pairb_left(int m) { return ((unsigned long long)(NNGP_PAIRB_LEFT_MASK) >> m) & 1ull; }
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
 #define NNGP_PHASE(name)                        \
@@ -137,8 +164,10 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 #define NNGP_PAIRB_THREE_WAVES_MAX 13
 #endif
 #define NNGP_PAIRB_ATTR                                                                              \
-    __attribute__((amdgpu_waves_per_eu((M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : M <= NNGP_PAIRB_TWO_WAVES_MAX ? 2 : 1), \
-                                       (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : 2))))
+    __attribute__((amdgpu_waves_per_eu(                                                                 \
+        (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3                                                             \
+         : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_left(M) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
+        (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : 2))))
 
 // Threads per block (one tile of kPairbThreads / 2 locations per block).  256 measured fastest:
 // 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
@@ -216,8 +245,15 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
-    constexpr bool NOZ = NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX);
-    constexpr bool SLDL = NNGP_PAIRB_SLDL && NOZ && (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
+    constexpr bool LEFT = pairb_left(M);
+    constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
+    constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
+                          (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
+    constexpr int KL0 = M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W : NNGP_PAIRB_LEFT_LDS_ROWS;
+    constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
+    __shared__ double lrow[KL > 0 ? KL * (KL + 1) : 1][KL > 0 ? kPairbThreads : 1];
+    constexpr bool ZLDS = NOZ && M >= NNGP_PAIRB_ZLDS_MIN;
+    __shared__ double zsh[ZLDS ? NP : 1][ZLDS ? kPairbThreads : 1];
     __shared__ double etab[NNGP_EXP_TAB_N];
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)
@@ -273,7 +309,11 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                     : ((values != nullptr && in_range) ? values + j : kZeroValue);
             if constexpr (D == 0) load_point_rt(pc, dim, o[s]);
             else load_point<D>(pc, o[s]);
-            z[s] = *pv;
+            if constexpr (!LEFT) z[s] = *pv;  // (the left-looking kernel gathers the values late)
+        }
+        if constexpr (ZLDS) {
+#pragma unroll
+            for (int s = 0; s < NP; ++s) zsh[s][threadIdx.x] = z[s];  // read back by this thread only
         }
         const bool bad_index = (int64_t)jmax >= n_points || jmin < -1;
 
@@ -285,9 +325,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
         __syncthreads();
 
+        double R[NP][NP][2];
+        bool bad = false;
+        double Fu, res;
+        if constexpr (!LEFT) {
         NNGP_PHASE(covariances);
         // ---- unit-variance covariances in own-parity-first order
-        double R[NP][NP][2];
         {
             double p[NP][DA];
 #pragma unroll
@@ -331,7 +374,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         // (both lanes), rows s > t hold their panel entries (L[a][2t+q], L[a][2t+1-q]) and z[t]
         // the forward-solved value of row 2t+q.
         NNGP_PHASE(elimination);
-        bool bad = false;
         if constexpr (SLDL) {
             // 2x2-blocked scalar-pivot LDL^T: per pair t the pivots d00 and e11 = d11 - l d10 (l =
             // d10 / d00) need a reciprocal each instead of an inverse square root.  Each later row's
@@ -429,7 +471,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         NNGP_PHASE(lastpair);
         // ---- last pair: (M-1, M) for odd M (one more column), (M, padding) for even M
-        double Fu, res;
         if (M % 2 == 1 && SLDL) {
             const double a00 = pr_from0(R[T][T][0]);
             const double a11 = pr_from1(R[T][T][0]);
@@ -454,6 +495,84 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             Fu = pr_from0(R[T][T][0]);
             if constexpr (!NOZ) res = pr_from0(z[T]);
         }
+        } else {
+            // ---- left-looking 2x2-blocked Cholesky (NNGP_PAIRB_LEFT_MIN): step u evaluates column
+            // pair u's covariances for rows s >= u, subtracts the finished column pairs t < u (the
+            // same 2x2 block products as the right-looking update, reordered), factors the diagonal
+            // block and maps the panel.  Row pair u is then final; rows < KL move to LDS.
+            NNGP_PHASE(leftlooking);
+#pragma unroll
+            for (int u = 0; u < NP; ++u) {
+                double pu[DA];
+#pragma unroll
+                for (int k = 0; k < DA; ++k) pu[k] = pr_swap(o[u][k]);
+#pragma unroll
+                for (int s = u + 1; s < NP; ++s) {
+                    R[s][u][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], o[u]));
+                    R[s][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], pu));
+                }
+                R[u][u][0] = Pc.diag;
+                R[u][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
+#pragma unroll
+                for (int t = 0; t < u; ++t) {
+                    const double S0 = R[u][t][0], S1 = R[u][t][1];
+                    const double P0 = pr_swap(S0), P1 = pr_swap(S1);
+#pragma unroll
+                    for (int s = u; s < NP; ++s) {
+                        const double y0 = R[s][t][0], y1 = R[s][t][1];
+                        R[s][u][0] = fma(-y0, S0, fma(-y1, S1, R[s][u][0]));
+                        R[s][u][1] = fma(-y0, P1, fma(-y1, P0, R[s][u][1]));
+                    }
+                }
+                if (u < T) {
+                    const double a00 = pr_from0(R[u][u][0]);
+                    const double a11 = pr_from1(R[u][u][0]);
+                    const double a10 = pr_from1(R[u][u][1]);
+                    bad |= !(a00 > 0.0);
+                    const double i00 = nngp_rsqrt(a00);
+                    const double l10 = a10 * i00;
+                    const double s11 = fma(-l10, l10, a11);
+                    bad |= !(s11 > 0.0);
+                    const double i11 = nngp_rsqrt(s11);
+                    R[u][u][0] = pr_sel(q1, i11, i00);
+                    R[u][u][1] = l10;
+                    const double u01 = -(l10 * i00) * i11;
+                    const double c00 = pr_sel(q1, i11, i00), c10 = u01 * wq1;
+                    const double c01 = u01 * wq0, c11 = pr_sel(q1, i00, i11);
+#pragma unroll
+                    for (int s = u + 1; s < NP; ++s) {
+                        const double x0 = R[s][u][0], x1 = R[s][u][1];
+                        R[s][u][0] = fma(x0, c00, x1 * c10);
+                        R[s][u][1] = fma(x0, c01, x1 * c11);
+                    }
+                } else if (M % 2 == 1) {  // u = T: the pair (M-1, M)
+                    const double a00 = pr_from0(R[T][T][0]);
+                    const double a11 = pr_from1(R[T][T][0]);
+                    const double a10 = pr_from1(R[T][T][1]);
+                    bad |= !(a00 > 0.0);
+                    const double i00 = nngp_rsqrt(a00);
+                    const double l10 = a10 * i00;
+                    Fu = fma(-l10, l10, a11);
+                    R[T][T][0] = i00;
+                    R[T][T][1] = l10;
+                } else {  // u = T: the pair (M, padding)
+                    Fu = pr_from0(R[T][T][0]);
+                }
+                if (u < KL) {
+#pragma unroll
+                    for (int t = 0; t <= u; ++t) {
+                        lrow[u * (u + 1) + 2 * t][threadIdx.x] = R[u][t][0];
+                        lrow[u * (u + 1) + 2 * t + 1][threadIdx.x] = R[u][t][1];
+                    }
+                }
+            }
+        }
+        // factor entry (row pair u, column pair t, slot k) for the back-substitution (rows < KL of
+        // the left-looking factor from LDS; u, t, k are compile-time after unrolling)
+        auto RB = [&](int u, int t, int k) -> double {
+            if (u < KL) return lrow[u * (u + 1) + 2 * t + k][threadIdx.x];
+            return R[u][t][k];
+        };
         bad |= !(Fu > 0.0);
         const double F = Fu * sigma2;  // the unit-variance pivot scaled back
 
@@ -463,10 +582,24 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             constexpr int SM = M / 2;
             constexpr bool VQ1 = (M % 2) == 1;  // row M sits in lane 1
             NNGP_PHASE(backsub);
+            if constexpr (LEFT) {
+                // the values are read only by the residual: gathered here (the row's indices again,
+                // cache-warm), their latency behind the back-substitution, instead of holding NP
+                // registers through the factorisation
+#pragma unroll
+                for (int s = 0; s < NP; ++s) {
+                    const int a = 2 * s + q;
+                    const int32_t j = a < M ? nbr[rl * M + a] : -1;
+                    const bool in_range = (uint32_t)j < n32;
+                    const double* pv = a == M ? (qvalues != nullptr ? qvalues + i : kZeroValue)
+                                              : ((values != nullptr && in_range) ? values + j : kZeroValue);
+                    z[s] = *pv;
+                }
+            }
             double bown[NP];
 #pragma unroll
             for (int s = 0; s < NP; ++s) bown[s] = 0.0;
-            if (M % 2 == 1) bown[T] = R[T][T][1] * R[T][T][0];  // lane 0: B_{M-1} = L[M][M-1] / L[M-1][M-1]
+            if (M % 2 == 1) bown[T] = RB(T, T, 1) * RB(T, T, 0);  // lane 0: B_{M-1} = L[M][M-1] / L[M-1][M-1]
 #pragma unroll
             for (int t = T - 1; t >= 0; --t) {
                 // partial sums over this lane's rows b = 2u + q, 2t + 2 <= b < M
@@ -477,25 +610,25 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                     const bool row_ok = 2 * u + 1 < M;  // else only lane 0's row is a neighbour row
                     double bu = bown[u];
                     if (!row_ok) bu = q1 ? 0.0 : bu;
-                    acc0 = fma(R[u][t][0], bu, acc0);
-                    acc1 = fma(R[u][t][1], bu, acc1);
+                    acc0 = fma(RB(u, t, 0), bu, acc0);
+                    acc1 = fma(RB(u, t, 1), bu, acc1);
                 }
                 const double tot = acc0 + pr_swap(acc1);  // sum_b L[b][2t+q] B_b
                 // v_{2t+q}: row M's own-parity entry is slot [t][0] in lane M%2, slot [t][1] in the other
-                const double vrow0 = R[SM][t][0], vrow1 = R[SM][t][1];
+                const double vrow0 = RB(SM, t, 0), vrow1 = RB(SM, t, 1);
                 double v;
                 if (VQ1) {
                     v = pr_sel(q1, vrow0, pr_swap(vrow1));
                 } else {
                     v = pr_sel(q1, pr_swap(vrow1), vrow0);
                 }
-                const double l10 = R[t][t][1];
+                const double l10 = RB(t, t, 1);
                 double bx, b0;
                 if constexpr (SLDL) {  // unit factor: B_{2t+1} = v - tot, B_{2t} = v - tot - l10 B_{2t+1}
                     bx = v - tot;
                     b0 = fma(-l10, pr_swap(bx), bx);
                 } else {
-                    const double iown = R[t][t][0];
+                    const double iown = RB(t, t, 0);
                     bx = (v - tot) * iown;                     // lane 1: B_{2t+1}
                     b0 = fma(-(l10 * iown), pr_swap(bx), bx);  // lane 0: B_{2t}
                 }
@@ -510,9 +643,10 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                     if (2 * s >= M) continue;
                     double bs = bown[s];
                     if (2 * s + 1 >= M) bs = q1 ? 0.0 : bs;  // lane 1's row here is row M (or padding)
-                    acc = fma(bs, z[s], acc);
+                    acc = fma(bs, ZLDS ? zsh[s][threadIdx.x] : z[s], acc);
                 }
-                const double vi = VQ1 ? pr_from1(z[SM]) : pr_from0(z[SM]);
+                const double zm = ZLDS ? zsh[SM][threadIdx.x] : z[SM];
+                const double vi = VQ1 ? pr_from1(zm) : pr_from0(zm);
                 res = vi - (acc + pr_swap(acc));
             }
             NNGP_PHASE(stores);

@@ -380,7 +380,7 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         if (e != hipSuccess || a.partials == nullptr) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoQuad) {
-        ok = a.dim == 2 && a.kind <= 1 && bf_group_launch(a, P, 4, s);
+        ok = bf_group_launch(a, P, 4, s);
         nb = bf_group_blocks(a.n_rows, 4);
     } else {
         nb = bf_wave_blocks(a.n_rows);

@@ -27,15 +27,19 @@ int hip_fail(hipError_t e, const char* what) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// NNGP_ALGO_AUTO: the 2x2-blocked two-lane kernel (bf_pairb.h) for 1 <= m <= 32 -- fastest per m,
-// measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py; profiles/r02ap for m <= 24, since
-// its round-2 cuts it ties the one-lane kernel at m = 1, 2 and is faster from m = 3; m = 25..32:
-// DESIGN.md 4.3), every kind and dimension; one wavefront per location above.
+// NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py):
+// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking at m = 19, 20, 22) for 1 <= m <= 24
+// (profiles/r02ap, r03e: since its round-2 cuts it ties the one-lane kernel at m = 1, 2 and is
+// faster from m = 3), four lanes per location for 25..32 (profiles/r03e: 1.08-2.78 ms per 1e6 rows,
+// 1.15-1.9x faster than the blocked pair kernel spilling at one wave), one wavefront per location
+// above; every kind and dimension (the four-lane kernel has a runtime-kind, runtime-dimension
+// instantiation beside its 2-D exponential / Matern-3/2 ones).
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     (void)kind;
     (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
-    if (m >= 1 && m <= 32) return nngp::kAlgoPairB;
+    if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
+    if (m >= 25 && m <= 32) return nngp::kAlgoQuad;
     return nngp::kAlgoWave;
 }
 
@@ -95,9 +99,9 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
         return fail(NNGP_EINVAL, "unknown algo %d", algo);
     const bool classic = dim == 2 && kind <= NNGP_COV_MATERN32;
-    if ((a == nngp::kAlgoLane || a == nngp::kAlgoQuad) && !classic)
-        return fail(NNGP_EUNSUP, "the lane / quad kernels serve 2-D exponential and Matern-3/2 only "
-                                 "(kind=%d, dim=%d): use NNGP_ALGO_AUTO, PAIRB or WAVE", kind, dim);
+    if (a == nngp::kAlgoLane && !classic)
+        return fail(NNGP_EUNSUP, "the lane kernel serves 2-D exponential and Matern-3/2 only "
+                                 "(kind=%d, dim=%d): use NNGP_ALGO_AUTO, PAIRB, QUAD or WAVE", kind, dim);
     if (a == nngp::kAlgoLane && (m < 1 || m > nngp::kLaneMaxM))
         return fail(NNGP_EUNSUP, "lane kernel needs 1 <= m <= %d (m=%d)", nngp::kLaneMaxM, m);
     if (a == nngp::kAlgoQuad && !nngp::bf_group_supported(m, 4))

@@ -166,6 +166,11 @@ NNGP_FN double nngp_cov_d2(const CovParams& P, const double* tab, double d2) {
     const double x = fmin(d2, P.d2max);
     if (KIND == NNGP_KIND_GAUSSIAN) return nngp_exp_tab(P, tab, x);  // sigma2 2^(nphi256 d2 / 256)
     const double d = nngp_sqrt(x);
+    if (KIND == NNGP_KIND_GENERIC) {  // runtime kind (nngp_cov_unit's generic branch, sigma2 in the table)
+        const double e = nngp_exp_tab(P, tab, P.gauss ? x : d);
+        const double u = fmin(P.phi * d, P.umax);
+        return fma(u, fma(u, fma(u, P.c[2], P.c[1]), P.c[0]), 1.0) * e;
+    }
     if (KIND == NNGP_KIND_SPHERICAL) {
         const double u = fmin(P.phi * d, 1.0);                       // u = 1: the polynomial is exactly 0
         const double p = fma(u, fma(0.5 * u, u, -1.5), 1.0);         // 1 + u (u^2 / 2 - 3/2)

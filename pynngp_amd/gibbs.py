@@ -88,7 +88,9 @@ class SeqNNGP:
     that coincides with a point of S carries its observation on that node.  ``y`` may hold
     NaN for unobserved locations: they enter no likelihood term and get posterior-
     predictive draws (``update_y_unobserved``), as do the reference points without data
-    when their covariates are known (``X`` None = intercept, or ``X_ref``).
+    when their covariates are known (``X`` None = intercept, or ``X_ref``).  The latent state
+    starts at ``w_init`` or, by default, at the reference's initialiser (``_init_ws``,
+    nngp.py:45-47: the uniform 5-NN mean of the observed responses at every node).
     """
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
@@ -258,7 +260,13 @@ class SeqNNGP:
         self.phi_tuning = float(phi_tuning)
         self.yres = self._residual_y(self.beta)
         if w_init is None:
-            w0 = np.zeros(n)
+            # the reference's state initialisation (_init_ws, nngp.py:45-47): the uniform 5-NN mean
+            # of the observed responses at every node (KNeighborsRegressor(5).fit(t, y).predict(s));
+            # a zero start lets sigma2 | w = 0 collapse towards 0 and the chain stalls there
+            t_obs = t_dev[torch.from_numpy(np.nonzero(observed)[0]).to(dev)]
+            k = min(5, self.n_obs)
+            idx = _lib.knn_query(t_obs, coords0, k).long()
+            w0 = to(y_host[observed])[idx].mean(dim=1).cpu().numpy()
         else:
             w0 = np.asarray(w_init, dtype=np.float64).reshape(-1)
             if w0.shape != (n,):

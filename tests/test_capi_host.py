@@ -80,11 +80,11 @@ def _sweep(lib, **kw):
     (dict(dim=0), -4, "dim=0"),
     (dict(dim=4), -4, "dim=4"),
     (dict(algo=1, m=8, kind=2), -4, "2-D exponential and Matern-3/2 only"),
-    (dict(algo=4, m=26, dim=3), -4, "2-D exponential and Matern-3/2 only"),
+    (dict(algo=1, m=10, dim=3), -4, "2-D exponential and Matern-3/2 only"),
     (dict(algo=4, m=20), -4, "4-lane kernel"),
     (dict(algo=3, m=15), -1, "unknown algo"),  # the removed comparison kernels
     (dict(algo=7, m=15), -1, "unknown algo"),
-    (dict(algo=5, m=33), -4, "blocked pair kernel"),
+    (dict(algo=5, m=25), -4, "blocked pair kernel"),
     (dict(sigma2=0.0), -1, "theta"),
     (dict(phi=float("nan")), -1, "theta"),
     (dict(tau2=-1.0), -1, "theta"),
@@ -161,7 +161,7 @@ def test_resolve_algo_table(lib):
     for m in (1, 15, 20, 24, 25, 32):
         for kind in range(5):
             for dim in (1, 2, 3):
-                assert lib.nngp_resolve_algo(0, m, kind, dim) == 5
+                assert lib.nngp_resolve_algo(0, m, kind, dim) == (5 if m <= 24 else 4)
     assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
     assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
     assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1

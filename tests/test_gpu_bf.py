@@ -74,7 +74,7 @@ ALL_KINDS = ("exponential", "matern32", "matern52", "gaussian", "spherical")
 
 
 QUAD_M = tuple(range(25, 33))  # instantiated for the 4-lane kernel
-PAIRB_M = tuple(range(1, 33))  # and for the 2x2-blocked 2-lane kernel (25..32: runtime kind and dimension)
+PAIRB_M = tuple(range(1, 25))  # and for the 2x2-blocked 2-lane kernel
 
 
 @pytest.mark.parametrize("algo", ["lane", "wave", "pairb"])
@@ -115,9 +115,10 @@ def test_bf_quad_all_m(lib, dev, c_oracle, m):
                                         ("matern52", (1.0, 12.0, 0.1)), ("gaussian", (1.0, 6.0, 0.2)),
                                         ("spherical", (1.0, 8.0, 0.05))])
 @pytest.mark.parametrize("dim", [1, 2, 3])
-def test_bf_pairb_generic_m25_32(lib, dev, c_oracle, m, kind, theta, dim):
-    """m = 25..32 (one runtime-kind, runtime-dimension pairb kernel per m), every kind and
-    dimension, under algo "auto" (which must pick it, never the wavefront kernel)."""
+def test_bf_quad_generic_m25_32(lib, dev, c_oracle, m, kind, theta, dim):
+    """m = 25..32 (the four-lane kernel: 2-D exponential / Matern-3/2 instantiations, one
+    runtime-kind, runtime-dimension instantiation per m for the rest), every kind and dimension,
+    under algo "auto" (which must pick it, never the wavefront kernel)."""
     rng = np.random.default_rng(500 + m + 7 * dim)
     coords = rng.uniform(0.0, 1.0, (1500, dim))
     coords[700:705] = coords[300]
@@ -130,7 +131,7 @@ def test_auto_never_wave_below_33(lib):
     for m in range(1, 33):
         for kind in ALL_KINDS:
             for dim in (1, 2, 3):
-                assert lib.resolve_algo("auto", m, kind, dim) == "pairb", (m, kind, dim)
+                assert lib.resolve_algo("auto", m, kind, dim) == ("pairb" if m <= 24 else "quad"), (m, kind, dim)
     assert lib.resolve_algo("auto", 33, "exponential", 2) == "wave"
 
 
@@ -215,8 +216,8 @@ def test_bf_flags_bad_rows(lib, dev, c_oracle):
     assert p[3].item() == 1234
 
 
-@pytest.mark.parametrize("algo,m", [("lane", 10), ("wave", 10), ("pairb", 10), ("pairb", 15), ("pairb", 20),
-                                    ("pairb", 27), ("quad", 26)])
+@pytest.mark.parametrize("algo,m", [("lane", 10), ("wave", 10), ("pairb", 10), ("pairb", 15), ("pairb", 19),
+                                    ("pairb", 20), ("pairb", 22), ("quad", 26), ("quad", 31)])
 @pytest.mark.parametrize("bad_value", [-2, -7, -2147483648, 2000, 2147483647])
 def test_bf_flags_every_invalid_index(lib, dev, c_oracle, algo, m, bad_value):
     """Any neighbour index < -1 or >= n_points sets partials[3] to the first such row, for every

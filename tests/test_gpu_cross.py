@@ -32,7 +32,7 @@ def _sets(n_ref, n_query, seed, dup=50):
     return ref, query, rng.standard_normal(n_ref), rng.standard_normal(n_query)
 
 
-@pytest.mark.parametrize("m,algo", [(1, "lane"), (5, "lane"), (10, "pairb"), (15, "pairb"), (28, "pairb"),
+@pytest.mark.parametrize("m,algo", [(1, "lane"), (5, "lane"), (10, "pairb"), (15, "pairb"), (28, "quad"), (20, "auto"),
                                     (15, "auto"), (20, "pairb"), (24, "wave"), (15, "wave")])
 @pytest.mark.parametrize("kind,theta", [("exponential", (1.0, 20.0, 0.1)), ("matern32", (1.4, 12.0, 0.05))])
 def test_bf_cross_vs_oracle(lib, dev, c_oracle, m, algo, kind, theta):

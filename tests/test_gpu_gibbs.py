@@ -293,11 +293,14 @@ def test_seqnngp_config5_scale_stationary(dev):
 def test_seqnngp_config5_cold_start_1000_sweeps(dev):
     """Config 5 as BASELINE states it (N = 1e6, m = 15, 1,000 Gibbs sweeps) from a COLD start:
     w from the reference's initialiser (_init_ws, nngp.py:45-47: the uniform 5-NN mean of y),
-    sigma2 and tau2 started 2x too large and phi 2x too small.  The field is drawn exactly from
-    the NNGP at the generating values (oracle_nngp_simulate).  After 500 burn-in sweeps the
-    posterior means must sit near the generating values: tau2 and the slope within 10 % / 0.02,
-    the microergodic sigma2 * phi (the combination an exponential field identifies in a fixed
-    domain) within 10 %, sigma2 and phi each within 30 %, and the latent mean must track w."""
+    sigma2, tau2 and phi each started 2x too large (so sigma2 * phi starts 4x off).  The field is
+    drawn exactly from the NNGP at the generating values (oracle_nngp_simulate).  After 500
+    burn-in sweeps the posterior means must sit at the generating values for what the data
+    identify: tau2 within 10 %, the slope within 0.02, the microergodic sigma2 * phi (what an
+    exponential field identifies in a fixed domain, Zhang 2004) within 10 %, and the latent mean
+    must track w.  sigma2 and phi separately move only slowly along that ridge (measured: a start
+    at sigma2 = 2, phi = 15 ends at 2.19, 13.7 after 1,000 sweeps with sigma2 * phi = 29.97), so they
+    are checked within a factor of 3 only; the intercept is confounded with the field's mean."""
     from oracle import nngp_oracle as O
     from pynngp_amd import Priors, SeqNNGP, _lib
 
@@ -315,15 +318,16 @@ def test_seqnngp_config5_cold_start_1000_sweeps(dev):
     idx = _lib.knn_query(ct, ct, 5).long()
     w0 = torch.from_numpy(y).to(dev)[idx].mean(dim=1).cpu().numpy()
     pri = Priors(sigma2_ig=(2.0, 1.0), tau2_ig=(2.0, 0.1), phi_unif=(1.0, 100.0))
-    s = SeqNNGP(c, y, X, m=m, priors=pri, sigma2=2 * sigma2, tau2=2 * tau2, phi=phi / 2, phi_tuning=0.01, seed=10,
+    s = SeqNNGP(c, y, X, m=m, priors=pri, sigma2=2 * sigma2, tau2=2 * tau2, phi=2 * phi, phi_tuning=0.01, seed=10,
                 device=dev, w_init=w0)
     res = s.sample(1000, burn=500, keep_w_mean=True)
     s2, ph, t2 = res["sigma2"].mean(), res["phi"].mean(), res["tau2"].mean()
-    print(f"cold start, N=1e6, 1000 sweeps: sigma2 {s2:.4f} phi {ph:.3f} sigma2*phi {(res['sigma2'] * res['phi']).mean():.3f} "
+    sp = (res["sigma2"] * res["phi"]).mean()
+    print(f"cold start, N=1e6, 1000 sweeps: sigma2 {s2:.4f} phi {ph:.3f} sigma2*phi {sp:.3f} "
           f"tau2 {t2:.4f} beta {res['beta'].mean(0)} accept {res['phi_accept_rate']:.2f}")
     assert 0.02 < res["phi_accept_rate"] < 0.95
     assert abs(t2 / tau2 - 1) < 0.10
     assert abs(res["beta"][:, 1].mean() - beta[1]) < 0.02
-    assert abs((res["sigma2"] * res["phi"]).mean() / (sigma2 * phi) - 1) < 0.10
-    assert abs(s2 / sigma2 - 1) < 0.30 and abs(ph / phi - 1) < 0.30
+    assert abs(sp / (sigma2 * phi) - 1) < 0.10
+    assert 1 / 3 < s2 / sigma2 < 3 and 1 / 3 < ph / phi < 3
     assert np.corrcoef(res["w_mean"], w)[0, 1] > 0.9
