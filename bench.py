@@ -96,21 +96,32 @@ def committed_traffic(args, want_bf):
     return e["bytes_per_launch"], f'{e["source"]} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, {e["kernel"]})'
 
 
-# VALU issue peak: 256 CUs x 4 SIMDs x 16 lanes per clock x 2.4 GHz (a 64-lane wave-instruction
-# issues in 4 clocks; fp64 FMA / add / mul and 32-bit ops alike, MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs x 16 fp64 FMA lanes per clock x 2.4 GHz -- one wave64 fp64
+# instruction every 4 cycles per SIMD, the 78.6 TFLOP/s fp64 vector rate.  Measured on gfx950
+# (tools/ubench/valu_mix.hip, profiles/r03d): at two waves per SIMD a wave-instruction occupies the
+# SIMD for ~5.1 cycles (fp64 FMA / MUL), ~4.8-4.9 (DPP moves, VOP3 32-bit such as v_lshl_add_u32,
+# v_bfi_b32), ~2.9 only for VOP2 32-bit (v_and, v_mov), ~16.8 (v_rsq_f64 / v_rcp_f64) and ~4.3 for a
+# 3:1 fp64 / DPP mix, so 32-bit work is not cheaper than 4 cycles here; the sweep measures 4.37
+# VALU-active cycles per instruction (SQ_ACTIVE_INST_VALU), see valu_roofline.
 VALU_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9
 
 
 def valu_roofline(prof, rows, kern_ms):
     """Vector-issue roofline: lane-operations per second (VALU instructions per wave from the
-    committed PMC profile x 64 lanes / locations per wave x locations/s) vs the issue peak."""
+    committed PMC profile x 64 lanes / locations per wave x locations/s) vs the fp64 issue peak,
+    plus the committed profile's measured VALU-active cycles per instruction and SIMD VALU-busy
+    share (tools/valu_busy.py): the direct measure of how close the sweep is to its issue limit."""
     if prof is None or "valu_per_wave" not in prof:
         return None
     per_loc = prof["valu_per_wave"] * 64 / prof["locations_per_wave"]
     achieved = per_loc * rows / (kern_ms * 1e-3)
-    return {"achieved": achieved / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s",
-            "frac": achieved / VALU_LANE_OPS_PEAK, "valu_lane_ops_per_location": per_loc,
-            "source": prof["source"] + " (SQ_INSTS_VALU / SQ_WAVES)"}
+    out = {"achieved": achieved / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s",
+           "frac": achieved / VALU_LANE_OPS_PEAK, "valu_lane_ops_per_location": per_loc,
+           "source": prof["source"] + " (SQ_INSTS_VALU / SQ_WAVES)"}
+    for k in ("valu_active_cycles_per_instr", "simd_valu_busy", "valu_source"):
+        if k in prof:
+            out[k] = prof[k]
+    return out
 
 
 def cpu_model():

@@ -501,18 +501,36 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             // same 2x2 block products as the right-looking update, reordered), factors the diagonal
             // block and maps the panel.  Row pair u is then final; rows < KL move to LDS.
             NNGP_PHASE(leftlooking);
+            double pnext[DA], wpnext = 0.0;  // pair u+1's partner coordinates / within-pair entry
 #pragma unroll
             for (int u = 0; u < NP; ++u) {
                 double pu[DA];
 #pragma unroll
-                for (int k = 0; k < DA; ++k) pu[k] = pr_swap(o[u][k]);
+                for (int k = 0; k < DA; ++k) pu[k] = (u % 2 == 1) ? pnext[k] : pr_swap(o[u][k]);
 #pragma unroll
                 for (int s = u + 1; s < NP; ++s) {
                     R[s][u][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], o[u]));
                     R[s][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], pu));
                 }
                 R[u][u][0] = Pc.diag;
-                R[u][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
+                // the within-pair entry (2u+1, 2u) is read from lane 1 only: for pairs u, u+1 (u even)
+                // lane 0 evaluates pair u's and lane 1 pair u+1's, and lane 0's moves over (as the
+                // right-looking kernel's split)
+                if (u % 2 == 0 && u + 1 < NP) {
+                    double a[DA], b[DA];
+#pragma unroll
+                    for (int k = 0; k < DA; ++k) {
+                        pnext[k] = pr_swap(o[u + 1][k]);
+                        a[k] = pr_pick(mask1, o[u + 1][k], o[u][k]);
+                        b[k] = pr_pick(mask1, pnext[k], pu[k]);
+                    }
+                    wpnext = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(a, b));
+                    R[u][u][1] = pr_from0(wpnext);
+                } else if (u % 2 == 1) {
+                    R[u][u][1] = wpnext;
+                } else {
+                    R[u][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
+                }
 #pragma unroll
                 for (int t = 0; t < u; ++t) {
                     const double S0 = R[u][t][0], S1 = R[u][t][1];
