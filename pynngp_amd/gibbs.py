@@ -260,13 +260,17 @@ class SeqNNGP:
         self.phi_tuning = float(phi_tuning)
         self.yres = self._residual_y(self.beta)
         if w_init is None:
-            # the reference's state initialisation (_init_ws, nngp.py:45-47): the uniform 5-NN mean
-            # of the observed responses at every node (KNeighborsRegressor(5).fit(t, y).predict(s));
-            # a zero start lets sigma2 | w = 0 collapse towards 0 and the chain stalls there
-            t_obs = t_dev[torch.from_numpy(np.nonzero(observed)[0]).to(dev)]
+            # the reference's state initialisation (_init_ws, nngp.py:45-47: the uniform 5-NN mean of
+            # the responses, KNeighborsRegressor(5).fit(t, y).predict(s)) applied to the responses
+            # less their least-squares mean X beta (the reference has no covariates; the mean stays
+            # with beta, which mixes slowly against a w that carries it): a zero start instead lets
+            # sigma2 | w = 0 collapse towards 0 and the chain stalls there
+            obs_idx = np.nonzero(observed)[0]
+            t_obs = t_dev[torch.from_numpy(obs_idx).to(dev)]
             k = min(5, self.n_obs)
             idx = _lib.knn_query(t_obs, coords0, k).long()
-            w0 = to(y_host[observed])[idx].mean(dim=1).cpu().numpy()
+            r_obs = y_host[observed] - X_t[observed] @ self.beta
+            w0 = to(r_obs)[idx].mean(dim=1).cpu().numpy()
         else:
             w0 = np.asarray(w_init, dtype=np.float64).reshape(-1)
             if w0.shape != (n,):

@@ -27,6 +27,10 @@
 #define BFI32(x) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(x) : "v"(k), "v"(k2));
 #define FMA32(x) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(x) : "v"(fb), "v"(fc));
 #define CND32(x) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(k));
+#define CNDS(x) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x) : "v"(k), "s"(smask));
+#define MOV32(x) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
+#define MOV64(x) asm volatile("v_mov_b64 %0, %1" : "=v"(x) : "v"(x));
+#define MIN64(x) asm volatile("v_min_f64 %0, %0, %1" : "+v"(x) : "v"(b));
 
 // 16-instruction bodies
 #define BODY_fma64 D8(FMA64) D8(FMA64)
@@ -39,6 +43,11 @@
 #define BODY_bfi32 F8(BFI32) F8(BFI32)
 #define BODY_fma32 F8(FMA32) F8(FMA32)
 #define BODY_cnd32 F8(CND32) F8(CND32)
+#define BODY_cnds F8(CNDS) F8(CNDS)
+#define BODY_mov32 F8(MOV32) F8(MOV32)
+#define BODY_mov64 D8(MOV64) D8(MOV64)
+#define BODY_min64 D8(MIN64) D8(MIN64)
+#define BODY_fma64_cnds D8(FMA64) F8(CNDS)
 // mixes (16 instructions each)
 #define BODY_fma64_dpp32 D8(FMA64) F8(DPP32)
 #define BODY_fma64_and32 D8(FMA64) F8(AND32)
@@ -63,6 +72,7 @@
         float f0 = threadIdx.x, f1 = f0 + 1, f2 = f0 + 2, f3 = f0 + 3, f4 = f0 + 4, f5 = f0 + 5,        \
               f6 = f0 + 6, f7 = f0 + 7, fb = 1.0000001f, fc = 0.5f;                                     \
         int k = 0x0f0f0f0f, k2 = (int)threadIdx.x;                                                      \
+        unsigned long long smask = __ballot((threadIdx.x & 1) != 0);                                    \
         asm volatile("s_mov_b64 vcc, -1" ::: "vcc");                                                    \
         __syncthreads();                                                                                \
         const long long t0 = __builtin_readcyclecounter();                                              \
@@ -80,6 +90,7 @@
 KERNEL(fma64) KERNEL(mul64) KERNEL(rsq64) KERNEL(rcp64) KERNEL(dpp32) KERNEL(and32) KERNEL(lshladd32)
 KERNEL(bfi32) KERNEL(fma32) KERNEL(cnd32) KERNEL(fma64_dpp32) KERNEL(fma64_and32) KERNEL(fma64_bfi32)
 KERNEL(fma64x3_dpp32) KERNEL(rsq64_fma64x7) KERNEL(fma64_ilp4) KERNEL(fma64_ilp2) KERNEL(fma64_ilp1)
+KERNEL(cnds) KERNEL(mov32) KERNEL(mov64) KERNEL(min64) KERNEL(fma64_cnds)
 
 int main() {
     struct K { const char* n; void (*f)(long long*, double*, int); } ks[] = {
@@ -88,7 +99,9 @@ int main() {
         {"fma32", k_fma32}, {"cnd32", k_cnd32}, {"fma64+dpp32 (1:1)", k_fma64_dpp32},
         {"fma64+and32 (1:1)", k_fma64_and32}, {"fma64+bfi32 (1:1)", k_fma64_bfi32},
         {"fma64x3+dpp32 (3:1)", k_fma64x3_dpp32}, {"rsq64+fma64x7 (1:7)", k_rsq64_fma64x7},
-        {"fma64 ILP4", k_fma64_ilp4}, {"fma64 ILP2", k_fma64_ilp2}, {"fma64 ILP1", k_fma64_ilp1}};
+        {"fma64 ILP4", k_fma64_ilp4}, {"fma64 ILP2", k_fma64_ilp2}, {"fma64 ILP1", k_fma64_ilp1},
+        {"cndmask_e64 (sgpr mask)", k_cnds}, {"mov32", k_mov32}, {"mov64", k_mov64}, {"min64", k_min64},
+        {"fma64+cndmask_e64 (1:1)", k_fma64_cnds}};
     const int cus = 256, iters = 2048;
     const size_t lds = 96 * 1024;
     long long* cyc;
