@@ -315,6 +315,7 @@ def main():
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--kind", default="exponential", choices=list(_lib.KIND_CODES))
     ap.add_argument("--theta", default="1.0,30.0,0.0", help="sigma2,phi,tau2")
+    ap.add_argument("--nu", type=float, default=None, help="smoothness of --kind matern")
     ap.add_argument("--algo", default="auto", choices=["auto", "lane", "wave", "quad", "pairb"])
     ap.add_argument("--loglik-only", action="store_true", help="skip the B/F writes (log-lik partials only)")
     ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order; natural layout)")
@@ -374,7 +375,7 @@ def main():
         return
 
     sigma2, phi, tau2 = (float(x) for x in args.theta.split(","))
-    cov = Covariance(args.kind, sigma2, phi, tau2)
+    cov = Covariance(args.kind, sigma2, phi, tau2, nu=args.nu)
     n_total = args.n * world
     coords, values = synth(n_total, seed=0)
     c = torch.from_numpy(coords).to(dev)
@@ -467,7 +468,7 @@ def main():
                 "n_total": n_total,
                 "m": args.m,
                 "kind": args.kind,
-                "theta": [sigma2, phi, tau2],
+                "theta": [sigma2, phi, tau2] + ([args.nu] if args.kind == "matern" else []),
                 "algo": args.algo,
                 "row_order": "index" if args.no_order else "z-order",
                 "layout": args.layout,
@@ -510,11 +511,12 @@ def main():
             F_gpu = sweep.F.cpu().numpy() if want_bf else None
             c_sw = sweep._coords_sweep  # storage- or input-order coordinates the rows / nbr refer to
             if F_gpu is None:
-                _, F_t, _ = _lib.bf_sweep(c_sw, sweep.nbr, 0, cov.kind, *cov.theta)
+                _, F_t, _ = _lib.bf_sweep(c_sw, sweep.nbr, 0, cov.kind, *cov.theta, nu=cov.nu_arg)
                 F_gpu = F_t.cpu().numpy()
             out["neighbor_build_cpu"] = knn_cpu_baseline(coords, args.m, n_total)
             out["cpu_baseline"] = cpu_baseline(c_sw.cpu().numpy(), values, sweep.nbr.cpu().numpy(), args.kind,
-                                               (sigma2, phi, tau2), args.cpu_seconds, F_gpu)
+                                               (sigma2, phi, tau2) + ((args.nu,) if args.kind == "matern" else ()),
+                                               args.cpu_seconds, F_gpu)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if distributed:

@@ -70,8 +70,8 @@ int main(int argc, char** argv) {
     /* NNGP._make_s_neighbor_sets (nngp.py:49-62) */
     CHECK_NNGP(nngp_knn_prior(d_xy, n, 2, m, 0, n, d_nbr, ws_knn, knn_bytes, NULL));
     /* _CNs / _Ccross / _Cs / _Bsi / _Fsi (nngp.py:73-96) + the log-likelihood for every location */
-    CHECK_NNGP(nngp_bf_sweep(d_xy, n, 2, d_nbr, NULL, n, m, 0, NNGP_COV_EXPONENTIAL, 1.0, 30.0, 0.1, d_v, d_B, d_F, NULL,
-                             d_p, ws_bf, bf_bytes, NNGP_ALGO_AUTO, NULL));
+    CHECK_NNGP(nngp_bf_sweep(d_xy, n, 2, d_nbr, NULL, n, m, 0, NNGP_COV_EXPONENTIAL, 1.0, 30.0, 0.1, /*nu*/ 0.0, d_v,
+                             d_B, d_F, NULL, d_p, ws_bf, bf_bytes, NNGP_ALGO_AUTO, NULL));
     double p[4], Flast;
     CHECK_HIP(hipMemcpy(p, d_p, sizeof p, hipMemcpyDeviceToHost));
     CHECK_HIP(hipMemcpy(&Flast, d_F + (n - 1), sizeof(double), hipMemcpyDeviceToHost));

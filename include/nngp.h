@@ -44,11 +44,15 @@ extern "C" {
 #define NNGP_COV_MATERN52 2    /* sigma2 (1 + u + u^2/3) exp(-u)                    */
 #define NNGP_COV_GAUSSIAN 3    /* sigma2 exp(-u^2)                                  */
 #define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
+#define NNGP_COV_MATERN 5      /* sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), 0 < nu <= 50: spNNGP's
+                                  "matern" of any smoothness nu (the `nu` argument of the sweeps;
+                                  ignored by the other kinds).  Served by the wavefront kernel. */
 
 /* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE serves 2-D
- * exponential / Matern-3/2 only, PAIRB, QUAD and WAVE every kind and dimension.  (3 and 7 were
+ * exponential / Matern-3/2 only, PAIRB, QUAD and WAVE kinds 0..4 in every dimension, WAVE also
+ * NNGP_COV_MATERN (AUTO sends it there for every m).  (3 and 7 were
  * comparison-only kernels of earlier builds; they are rejected as unknown.) */
-#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above              */
+#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above (and matern)  */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
 #define NNGP_ALGO_QUAD 4  /* four lanes per location (25 <= m <= 32)                         */
@@ -130,11 +134,13 @@ int nngp_knn_query(const double *ref, int64_t n_ref, int32_t dim, const double *
  * the workspace and nngp_bf_finalize (same n_rows, m, kind, dim, algo) folds them later,
  * e.g. on another stream while the next sweep (with another workspace) runs.
  * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo) bytes, 256-B aligned.
+ * kind, sigma2 > 0, phi > 0, tau2 >= 0: the covariance (the reference's `cov`); nu: the smoothness
+ * of NNGP_COV_MATERN (0 < nu <= 50), ignored by the other kinds.
  * ------------------------------------------------------------------------- */
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo);
 int nngp_bf_sweep(const double *coords, int64_t n_points, int32_t dim, const int32_t *nbr, const int32_t *order,
                   int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
-                  const double *values, double *B, double *F, double *R, double *partials, void *workspace,
+                  double nu, const double *values, double *B, double *F, double *R, double *partials, void *workspace,
                   size_t workspace_bytes, int32_t algo, void *stream);
 /* The deferred fold of a sweep run with partials == NULL (fixed order: the same
  * bits as the in-line fold).  n_rows, m, kind, dim and algo must be the sweep's (they select
@@ -157,11 +163,13 @@ int nngp_bf_finalize(const void *workspace, size_t workspace_bytes, int64_t n_ro
  * the kriging mean).  partials as nngp_bf_sweep (with query_values: the
  * conditional log density of v_t given v_S).  Rows q in [q0, q0 + n_rows) of
  * n_query; order / workspace as nngp_bf_sweep (nngp_row_order on the query
- * coordinates; nngp_bf_sweep_workspace_bytes).  ref and query are (n, dim).
+ * coordinates; nngp_bf_sweep_workspace_bytes), kind / theta / nu as nngp_bf_sweep.  ref and
+ * query are (n, dim).
  * ------------------------------------------------------------------------- */
 int nngp_bf_cross(const double *ref, int64_t n_ref, int32_t dim, const double *query, int64_t n_query,
                   const int32_t *nbr, const int32_t *order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind,
-                  double sigma2, double phi, double tau2, const double *ref_values, const double *query_values,
+                  double sigma2, double phi, double tau2, double nu, const double *ref_values,
+                  const double *query_values,
                   double *B, double *F, double *R, double *partials, void *workspace, size_t workspace_bytes,
                   int32_t algo, void *stream);
 

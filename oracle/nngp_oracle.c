@@ -97,7 +97,8 @@ int oracle_knn_prior_rows(const double *coords, int64_t n, int32_t dim, int32_t 
 
 /* Covariance kinds (the reference's `cov` plug-in, nngp.py:6,12), u = phi d:
  *   0 exponential sigma2 e^-u   1 matern32 sigma2 (1 + u) e^-u   2 matern52 sigma2 (1 + u + u^2/3) e^-u
- *   3 gaussian    sigma2 e^-u^2 4 spherical sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 */
+ *   3 gaussian    sigma2 e^-u^2 4 spherical sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0
+ *   5 matern      sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), nu = theta[3] (matern_rho below) */
 /* ---------------------------------------------------------------------------
  * The reference's own neighbour-set ALGORITHM, restated for the CPU baseline:
  * NNGP._make_s_neighbor_sets (nngp.py:49-62) builds a fresh sklearn KDTree over
@@ -444,9 +445,37 @@ int oracle_knn_prior_prefix_kdtree(const double *coords, int64_t n, int32_t dim,
     return rc ? -2 : 0;
 }
 
-static inline double cov_eval(int kind, double d, double sigma2, double phi) {
+/* Matern of general smoothness nu (kind 5, spNNGP's "matern"): rho(u) = u^nu K_nu(u) / (2^(nu-1) Gamma(nu))
+ * from the integral K_nu(u) = int_0^inf exp(-u cosh t) cosh(nu t) dt (Watson 6.22 (5)) by the trapezoidal
+ * rule in long double -- a method independent of the kernels' Temme series / continued fraction
+ * (nngp_math.h).  The integrand is entire and decays double-exponentially, so the trapezoidal error is
+ * ~exp(-2 pi a / h) times the integrand's growth into the strip |Im t| < a, ~(cos a)^-nu: h = 1/20
+ * leaves < 1e-25 up to nu = 50; for large u the integrand is a peak of width ~u^-1/2 at t = 0, so
+ * h <= u^-1/2 / 4 (the Gaussian's trapezoidal error ~exp(-2 pi^2 / (16 h^2 u)) ~ 1e-53).  Every term is summed as
+ * exp(log term): nu ln u - u cosh t + ln cosh(nu t) - ln(2^(nu-1) Gamma(nu)), so nothing over- or
+ * underflows for any u > 0 (u^nu and K_nu(u) separately would for tiny u). */
+static double matern_rho(double nu, double u) {
+    if (!(u > 0.0)) return 1.0;
+    const long double hw = 0.25L / sqrtl((long double)u);
+    const long double h = hw < 0.05L ? hw : 0.05L, lu = logl((long double)u), nul = (long double)nu;
+    const long double lnorm = (nul - 1.0L) * logl(2.0L) + lgammal(nul);
+    const long double tpk = asinhl(nul / (long double)u); /* the integrand's peak */
+    long double sum = 0.0L, emax = -INFINITY;
+    for (long k = 0;; ++k) {
+        const long double t = h * (long double)k;
+        const long double lch = nul * t + log1pl(expl(-2.0L * nul * t)) - logl(2.0L); /* ln cosh(nu t) */
+        const long double e = nul * lu - (long double)u * coshl(t) + lch - lnorm;
+        if (e > emax) emax = e;
+        sum += (k == 0 ? 0.5L : 1.0L) * expl(e);
+        if (t > tpk && e < emax - 100.0L) break;
+    }
+    return (double)(h * sum);
+}
+
+static inline double cov_eval_nu(int kind, double d, double sigma2, double phi, double nu) {
     const double u = phi * d;
     switch (kind) {
+        case 5: return sigma2 * matern_rho(nu, u);
         case 1: return sigma2 * (1.0 + u) * exp(-u);
         case 2: return sigma2 * (1.0 + u + u * u / 3.0) * exp(-u);
         case 3: return sigma2 * exp(-u * u);
@@ -454,6 +483,9 @@ static inline double cov_eval(int kind, double d, double sigma2, double phi) {
         default: return sigma2 * exp(-u);
     }
 }
+
+/* exported for tests/test_matern.py (the restatement checked against mpmath) */
+double oracle_matern_rho(double nu, double u) { return matern_rho(nu, u); }
 
 static inline double pdist(const double *a, const double *b, int dim) { return sqrt(rdist(a, b, dim)); }
 
@@ -468,8 +500,9 @@ static inline double pdist(const double *a, const double *b, int dim) { return s
 int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t dim, int32_t m, int32_t kind,
                     const double *theta, const double *values, double *Bout, double *Fout, double *partials,
                     int64_t i0, int64_t i1) {
-    if (m < 0 || dim < 1 || i0 < 0 || i1 > n || i0 > i1 || kind < 0 || kind > 4) return -1;
+    if (m < 0 || dim < 1 || i0 < 0 || i1 > n || i0 > i1 || kind < 0 || kind > 5) return -1;
     const double sigma2 = theta[0], phi = theta[1], tau2 = theta[2];
+    const double nu = kind == 5 ? theta[3] : 0.0; /* theta = (sigma2, phi, tau2, nu) for kind 5 */
     const int64_t rows = i1 - i0;
     double *logF = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1));
     double *quad = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1));
@@ -504,10 +537,10 @@ int oracle_bf_sweep(const double *coords, const int32_t *nbr, int64_t n, int32_t
                     const double *xa = coords + dim * (int64_t)row[slot[a]];
                     for (int bb = 0; bb < a; ++bb) {
                         const double *xb = coords + dim * (int64_t)row[slot[bb]];
-                        L[a * k + bb] = cov_eval(kind, pdist(xa, xb, dim), sigma2, phi);
+                        L[a * k + bb] = cov_eval_nu(kind, pdist(xa, xb, dim), sigma2, phi, nu);
                     }
                     L[a * k + a] = sigma2 + tau2;
-                    c[a] = cov_eval(kind, pdist(xi, xa, dim), sigma2, phi);
+                    c[a] = cov_eval_nu(kind, pdist(xi, xa, dim), sigma2, phi, nu);
                 }
                 /* Cholesky (Cholesky-Banachiewicz, row by row) */
                 for (int a = 0; a < k && !bad; ++a) {

@@ -43,7 +43,9 @@ Euclidean distance in fp64 over any number of coordinate columns -- the referenc
 KDTree takes ordinates of any dimension, ``nngp.py:55-61``):
 ``exponential`` sigma2 e^-u; ``matern32`` sigma2 (1 + u) e^-u; ``matern52``
 sigma2 (1 + u + u^2/3) e^-u; ``gaussian`` sigma2 e^-u^2; ``spherical``
-sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family).
+sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family); ``matern`` (general
+smoothness nu, theta = (sigma2, phi, tau2, nu)) sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) through
+scipy.special.kv (AMOS) here and a long-double trapezoidal integral in the C restatement.
 """
 from __future__ import annotations
 
@@ -53,7 +55,7 @@ import subprocess
 
 import numpy as np
 
-KINDS = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4}
+KINDS = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4, "matern": 5}
 LOG_2PI = float(np.log(2.0 * np.pi))
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -116,9 +118,28 @@ def ws_init(t: np.ndarray, y: np.ndarray, s: np.ndarray, k: int = 5) -> np.ndarr
 # ----------------------------------------------------------------------------
 # covariance plug-in and per-location algebra (nngp.py:73-96)
 # ----------------------------------------------------------------------------
-def cov_fn(kind: str, d: np.ndarray, sigma2: float, phi: float) -> np.ndarray:
+def _theta(theta):
+    """(sigma2, phi, tau2, nu): theta = (sigma2, phi, tau2) or, for the ``matern`` kind, (..., nu)."""
+    return float(theta[0]), float(theta[1]), float(theta[2]), (float(theta[3]) if len(theta) > 3 else None)
+
+
+def matern_rho(nu: float, u: np.ndarray) -> np.ndarray:
+    """u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) (1 at u = 0) with scipy's K_nu."""
+    from scipy import special
+    u = np.asarray(u, dtype=np.float64)
+    us = np.where(u > 0, u, 1.0)
+    with np.errstate(invalid="ignore", over="ignore", under="ignore", divide="ignore"):
+        k = special.kv(nu, us)
+        r = np.exp(nu * np.log(us) - (nu - 1.0) * np.log(2.0) - special.gammaln(nu) + np.log(k))
+    # K_nu overflows only for u so small (nu > 1/2) that 1 - rho ~ u^2 is far below an ulp
+    return np.where((u > 0) & np.isfinite(k), r, 1.0)
+
+
+def cov_fn(kind: str, d: np.ndarray, sigma2: float, phi: float, nu: float | None = None) -> np.ndarray:
     """The covariance kinds, u = phi d (module docstring)."""
     u = phi * np.asarray(d, dtype=np.float64)
+    if kind == "matern":
+        return sigma2 * matern_rho(nu, u)
     if kind == "exponential":
         return sigma2 * np.exp(-u)
     if kind == "matern32":
@@ -138,12 +159,12 @@ def _pair_dist(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 def location_blocks(coords, nbr_row, i, kind, theta):
     """(C_N, c, C_ii) for one location: ``_CNs``, ``_Ccross``, ``_Cs``."""
-    sigma2, phi, tau2 = theta
+    sigma2, phi, tau2, nu = _theta(theta)
     idx = nbr_row[nbr_row >= 0].astype(np.int64)
     xs = coords[idx]
-    CN = cov_fn(kind, _pair_dist(xs[:, None, :], xs[None, :, :]), sigma2, phi)
+    CN = cov_fn(kind, _pair_dist(xs[:, None, :], xs[None, :, :]), sigma2, phi, nu)
     CN = CN + tau2 * np.eye(idx.size)
-    c = cov_fn(kind, _pair_dist(coords[i][None, :], xs), sigma2, phi)
+    c = cov_fn(kind, _pair_dist(coords[i][None, :], xs), sigma2, phi, nu)
     return CN, c, sigma2 + tau2
 
 
@@ -169,7 +190,7 @@ def bf_sweep(coords, nbr, kind, theta, values=None, i0=0):
     coords = np.ascontiguousarray(coords, dtype=np.float64)
     nbr = np.ascontiguousarray(nbr, dtype=np.int32)
     n, m = nbr.shape
-    sigma2, phi, tau2 = theta
+    sigma2, phi, tau2, nu = _theta(theta)
     B = np.zeros((n, m))
     F = np.empty(n)
     valid = nbr >= 0
@@ -184,9 +205,9 @@ def bf_sweep(coords, nbr, kind, theta, values=None, i0=0):
             continue
         idx = nbr[sel, :k].astype(np.int64)
         xs = coords[idx]  # (b, k, 2)
-        CN = cov_fn(kind, _pair_dist(xs[:, :, None, :], xs[:, None, :, :]), sigma2, phi)
+        CN = cov_fn(kind, _pair_dist(xs[:, :, None, :], xs[:, None, :, :]), sigma2, phi, nu)
         CN = CN + tau2 * np.eye(k)[None]
-        c = cov_fn(kind, _pair_dist(coords[rows_i[sel]][:, None, :], xs), sigma2, phi)
+        c = cov_fn(kind, _pair_dist(coords[rows_i[sel]][:, None, :], xs), sigma2, phi, nu)
         L = np.linalg.cholesky(CN)
         v = np.linalg.solve(L, c[..., None])
         Bk = np.linalg.solve(np.swapaxes(L, 1, 2), v)[..., 0]
@@ -219,9 +240,9 @@ def nngp_loglik(coords, nbr, kind, theta, values):
 
 def dense_gp_loglik(coords, kind, theta, values):
     """Exact GP log density (known answer for m = N-1)."""
-    sigma2, phi, tau2 = theta
+    sigma2, phi, tau2, nu = _theta(theta)
     d = _pair_dist(coords[:, None, :], coords[None, :, :])
-    C = cov_fn(kind, d, sigma2, phi) + tau2 * np.eye(coords.shape[0])
+    C = cov_fn(kind, d, sigma2, phi, nu) + tau2 * np.eye(coords.shape[0])
     L = np.linalg.cholesky(C)
     z = np.linalg.solve(L, values)
     n = coords.shape[0]
@@ -264,6 +285,8 @@ def load_c_oracle():
     lib.oracle_bf_sweep.argtypes = [P, P, I64, I32, I32, I32, P, P, P, P, P, I64, I64]
     lib.oracle_bf_sweep.restype = ctypes.c_int
     lib.oracle_num_threads.restype = ctypes.c_int
+    lib.oracle_matern_rho.argtypes = [ctypes.c_double, ctypes.c_double]
+    lib.oracle_matern_rho.restype = ctypes.c_double
     lib.oracle_nngp_simulate.argtypes = [P, P, P, ctypes.c_int64, ctypes.c_int32, P, P]
     lib.oracle_nngp_simulate.restype = ctypes.c_int
     _C = lib
@@ -352,6 +375,11 @@ def c_bf_sweep(coords, nbr, kind, theta, values=None, i0=0, want_bf=True):
     return B, F, partials
 
 
+def c_matern_rho(nu: float, u: float) -> float:
+    """The C restatement's Matern correlation (long-double trapezoidal integral)."""
+    return load_c_oracle().oracle_matern_rho(float(nu), float(u))
+
+
 def c_nngp_simulate(nbr, B, F, eps):
     """w ~ NNGP by forward substitution (oracle_nngp_simulate): w_i = B_i w_N(i) + sqrt(F_i) eps_i."""
     lib = load_c_oracle()
@@ -384,9 +412,9 @@ def c_bf_cross(ref, query, nbr, kind, theta, ref_values=None, query_values=None,
 def dense_kriging(ref, query, kind, theta, ref_values=None):
     """Exact GP conditional of the query points given ALL of ref (numpy solve):
     B = C(t, S) (C(S) + tau2 I)^{-1}, F = sigma2 + tau2 - B C(S, t), mean = B v_S."""
-    sigma2, phi, tau2 = theta
-    Css = cov_fn(kind, _pair_dist(ref[:, None, :], ref[None, :, :]), sigma2, phi) + tau2 * np.eye(len(ref))
-    Cts = cov_fn(kind, _pair_dist(query[:, None, :], ref[None, :, :]), sigma2, phi)
+    sigma2, phi, tau2, nu = _theta(theta)
+    Css = cov_fn(kind, _pair_dist(ref[:, None, :], ref[None, :, :]), sigma2, phi, nu) + tau2 * np.eye(len(ref))
+    Cts = cov_fn(kind, _pair_dist(query[:, None, :], ref[None, :, :]), sigma2, phi, nu)
     B = np.linalg.solve(Css, Cts.T).T
     F = sigma2 + tau2 - np.einsum("ij,ij->i", B, Cts)
     mean = None if ref_values is None else B @ np.asarray(ref_values, dtype=np.float64)

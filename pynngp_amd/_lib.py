@@ -44,7 +44,8 @@ SYMBOLS = (
     "nngp_gibbs_stats",
 )
 
-KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4}
+KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4, "matern": 5}
+MATERN_NU_MAX = 50.0
 ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
@@ -81,9 +82,9 @@ def load() -> ctypes.CDLL:
     lib.nngp_knn_query.restype = ctypes.c_int
     lib.nngp_bf_sweep_workspace_bytes.argtypes = [I64, I32, I32, I32, I32]
     lib.nngp_bf_sweep_workspace_bytes.restype = SZ
-    lib.nngp_bf_sweep.argtypes = [P, I64, I32, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, I32, P]
-    lib.nngp_bf_cross.argtypes = [P, I64, I32, P, I64, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, P, SZ, I32,
-                                  P]
+    lib.nngp_bf_sweep.argtypes = [P, I64, I32, P, P, I64, I32, I64, I32, D, D, D, D, P, P, P, P, P, P, SZ, I32, P]
+    lib.nngp_bf_cross.argtypes = [P, I64, I32, P, I64, P, P, I64, I32, I64, I32, D, D, D, D, P, P, P, P, P, P, P, SZ,
+                                  I32, P]
     lib.nngp_bf_cross.restype = ctypes.c_int
     lib.nngp_row_order_workspace_bytes.argtypes = [I64]
     lib.nngp_row_order_workspace_bytes.restype = SZ
@@ -257,14 +258,28 @@ def knn_query(ref: torch.Tensor, query: torch.Tensor, k: int) -> torch.Tensor:
     return out
 
 
+def _check_kind(kind: str, nu: Optional[float]) -> float:
+    """The kind's code must exist; the ``matern`` kind needs 0 < nu <= 50 (returned as the C argument)."""
+    if kind not in KIND_CODES:
+        raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
+    if kind == "matern":
+        if nu is None or not 0.0 < float(nu) <= MATERN_NU_MAX:
+            raise ValueError(f"the matern kind needs a smoothness 0 < nu <= {MATERN_NU_MAX:g} (got {nu!r})")
+        return float(nu)
+    return -1.0
+
+
 def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2: float, phi: float,
              tau2: float = 0.0, values: Optional[torch.Tensor] = None, want_bf: bool = True,
              algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
              partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
              order: Optional[torch.Tensor] = None,
              R: Optional[torch.Tensor] = None,
-             defer: bool = False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+             defer: bool = False, nu: Optional[float] = None
+             ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
+
+    ``nu``: the smoothness of the ``matern`` kind (0 < nu <= 50; required there, ignored otherwise).
 
     ``defer=True`` (needs ``workspace``): the final fold is left to :func:`bf_finalize`
     on the same workspace (e.g. on another stream); partials is returned as None.
@@ -288,8 +303,7 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     rows, m = nbr.shape
     if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
         raise ValueError("order must be int32 (rows,)")
-    if kind not in KIND_CODES:
-        raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
+    nu = _check_kind(kind, nu)
     lib = load()
     a = ALGO_CODES[algo]
     if want_bf:
@@ -314,7 +328,7 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     if workspace.device != dev or not workspace.is_contiguous():
         raise ValueError("workspace must be a contiguous tensor on the sweep's device")
     _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], d, _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
-                             float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B), _ptr(F), _ptr(R),
+                             float(sigma2), float(phi), float(tau2), nu, _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),
            "nngp_bf_sweep")
     return B, F, partials
@@ -342,7 +356,7 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
              B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
              partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
              order: Optional[torch.Tensor] = None,
-             R: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+             R: Optional[torch.Tensor] = None, nu: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """B_t, F_t of query rows ``q0 .. q0 + len(nbr)`` against the reference set ``ref``
     (nngp_bf_cross; prediction at t not in S).
 
@@ -367,8 +381,7 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
     rows, m = nbr.shape
     if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
         raise ValueError("order must be int32 (rows,)")
-    if kind not in KIND_CODES:
-        raise ValueError(f"unknown covariance kind {kind!r}; expected one of {sorted(KIND_CODES)}")
+    nu = _check_kind(kind, nu)
     lib = load()
     a = ALGO_CODES[algo]
     _check_out(B, "B", (rows, m), dev)
@@ -382,7 +395,7 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)
     _check(lib.nngp_bf_cross(_ptr(ref), ref.shape[0], d, _ptr(query), query.shape[0], _ptr(nbr), _ptr(order), rows, m,
-                             int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(ref_values),
+                             int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), nu, _ptr(ref_values),
                              _ptr(query_values), _ptr(B), _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace),
                              workspace.numel(), a, _stream(dev)), "nngp_bf_cross")
     return B, F, partials

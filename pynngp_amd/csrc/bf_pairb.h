@@ -111,7 +111,18 @@ namespace nngp {
 #ifndef NNGP_PAIRB_LEFT_LDS_ROWS_1W  // ... and at one wave per SIMD (8: 147 KB)
 #define NNGP_PAIRB_LEFT_LDS_ROWS_1W 8
 #endif
+// Left-looking at three waves per SIMD (<= 168 VGPRs; bit m of NNGP_PAIRB_LEFT_3W_MASK, which
+// must also be set in NNGP_PAIRB_LEFT_MASK): NNGP_PAIRB_LEFT_LDS_ROWS_3W factor rows in LDS.
+#ifndef NNGP_PAIRB_LEFT_3W_MASK
+#define NNGP_PAIRB_LEFT_3W_MASK 0ull
+#endif
+#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_3W  // (4: 40 KB per block, 123 KB per CU at three blocks)
+#define NNGP_PAIRB_LEFT_LDS_ROWS_3W 4
+#endif
 constexpr bool pairb_left(int m) { return ((unsigned long long)(NNGP_PAIRB_LEFT_MASK) >> m) & 1ull; }
+constexpr bool pairb_left3(int m) {
+    return pairb_left(m) && (((unsigned long long)(NNGP_PAIRB_LEFT_3W_MASK) >> m) & 1ull);
+}
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
 #define NNGP_PHASE(name)                        \
@@ -165,9 +176,9 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 #endif
 #define NNGP_PAIRB_ATTR                                                                              \
     __attribute__((amdgpu_waves_per_eu(                                                                 \
-        (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3                                                             \
+        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3(M)) ? 3                                         \
          : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_left(M) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
-        (M <= NNGP_PAIRB_THREE_WAVES_MAX ? 3 : 2))))
+        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3(M)) ? 3 : 2))))
 
 // Threads per block (one tile of kPairbThreads / 2 locations per block).  256 measured fastest:
 // 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
@@ -249,7 +260,9 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
     constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
                           (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
-    constexpr int KL0 = M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W : NNGP_PAIRB_LEFT_LDS_ROWS;
+    constexpr int KL0 = pairb_left3(M)                         ? NNGP_PAIRB_LEFT_LDS_ROWS_3W
+                        : M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W
+                                                              : NNGP_PAIRB_LEFT_LDS_ROWS;
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
     __shared__ double lrow[KL > 0 ? KL * (KL + 1) : 1][KL > 0 ? kPairbThreads : 1];
     constexpr bool ZLDS = NOZ && M >= NNGP_PAIRB_ZLDS_MIN;

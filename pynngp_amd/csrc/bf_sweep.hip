@@ -366,7 +366,7 @@ hipError_t bf_finalize_launch(const double* bpart, int64_t n_records, double* pa
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     if (a.n_rows == 0)  // empty shard: partials = [0, 0, -1, -1]
         return a.partials != nullptr ? bf_finalize_launch(a.bpart, 0, a.partials, s) : hipSuccess;
-    const CovParams P = nngp_cov_params(a.kind, a.sigma2, a.phi, a.tau2);
+    const CovParams P = nngp_cov_params_nu(a.kind, a.sigma2, a.phi, a.tau2, a.nu);
     bool ok;
     int64_t nb;
     if (algo == kAlgoLane) {

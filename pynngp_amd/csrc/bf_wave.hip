@@ -32,7 +32,48 @@ __device__ __forceinline__ void wave_row(const CovParams& P, const double* etab,
     }
 }
 
+// General-smoothness Matern: each entry is a Bessel-function evaluation with data-dependent loops
+// (nngp_matern_rho), so the wave evaluates the joint block's M (M + 1) / 2 distinct entries once,
+// spread over all 64 lanes (entry e = (a, b), a > b, e = a (a - 1) / 2 + b; the two points'
+// coordinates come from lanes a and b by ds_bpermute), into this wave's LDS slice, and lane a then
+// reads its row back -- instead of each lane evaluating its own row (one entry per lane and step,
+// lanes past the row idle: ~1/8 of the lanes busy at m = 15).  Intra-wave LDS exchange: a
+// wavefront-scope release / acquire around a wave barrier (the waves of a block run different
+// numbers of locations, so no block barrier).
 template <int NR>
+__device__ __forceinline__ void wave_row_matern(const CovParams& P, const double (&xg)[3], int lane, int M,
+                                                double* __restrict__ cb, double (&row)[NR]) {
+    const int ne = (M + 1) * M / 2;
+#pragma nounroll
+    for (int e0 = 0; e0 < ne; e0 += 64) {  // wave-uniform trip count: the shuffles run with every lane active
+        const int e = min(e0 + lane, ne - 1);
+        int a = (int)(0.5 * (1.0 + sqrt(1.0 + 8.0 * (double)e)));
+        while (a * (a - 1) / 2 > e) --a;
+        while ((a + 1) * a / 2 <= e) ++a;
+        const int b = e - a * (a - 1) / 2;
+        double xa[3], xb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            xa[k] = __shfl(xg[k], a);
+            xb[k] = __shfl(xg[k], b);
+        }
+        if (e0 + lane < ne) cb[e] = nngp_cov_d2<NNGP_KIND_MATERN>(P, nullptr, point_d2<3>(xa, xb));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int base = lane * (lane - 1) / 2;
+#pragma unroll
+    for (int b = 0; b < NR; ++b) row[b] = b == lane ? P.diag : (b < lane && lane <= M ? cb[base + b] : 0.0);
+    // the slice is rewritten for the next location only after every lane has read its row
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// MATERN: the general-smoothness Matern kind in an instantiation of its own (its Bessel loops would
+// raise the register peak of the other kinds' kernel: 223 -> 264 VGPRs at NR = 64)
+template <int NR, bool MATERN>
 __global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords, int64_t n_points, int dim, int kind,
                                                const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                int64_t n_rows, int64_t i0, int M,
@@ -41,6 +82,9 @@ __global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords
                                                double* __restrict__ bpart) {
     const int lane = threadIdx.x & 63;
     __shared__ double etab[NNGP_EXP_TAB_N];
+    // MATERN: one slice of the joint block's distinct entries per wave (4 waves per block)
+    constexpr int kSlice = NR * (NR - 1) / 2;
+    __shared__ double cbuf[MATERN ? 4 * kSlice : 1];
     nngp_exp_table_load(etab, P.sigma2);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -67,12 +111,16 @@ __global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords
 
         // row `lane` of the joint block (entries b <= lane are meaningful)
         double row[NR];
-        switch (kind) {
-            case 0: wave_row<NR, 0>(P, etab, xg, lane, row); break;
-            case 1: wave_row<NR, 1>(P, etab, xg, lane, row); break;
-            case 2: wave_row<NR, 2>(P, etab, xg, lane, row); break;
-            case 3: wave_row<NR, 3>(P, etab, xg, lane, row); break;
-            default: wave_row<NR, 4>(P, etab, xg, lane, row); break;
+        if constexpr (MATERN) {
+            wave_row_matern<NR>(P, xg, lane, M, cbuf + (threadIdx.x >> 6) * kSlice, row);
+        } else {
+            switch (kind) {
+                case 0: wave_row<NR, 0>(P, etab, xg, lane, row); break;
+                case 1: wave_row<NR, 1>(P, etab, xg, lane, row); break;
+                case 2: wave_row<NR, 2>(P, etab, xg, lane, row); break;
+                case 3: wave_row<NR, 3>(P, etab, xg, lane, row); break;
+                default: wave_row<NR, 4>(P, etab, xg, lane, row); break;
+            }
         }
         bool bad = false;
         double ip_mine = 1.0;  // lane p keeps 1/L[p][p]
@@ -132,7 +180,8 @@ __global__ __launch_bounds__(256) void bf_wave(const double* __restrict__ coords
 
 template <int NR>
 static void launch_wave(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s) {
-    hipLaunchKernelGGL((bf_wave<NR>), dim3((unsigned)n_blocks), dim3(256), 0, s, a.coords, a.n_points, a.dim,
+    auto kern = a.kind == NNGP_KIND_MATERN ? bf_wave<NR, true> : bf_wave<NR, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n_blocks), dim3(256), 0, s, a.coords, a.n_points, a.dim,
                        a.kind, a.nbr, a.order, a.n_rows, a.i0, a.m, P, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R,
                        a.bpart);
 }
@@ -145,7 +194,7 @@ int64_t bf_wave_blocks(int64_t n_rows) {
 
 // every kind and dimension: the generic path (any m <= 63)
 bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t nb, hipStream_t s) {
-    if (a.dim < 1 || a.dim > 3 || a.kind < 0 || a.kind > 4) return false;
+    if (a.dim < 1 || a.dim > 3 || a.kind < 0 || a.kind > NNGP_KIND_MATERN) return false;
     if (a.m + 1 <= 16)
         launch_wave<16>(a, P, nb, s);
     else if (a.m + 1 <= 32)

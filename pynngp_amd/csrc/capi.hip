@@ -35,9 +35,10 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // above; every kind and dimension (the four-lane kernel has a runtime-kind, runtime-dimension
 // instantiation beside its 2-D exponential / Matern-3/2 ones).
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
-    (void)kind;
     (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
+    // general-smoothness Matern: the Bessel function's loops stay out of the unrolled register kernels
+    if (kind == NNGP_COV_MATERN) return nngp::kAlgoWave;
     if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
     if (m >= 25 && m <= 32) return nngp::kAlgoQuad;
     return nngp::kAlgoWave;
@@ -77,7 +78,7 @@ size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, in
 
 static int bf_common(const double* coords, int64_t n_points, int32_t dim, const double* qcoords, int64_t n_locs,
                      const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t i0, int32_t kind,
-                     double sigma2, double phi, double tau2, const double* values, const double* qvalues, double* B,
+                     double sigma2, double phi, double tau2, double nu, const double* values, const double* qvalues, double* B,
                      double* F, double* R, double* partials, void* workspace, size_t workspace_bytes, int32_t algo,
                      void* stream) {
     if (coords == nullptr || qcoords == nullptr || workspace == nullptr)
@@ -88,9 +89,11 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
                     (long long)n_locs);
-    if (kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_SPHERICAL) return fail(NNGP_EINVAL, "unknown kind %d", kind);
+    if (kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_MATERN) return fail(NNGP_EINVAL, "unknown kind %d", kind);
     if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
+    if (kind == NNGP_COV_MATERN && !(nu > 0.0 && nu <= NNGP_MATERN_NU_MAX))
+        return fail(NNGP_EINVAL, "the matern kind needs 0 < nu <= %g (nu=%g)", NNGP_MATERN_NU_MAX, nu);
     if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
     if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
     if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
@@ -98,6 +101,9 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     int a = resolve_algo(algo, m, kind, dim);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
         return fail(NNGP_EINVAL, "unknown algo %d", algo);
+    if (kind == NNGP_COV_MATERN && a != nngp::kAlgoWave)
+        return fail(NNGP_EUNSUP, "the matern kind runs on the wavefront kernel (NNGP_ALGO_AUTO or WAVE), not algo %d",
+                    algo);
     const bool classic = dim == 2 && kind <= NNGP_COV_MATERN32;
     if (a == nngp::kAlgoLane && !classic)
         return fail(NNGP_EUNSUP, "the lane kernel serves 2-D exponential and Matern-3/2 only "
@@ -113,7 +119,7 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
 
     hipStream_t s = (hipStream_t)stream;
-    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, dim, sigma2, phi, tau2, order, values, qcoords,
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, dim, sigma2, phi, tau2, nu, order, values, qcoords,
                       qvalues, B, F, R, partials, (double*)workspace};
     hipError_t e = nngp::bf_launch(args, a, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep launch");
@@ -122,20 +128,20 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
 
 int nngp_bf_sweep(const double* coords, int64_t n_points, int32_t dim, const int32_t* nbr, const int32_t* order,
                   int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
-                  const double* values, double* B, double* F, double* R, double* partials, void* workspace,
+                  double nu, const double* values, double* B, double* F, double* R, double* partials, void* workspace,
                   size_t workspace_bytes, int32_t algo, void* stream) {
-    return bf_common(coords, n_points, dim, coords, n_points, nbr, order, n_rows, m, i0, kind, sigma2, phi, tau2,
+    return bf_common(coords, n_points, dim, coords, n_points, nbr, order, n_rows, m, i0, kind, sigma2, phi, tau2, nu,
                      values, values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
 int nngp_bf_cross(const double* ref, int64_t n_ref, int32_t dim, const double* query, int64_t n_query,
                   const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t q0, int32_t kind,
-                  double sigma2, double phi, double tau2, const double* ref_values, const double* query_values,
-                  double* B, double* F, double* R, double* partials, void* workspace, size_t workspace_bytes,
-                  int32_t algo, void* stream) {
+                  double sigma2, double phi, double tau2, double nu, const double* ref_values,
+                  const double* query_values, double* B, double* F, double* R, double* partials, void* workspace,
+                  size_t workspace_bytes, int32_t algo, void* stream) {
     if (query_values != nullptr && ref_values == nullptr)
         return fail(NNGP_EINVAL, "query_values need ref_values");
-    return bf_common(ref, n_ref, dim, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, ref_values,
+    return bf_common(ref, n_ref, dim, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, nu, ref_values,
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
@@ -143,7 +149,7 @@ int nngp_bf_finalize(const void* workspace, size_t workspace_bytes, int64_t n_ro
                      int32_t dim, int32_t algo, double* partials, void* stream) {
     if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
-    if (dim < 1 || dim > NNGP_MAX_DIM || kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_SPHERICAL)
+    if (dim < 1 || dim > NNGP_MAX_DIM || kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_MATERN)
         return fail(NNGP_EINVAL, "bad kind %d or dim %d", kind, dim);
     const int a = resolve_algo(algo, m, kind, dim);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)

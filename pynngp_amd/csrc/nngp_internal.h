@@ -87,6 +87,7 @@ struct BfArgs {
     int kind;
     int dim;                   // coordinate dimension (1..3)
     double sigma2, phi, tau2;
+    double nu;                 // smoothness of NNGP_KIND_MATERN (unused by the other kinds)
     const int32_t* order;      // (n_rows,) local row of nbr row t (nngp_row_order layout), or null (identity)
     const double* values;      // (n_points,) or null
     const double* qcoords;     // coordinates of the locations themselves: coords (sweep) or query points (cross)

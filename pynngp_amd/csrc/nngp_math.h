@@ -20,6 +20,7 @@
 #pragma once
 
 #include "exp2_table.h"
+#include "rgamma_series.h"
 
 #ifdef NNGP_MATH_HOST
 #include <math.h>
@@ -61,11 +62,17 @@ static __device__ const double kExp2Tab[256] = NNGP_EXP2_TAB;
 #define NNGP_KIND_MATERN52 2     // sigma2 (1 + u + u^2 / 3) e^-u
 #define NNGP_KIND_GAUSSIAN 3     // sigma2 e^-u^2          (no square root: the exponent is phi^2 d^2)
 #define NNGP_KIND_SPHERICAL 4    // sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0   (no exponential)
-#define NNGP_N_KINDS 5
-// Runtime kind (the m = 25..32 kernels, one instantiation for all five kinds): every kind as
+#define NNGP_KIND_MATERN 5       // sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), any smoothness nu (spNNGP's
+                                 // "matern"; nu = 1/2, 3/2, 5/2 give the exponential / Matern-3/2 / -5/2 kinds)
+#define NNGP_N_KINDS 6
+#define NNGP_MATERN_NU_MAX 50.0
+#ifndef NNGP_MATERN_X_SWITCH
+#define NNGP_MATERN_X_SWITCH 1.5  // Temme below, the continued fraction above (the most accurate split, tests/test_matern.py)
+#endif
+// Runtime kind (the m = 25..32 kernels, one instantiation for kinds 0..4): every kind as
 // p(u) e, p(u) = 1 + c1 u + c2 u^2 + c3 u^3 with u = min(phi d, umax), e = 2^(nphi256 g / 256) with
 // g = d (g = d^2 for the gaussian kind; nphi256 = 0, i.e. e = 1, for the spherical kind).
-#define NNGP_KIND_GENERIC 5
+#define NNGP_KIND_GENERIC 7
 
 // Covariance parameters, built once on the host (nngp_cov_params) and passed by value.
 struct CovParams {
@@ -79,6 +86,10 @@ struct CovParams {
     double c[3];     // NNGP_KIND_GENERIC: polynomial coefficients c1, c2, c3 of the kind
     double umax;     // NNGP_KIND_GENERIC: u = phi d is clamped at umax (1 for the spherical kind)
     int gauss;       // NNGP_KIND_GENERIC: the exponent's variable is d^2 (gaussian), else d
+    // NNGP_KIND_MATERN (nngp_matern_setup): nu = nl + mu, |mu| <= 1/2; Temme's Gamma_1(mu), Gamma_2(mu),
+    // Gamma(1 + mu), Gamma(1 - mu), mu pi / sin(mu pi), and the scale 2^(1 - nl) / Gamma(nu)
+    double nu, mu, mg1, mg2, mgp, mgm, mfac, mscale;
+    int mnl;
 };
 
 NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double tau2) {
@@ -91,6 +102,11 @@ NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double ta
     } else if (kind == NNGP_KIND_SPHERICAL) {
         p.nphi256 = 0.0;
         p.d2max = 4.0 / (phi * phi);  // any d2 past (1/phi)^2 gives 0; the clamp keeps sqrt in range
+    } else if (kind == NNGP_KIND_MATERN) {
+        p.nphi256 = 0.0;
+        // u = 1500 (+ 30 nu below, nngp_matern_setup): e^-u underflows, so the covariance is exactly 0
+        // (far-away padding points decouple) and u^nu stays finite
+        p.d2max = (1500.0 / phi) * (1500.0 / phi);
     } else {
         p.nphi256 = -256.0 * (phi * NNGP_LOG2E);
         // 2^-1080 sigma2 == 0; the polynomial factor of the Matern kinds (<= 1 + u + u^2/3 at
@@ -106,7 +122,145 @@ NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double ta
     p.c[2] = kind == NNGP_KIND_SPHERICAL ? 0.5 : 0.0;
     p.umax = kind == NNGP_KIND_SPHERICAL ? 1.0 : 1e300;
     p.gauss = kind == NNGP_KIND_GAUSSIAN;
+    p.nu = p.mu = p.mg1 = p.mg2 = p.mgp = p.mgm = p.mfac = p.mscale = 0.0;
+    p.mnl = 0;
     return p;
+}
+
+// ---------------------------------------------------------------- Matern, general smoothness nu
+// rho(u) = u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), u = phi d (spNNGP's parameterisation: nu = 3/2 is
+// (1 + u) e^-u).  nu = nl + mu with nl = floor(nu + 1/2), |mu| <= 1/2.  K_mu and K_{mu+1} come from
+// Temme's series (u <= 1.5) or the Thompson-Barnett continued fraction (u > 1.5), K_nu from the upward
+// recurrence.  Everything is carried scaled, J_k = u^k (u/2)^mu K_{mu+k}(u), so that
+//   rho(u) = 2^(1 - nl) / Gamma(nu) * J_nl,   J_{k+1} = 2 (mu + k) J_k + u^2 J_{k-1}
+// (positive terms only) and the small-u limit (J_nl -> 2^(nl-1) Gamma(nu)) involves no large
+// exponential: the scaling removes the (u/2)^-mu of Temme's p-series exactly.
+// Host part: the per-theta constants (1 / Gamma(1 +- mu) from the entire series of
+// rgamma_series.h, so Temme's Gamma_1 = (1/Gamma(1-mu) - 1/Gamma(1+mu)) / (2 mu) is its odd part
+// without cancellation).
+NNGP_HD void nngp_matern_setup(CovParams& p, double nu) {
+    const double a[NNGP_RGAMMA_N] = NNGP_RGAMMA_COEF;
+    const double nlf = floor(nu + 0.5);
+    const double mu = nu - nlf;
+    double gp = 0.0, gm = 0.0, g1 = 0.0, g2 = 0.0;  // 1/Gamma(1+mu), 1/Gamma(1-mu), odd / even parts
+    for (int k = NNGP_RGAMMA_N - 1; k >= 0; --k) {
+        gp = fma(gp, mu, a[k]);
+        gm = fma(gm, -mu, a[k]);
+    }
+    for (int k = NNGP_RGAMMA_N - 1 - ((NNGP_RGAMMA_N - 1) % 2 == 0); k >= 1; k -= 2) g1 = fma(g1, mu * mu, a[k]);
+    for (int k = NNGP_RGAMMA_N - 1 - ((NNGP_RGAMMA_N - 1) % 2 == 1); k >= 0; k -= 2) g2 = fma(g2, mu * mu, a[k]);
+    p.nu = nu;
+    p.mu = mu;
+    p.mnl = (int)nlf;
+    p.mg1 = -g1;  // Gamma_1(mu) = -sum_{k odd} a_k mu^(k-1)
+    p.mg2 = g2;   // Gamma_2(mu) = sum_{k even} a_k mu^k
+    p.mgp = 1.0 / gp;  // Gamma(1 + mu)
+    p.mgm = 1.0 / gm;  // Gamma(1 - mu)
+    const double pm = 3.141592653589793 * mu;
+    p.mfac = mu == 0.0 ? 1.0 : pm / sin(pm);
+    // Gamma(nu) = Gamma(1 + mu) prod_{j=1}^{nl-1} (j + mu)   (nl = 0: Gamma(mu) = Gamma(1 + mu) / mu)
+    double gnu = p.mgp;
+    if (p.mnl == 0) gnu /= mu;
+    for (int j = 1; j < p.mnl; ++j) gnu *= (double)j + mu;
+    p.mscale = ldexp(1.0, 1 - p.mnl) / gnu;
+    const double umax = 1500.0 + 30.0 * nu;
+    p.d2max = (umax / p.phi) * (umax / p.phi);
+}
+
+NNGP_HD CovParams nngp_cov_params_nu(int kind, double sigma2, double phi, double tau2, double nu) {
+    CovParams p = nngp_cov_params(kind, sigma2, phi, tau2);
+    if (kind == NNGP_KIND_MATERN) nngp_matern_setup(p, nu);
+    return p;
+}
+
+// sinh(s) / s (a series below |s| = 1/2, where sinh loses bits to the cancellation of its exponentials)
+NNGP_HD double nngp_sinhc(double s) {
+    if (fabs(s) < 0.5) {
+        const double z = s * s;  // sum_k z^k / (2k + 1)!, k <= 8: the next term is below 2^-70
+        double t = 1.0 / 355687428096000.0;  // 1/17!
+        t = fma(t, z, 1.0 / 1307674368000.0);
+        t = fma(t, z, 1.0 / 6227020800.0);
+        t = fma(t, z, 1.0 / 39916800.0);
+        t = fma(t, z, 1.0 / 362880.0);
+        t = fma(t, z, 1.0 / 5040.0);
+        t = fma(t, z, 1.0 / 120.0);
+        t = fma(t, z, 1.0 / 6.0);
+        return fma(t, z, 1.0);
+    }
+    return sinh(s) / s;
+}
+
+// J_0 = (x/2)^mu K_mu(x), J_1 = x (x/2)^mu K_{mu+1}(x) for x > 0
+NNGP_HD void nngp_matern_j01(const CovParams& P, double x, double& j0, double& j1) {
+    const double mu = P.mu;
+    if (x <= NNGP_MATERN_X_SWITCH) {
+        // Temme (1975): K_mu = sum_k c_k f_k, K_{mu+1} = (2/x) sum_k c_k (p_k - k f_k), c_k = (x^2/4)^k / k!,
+        // f_0 = (mu pi / sin mu pi) (Gamma_1 cosh s + Gamma_2 L sinh(s) / s), s = mu L, L = ln(2/x),
+        // p_0 = (x/2)^-mu Gamma(1+mu) / 2, q_0 = (x/2)^mu Gamma(1-mu) / 2,
+        // f_k = (k f_{k-1} + p_{k-1} + q_{k-1}) / (k^2 - mu^2), p_k = p_{k-1} / (k - mu), q_k = q_{k-1} / (k + mu);
+        // here every f, p, q carries the factor E = (x/2)^mu = e^-s
+        const double L = -log(0.5 * x);
+        const double s = mu * L;
+        const double E = exp(-s);
+        double f = P.mfac * (P.mg1 * (0.5 * fma(E, E, 1.0)) + P.mg2 * L * (E * nngp_sinhc(s)));
+        double pk = 0.5 * P.mgp;
+        double qk = 0.5 * (E * E) * P.mgm;
+        const double hh = 0.25 * x * x;
+        double c = 1.0, s0 = f, s1 = pk;
+        for (int k = 1; k < 60; ++k) {
+            const double dk = (double)k;
+            f = (dk * f + pk + qk) / fma(dk, dk, -mu * mu);
+            c *= hh / dk;
+            pk /= dk - mu;
+            qk /= dk + mu;
+            const double t0 = c * f, t1 = c * fma(-dk, f, pk);
+            s0 += t0;
+            s1 += t1;
+            if (fabs(t0) <= 0x1p-56 * fabs(s0) && fabs(t1) <= 0x1p-56 * fabs(s1)) break;
+        }
+        j0 = s0;
+        j1 = 2.0 * s1;
+    } else {
+        // Thompson & Barnett (1987), Steed's evaluation of the continued fraction for K_{mu+1} / K_mu
+        // together with the sum S giving K_mu = sqrt(pi / 2x) e^-x / S (x > 1.5: a few dozen terms)
+        const double a1 = 0.25 - mu * mu;
+        double b = 2.0 * (1.0 + x), d = 1.0 / b, dh = d, h = d;
+        double q0 = 0.0, q1 = 1.0, q = a1, c = a1, a = -a1, S = fma(q, dh, 1.0);
+        for (int i = 1; i < 400; ++i) {
+            const double di = (double)i;
+            a -= 2.0 * di;
+            c = -a * c / (di + 1.0);
+            const double qn = (q0 - b * q1) / a;
+            q0 = q1;
+            q1 = qn;
+            q = fma(c, qn, q);
+            b += 2.0;
+            d = 1.0 / fma(a, d, b);
+            dh = fma(b, d, -1.0) * dh;
+            h += dh;
+            const double dS = q * dh;
+            S += dS;
+            if (fabs(dS) <= 0x1p-56 * fabs(S)) break;
+        }
+        const double E = exp(mu * log(0.5 * x));
+        j0 = E * sqrt(1.5707963267948966 / x) * exp(-x) / S;
+        j1 = j0 * (mu + x + 0.5 - a1 * h);
+    }
+}
+
+// rho(u) for u >= 0 (u = 0: the limit 1)
+NNGP_HD double nngp_matern_rho(const CovParams& P, double u) {
+    if (!(u > 0.0)) return 1.0;
+    double j0, j1;
+    nngp_matern_j01(P, u, j0, j1);
+    if (P.mnl == 0) return P.mscale * j0;
+    const double u2 = u * u;
+    for (int k = 1; k < P.mnl; ++k) {
+        const double j2 = fma(2.0 * (P.mu + (double)k), j1, u2 * j0);
+        j0 = j1;
+        j1 = j2;
+    }
+    return P.mscale * j1;
 }
 
 #ifndef NNGP_MATH_HOST
@@ -166,6 +320,7 @@ NNGP_FN double nngp_cov_d2(const CovParams& P, const double* tab, double d2) {
     const double x = fmin(d2, P.d2max);
     if (KIND == NNGP_KIND_GAUSSIAN) return nngp_exp_tab(P, tab, x);  // sigma2 2^(nphi256 d2 / 256)
     const double d = nngp_sqrt(x);
+    if (KIND == NNGP_KIND_MATERN) return P.sigma2 * nngp_matern_rho(P, P.phi * d);
     if (KIND == NNGP_KIND_GENERIC) {  // runtime kind (nngp_cov_unit's generic branch, sigma2 in the table)
         const double e = nngp_exp_tab(P, tab, P.gauss ? x : d);
         const double u = fmin(P.phi * d, P.umax);

@@ -111,7 +111,7 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
                   int64_t kind, double sigma2, double phi, double tau2, const c10::optional<at::Tensor>& values,
                   const c10::optional<at::Tensor>& B, const c10::optional<at::Tensor>& F,
                   const c10::optional<at::Tensor>& R, const at::Tensor& partials, const at::Tensor& ws,
-                  int64_t algo) {
+                  int64_t algo, double nu) {
     check_coords(coords, "coords");
     const at::OptionalDeviceGuard guard(coords.device());
     check_nbr(nbr, coords);
@@ -129,7 +129,7 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
     TORCH_CHECK(ws.is_contiguous(), "workspace must be contiguous");
     check_same_device(coords, ws, "workspace");
     check_rc(nngp_bf_sweep(coords.data_ptr<double>(), n, (int32_t)d, nbr.data_ptr<int32_t>(), ptr<int32_t>(order), rows,
-                           (int32_t)m, i0, (int32_t)kind, sigma2, phi, tau2, ptr<double>(values), ptr<double>(B),
+                           (int32_t)m, i0, (int32_t)kind, sigma2, phi, tau2, nu, ptr<double>(values), ptr<double>(B),
                            ptr<double>(F), ptr<double>(R), partials.data_ptr<double>(), ws.data_ptr(),
                            (size_t)ws.nbytes(), (int32_t)algo, stream(coords)),
              "nngp_bf_sweep");
@@ -138,7 +138,8 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_sweep(const at::Tensor& coords, const at::Tensor& nbr, int64_t i0,
                                                         int64_t kind, double sigma2, double phi, double tau2,
                                                         const c10::optional<at::Tensor>& values, bool want_bf,
-                                                        int64_t algo, const c10::optional<at::Tensor>& order) {
+                                                        int64_t algo, const c10::optional<at::Tensor>& order,
+                                                        double nu) {
     check_coords(coords, "coords");
     const at::OptionalDeviceGuard guard(coords.device());
     check_nbr(nbr, coords);
@@ -151,14 +152,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_sweep(const at::Tensor& coords
                                                                (int32_t)coords.size(1), (int32_t)algo), coords);
     bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values,
                  want_bf ? c10::optional<at::Tensor>(B) : c10::nullopt,
-                 want_bf ? c10::optional<at::Tensor>(F) : c10::nullopt, c10::nullopt, p, ws, algo);
+                 want_bf ? c10::optional<at::Tensor>(F) : c10::nullopt, c10::nullopt, p, ws, algo, nu);
     return {B, F, p};
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, const at::Tensor& query,
                                                         const at::Tensor& nbr, int64_t kind, double sigma2, double phi,
                                                         double tau2, const c10::optional<at::Tensor>& ref_values,
-                                                        int64_t algo) {
+                                                        int64_t algo, double nu) {
     check_coords(ref, "ref");
     const at::OptionalDeviceGuard guard(ref.device());
     check_coords(query, "query");
@@ -174,7 +175,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
                                                                (int32_t)algo), ref);
     check_rc(nngp_bf_cross(ref.data_ptr<double>(), ref.size(0), (int32_t)d, query.data_ptr<double>(), query.size(0),
                            nbr.data_ptr<int32_t>(), nullptr, rows, (int32_t)m, 0, (int32_t)kind, sigma2, phi, tau2,
-                           ptr<double>(ref_values), nullptr, B.data_ptr<double>(), F.data_ptr<double>(),
+                           nu, ptr<double>(ref_values), nullptr, B.data_ptr<double>(), F.data_ptr<double>(),
                            ref_values.has_value() ? R.data_ptr<double>() : nullptr, p.data_ptr<double>(),
                            ws.data_ptr(), ws.nbytes(), (int32_t)algo, stream(ref)),
              "nngp_bf_cross");
@@ -223,12 +224,12 @@ TORCH_LIBRARY(nngp, m) {
     m.def("knn_prior_rows(Tensor coords, int m, Tensor rows) -> Tensor");
     m.def("knn_query(Tensor ref, Tensor query, int k) -> Tensor");
     m.def("bf_sweep(Tensor coords, Tensor nbr, int i0, int kind, float sigma2, float phi, float tau2, Tensor? values, "
-          "bool want_bf, int algo, Tensor? order=None) -> (Tensor, Tensor, Tensor)");
+          "bool want_bf, int algo, Tensor? order=None, float nu=-1.0) -> (Tensor, Tensor, Tensor)");
     m.def("bf_sweep_out(Tensor coords, Tensor nbr, Tensor? order, int i0, int kind, float sigma2, float phi, "
           "float tau2, Tensor? values, Tensor(a!)? B, Tensor(b!)? F, Tensor(c!)? R, Tensor(d!) partials, "
-          "Tensor(e!) workspace, int algo) -> ()");
+          "Tensor(e!) workspace, int algo, float nu=-1.0) -> ()");
     m.def("bf_cross(Tensor ref, Tensor query, Tensor nbr, int kind, float sigma2, float phi, float tau2, "
-          "Tensor? ref_values, int algo) -> (Tensor, Tensor, Tensor)");
+          "Tensor? ref_values, int algo, float nu=-1.0) -> (Tensor, Tensor, Tensor)");
     m.def("row_order(Tensor coords, int i0, int rows, Tensor? nbr) -> (Tensor, Tensor)");
     m.def("combine_partials_out(Tensor gathered, Tensor(a!) out) -> ()");
 }

@@ -96,10 +96,12 @@ class SeqNNGP:
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
                  seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
-                 ref=None, X_ref=None):
+                 ref=None, X_ref=None, nu: Optional[float] = None):
         self.device = _default_device(device)
         dev = self.device
         self.kind = kind
+        self._nu_arg = _lib._check_kind(kind, nu)  # the matern kind's (fixed) smoothness; -1 otherwise
+        self.nu = nu if kind == "matern" else None
         self.m = int(m)
         if not 1 <= self.m <= _lib.MAX_M:
             raise ValueError(f"m={m} outside [1, {_lib.MAX_M}]")
@@ -308,7 +310,7 @@ class SeqNNGP:
     def _sweep_into(self, phi, B, Ft, r):
         """Factors of the unit-variance NNGP at phi, and residuals of the current w."""
         torch.ops.nngp.bf_sweep_out(self.coords, self.nbr, None, 0, self._kind_code, 1.0, float(phi), 0.0, self.w, B,
-                                    Ft, r, self._part, self._ws, self._algo_code)
+                                    Ft, r, self._part, self._ws, self._algo_code, self._nu_arg)
 
     @staticmethod
     def _check(p):
@@ -433,7 +435,7 @@ class SeqNNGP:
 
     # ------------------------------------------------------------------ checkpoint / resume
     def _settings(self) -> dict:
-        return {"algo": self.algo, "phi_tuning": self.phi_tuning, "fix_tau2": self.fix_tau2,
+        return {"algo": self.algo, "phi_tuning": self.phi_tuning, "fix_tau2": self.fix_tau2, "nu": self.nu,
                 "priors": {k: list(v) for k, v in dataclasses.asdict(self.priors).items()},
                 "n_t": self.n_t, "n_obs": self.n_obs, "n_colors": int(self.n_colors)}
 

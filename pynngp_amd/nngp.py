@@ -44,7 +44,9 @@ class Covariance:
 
     ``exponential`` sigma2 e^-u; ``matern32`` sigma2 (1 + u) e^-u; ``matern52``
     sigma2 (1 + u + u^2/3) e^-u; ``gaussian`` sigma2 e^-u^2; ``spherical``
-    sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family, fused in the kernels).
+    sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0 (the spNNGP family, fused in the kernels);
+    ``matern`` sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) for any smoothness ``nu`` in (0, 50]
+    (spNNGP's "matern"; served by the wavefront kernel, nngp.h NNGP_COV_MATERN).
     ``tau2`` is a nugget added to the diagonal (response model; 0 = latent model).
     Called as ``cov(a, b)`` on coordinate rows of any dimension (numpy or torch), it
     returns the cross-covariance matrix without the nugget, like a reference plug-in would.
@@ -54,12 +56,19 @@ class Covariance:
     sigma2: float
     phi: float
     tau2: float = 0.0
+    nu: Optional[float] = None  # smoothness of the ``matern`` kind (None for the others)
 
     def __post_init__(self):
         if self.kind not in _lib.KIND_CODES:
             raise ValueError(f"unknown covariance kind {self.kind!r}; expected one of {sorted(_lib.KIND_CODES)}")
         if not (self.sigma2 > 0 and self.phi > 0 and self.tau2 >= 0):
             raise ValueError("need sigma2 > 0, phi > 0, tau2 >= 0")
+        _lib._check_kind(self.kind, self.nu)
+
+    @property
+    def nu_arg(self) -> Optional[float]:
+        """``nu`` as the sweeps take it (None unless the kind is ``matern``)."""
+        return float(self.nu) if self.kind == "matern" else None
 
     @property
     def theta(self):
@@ -75,6 +84,15 @@ class Covariance:
         b = b.reshape(-1, d)
         t = a[:, None, :] - b[None, :, :]
         u = self.phi * lib.sqrt((t * t).sum(-1))
+        if self.kind == "matern":  # K_nu of real order: scipy on the host (torch has only K_0, K_1)
+            from scipy import special
+            un = u.detach().cpu().numpy() if lib is torch else u
+            us = np.where(un > 0, un, 1.0)
+            with np.errstate(over="ignore", under="ignore", invalid="ignore", divide="ignore"):
+                k = special.kv(self.nu, us)
+                r = np.exp(self.nu * np.log(us) - (self.nu - 1.0) * np.log(2.0) - special.gammaln(self.nu) + np.log(k))
+            r = self.sigma2 * np.where((un > 0) & np.isfinite(k), r, 1.0)
+            return torch.as_tensor(r, dtype=u.dtype, device=u.device) if lib is torch else r
         if self.kind == "gaussian":
             return self.sigma2 * lib.exp(-u * u)
         if self.kind == "spherical":
@@ -231,7 +249,7 @@ class NNGP:
         if nbr.shape[1] == 0:  # m = 0: the marginal
             return np.zeros(n), np.full(n, cv.sigma2 + cv.tau2)
         R = torch.empty(n, dtype=torch.float64, device=self.device)
-        _, F, p = _lib.bf_cross(self._s_dev, q, nbr, cv.kind, *cv.theta, ref_values=v, algo=algo, R=R)
+        _, F, p = _lib.bf_cross(self._s_dev, q, nbr, cv.kind, *cv.theta, ref_values=v, algo=algo, R=R, nu=cv.nu_arg)
         _raise_on_bad(p.cpu().numpy())
         return (-R).cpu().numpy(), F.cpu().numpy()
 
@@ -278,7 +296,7 @@ class NNGP:
 
     def _row_bf(self, i):
         cv = self._covariance()
-        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr[i: i + 1], int(i), cv.kind, *cv.theta)
+        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr[i: i + 1], int(i), cv.kind, *cv.theta, nu=cv.nu_arg)
         _raise_on_bad(p.cpu().numpy())
         k = min(int(i), self.m)
         return B[0, :k].cpu().numpy(), float(F[0].item())
@@ -295,7 +313,8 @@ class NNGP:
     def compute_BF(self, algo: str = "auto"):
         """All B (N, m) and F (N,) as device tensors (one fused sweep)."""
         cv = self._covariance()
-        B, F, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, algo=algo, order=self._order)
+        B, F, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, algo=algo, order=self._order,
+                                nu=cv.nu_arg)
         _raise_on_bad(p.cpu().numpy())
         self._B, self._F = B, F
         return B, F
@@ -317,7 +336,7 @@ class NNGP:
         if v.dim() != 1:
             raise ValueError("loglik needs one value per location (1-D values)")
         _, _, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, values=v, want_bf=False,
-                                algo=algo, order=self._order)
+                                algo=algo, order=self._order, nu=cv.nu_arg)
         ph = p.cpu().numpy()
         _raise_on_bad(ph)
         n = self.nbr.shape[0]
@@ -340,6 +359,7 @@ class NNGP:
         ry = torch.empty(n, dtype=torch.float64, device=self.device)
         r1 = torch.empty_like(ry)
         kw = dict(algo=algo, order=self._order)
+        kw["nu"] = cov.nu_arg
         _, F, py = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=v, R=ry, **kw)
         ones = torch.ones_like(v)
         _, _, p1 = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=ones, R=r1, **kw)
@@ -352,16 +372,19 @@ class NNGP:
         return -0.5 * (n * LOG_2PI + logF + quad), float(mu)
 
     def fit(self, kind: Optional[str] = None, x0=None, mean: str = "constant", fix_tau2: Optional[float] = None,
-            method: str = "Nelder-Mead", maxiter: int = 400, algo: str = "auto"):
+            method: str = "Nelder-Mead", maxiter: int = 400, algo: str = "auto", nu: Optional[float] = None):
         """Maximum-likelihood (sigma2, phi, tau2) of the NNGP response model on S = T, each
         objective evaluation one or two fused GPU sweeps (scipy.optimize on log-parameters).
         ``x0`` defaults to ``cov``'s theta; ``fix_tau2`` holds the nugget fixed (e.g. 0 for the
-        latent model).  Sets ``cov`` to the estimate and returns a dict with theta, mu,
-        loglik and the optimizer's evaluation count."""
+        latent model); ``nu`` the (fixed) smoothness of the ``matern`` kind, default ``cov``'s.
+        Sets ``cov`` to the estimate and returns a dict with theta, mu, loglik and the
+        optimizer's evaluation count."""
         from scipy.optimize import minimize
 
         base = self.cov if isinstance(self.cov, Covariance) else None
         kind = kind or (base.kind if base is not None else "exponential")
+        if nu is None and base is not None and base.kind == kind:
+            nu = base.nu
         th0 = tuple(x0) if x0 is not None else (base.theta if base is not None else (1.0, 10.0, 0.1))
         free_tau = fix_tau2 is None
         z0 = [math.log(th0[0]), math.log(th0[1])] + ([math.log(max(th0[2], 1e-6))] if free_tau else [])
@@ -374,7 +397,7 @@ class NNGP:
         def obj(z):
             th = theta_of(z)
             try:
-                ll, mu = self.profile_loglik(Covariance(kind, *th), mean=mean, algo=algo)
+                ll, mu = self.profile_loglik(Covariance(kind, *th, nu=nu), mean=mean, algo=algo)
             except NNGPNumericalError:
                 return 1e300
             if ll > best["ll"]:
@@ -384,7 +407,7 @@ class NNGP:
         res = minimize(obj, np.array(z0), method=method, options={"maxiter": maxiter, "xatol": 1e-6,
                                                                   "fatol": 1e-9} if method == "Nelder-Mead"
                        else {"maxiter": maxiter})
-        self.cov = Covariance(kind, *best["theta"])
+        self.cov = Covariance(kind, *best["theta"], nu=nu)
         self._B = self._F = None
         return {"theta": best["theta"], "mu": best["mu"], "loglik": best["ll"], "n_evals": int(res.nfev),
                 "converged": bool(res.success)}
@@ -417,7 +440,7 @@ class NNGP:
                     sampler_kw["eps"] = ev
             ref = None if self._same_sets() else self.s
             smp = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi, seed=seed,
-                          device=self.device, ref=ref, **sampler_kw)
+                          device=self.device, ref=ref, nu=cv.nu_arg, **sampler_kw)
             ws = np.asarray(self.ws, dtype=np.float64)
             smp.set_w(ws=np.where(np.isfinite(ws), ws, 0.0),
                       wt=None if ref is None else np.where(np.isfinite(self.wt), self.wt, 0.0))

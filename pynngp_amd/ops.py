@@ -11,15 +11,16 @@ for tracing.
     torch.ops.nngp.knn_prior(coords, m, q0, q1) -> nbr
     torch.ops.nngp.knn_prior_rows(coords, m, rows) -> nbr
     torch.ops.nngp.knn_query(ref, query, k) -> nbr
-    torch.ops.nngp.bf_sweep(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None)
+    torch.ops.nngp.bf_sweep(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None, nu=-1.0)
         -> (B, F, partials)
     torch.ops.nngp.bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials,
-                                workspace, algo) -> ()       # the hot path: caller-owned buffers
-    torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo) -> (B, F, mean)
+                                workspace, algo, nu=-1.0) -> ()       # the hot path: caller-owned buffers
+    torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo, nu=-1.0) -> (B, F, mean)
     torch.ops.nngp.row_order(coords, i0, rows, nbr) -> (order, nbr_sorted)
     torch.ops.nngp.combine_partials_out(gathered, out) -> ()
 
-``kind`` / ``algo`` are the integer codes of include/nngp.h (:func:`kind_code`, :func:`algo_code`).
+``kind`` / ``algo`` are the integer codes of include/nngp.h (:func:`kind_code`, :func:`algo_code`);
+``nu`` is the smoothness of the ``matern`` kind (0 < nu <= 50; ignored by the other kinds).
 """
 from __future__ import annotations
 
@@ -29,7 +30,7 @@ import torch
 
 from . import _lib
 
-_KINDS = tuple(_lib.KIND_CODES)  # code order: exponential, matern32, matern52, gaussian, spherical
+_KINDS = tuple(_lib.KIND_CODES)  # code order: exponential, matern32, matern52, gaussian, spherical, matern
 _ALGOS = dict(_lib.ALGO_CODES)
 # always the in-tree build; it binds to whichever libnngp_hip.so _lib loaded first (matched by
 # SONAME, so an NNGP_LIB variant build is the one the operators call)
@@ -70,18 +71,18 @@ def _register_fakes() -> None:
         return query.new_empty((query.shape[0], k), dtype=torch.int32)
 
     @fake("bf_sweep")
-    def _(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None):
+    def _(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None, nu=-1.0):
         rows, m = nbr.shape
         if want_bf:
             return coords.new_empty((rows, m)), coords.new_empty((rows,)), coords.new_empty((4,))
         return coords.new_empty((0, m)), coords.new_empty((0,)), coords.new_empty((4,))
 
     @fake("bf_sweep_out")
-    def _(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials, workspace, algo):
+    def _(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials, workspace, algo, nu=-1.0):
         return None
 
     @fake("bf_cross")
-    def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo):
+    def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo, nu=-1.0):
         rows, m = nbr.shape
         return query.new_empty((rows, m)), query.new_empty((rows,)), query.new_empty((rows,))
 
@@ -112,8 +113,10 @@ def algo_code(algo: str) -> int:
 def bf_sweep_out(coords, nbr, order, i0, kind: str, theta, values, B, F, R, partials, workspace,
                  algo: str = "auto") -> None:
     """The fused sweep into caller-owned buffers through ``torch.ops.nngp.bf_sweep_out``
-    (stream-ordered on torch's current stream, no host synchronisation)."""
+    (stream-ordered on torch's current stream, no host synchronisation).  ``theta`` =
+    (sigma2, phi, tau2), or (sigma2, phi, tau2, nu) for the ``matern`` kind."""
     load()
+    nu = float(theta[3]) if len(theta) > 3 else -1.0
     torch.ops.nngp.bf_sweep_out(coords, nbr, order, int(i0), kind_code(kind), float(theta[0]), float(theta[1]),
-                                float(theta[2]), values, B, F, R, partials, workspace, algo_code(algo))
+                                float(theta[2]), values, B, F, R, partials, workspace, algo_code(algo), nu)
 

@@ -155,10 +155,12 @@ class ShardedLogLik:
         s2, phi, tau2 = cov.theta
         if self.api == "ctypes":  # the same C-ABI call without the dispatcher (A/B of the op overhead)
             _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, s2, phi, tau2, values=values,
-                          want_bf=want_bf, algo=self.algo, B=B, F=F, partials=p, workspace=self._ws, order=self.order)
+                          want_bf=want_bf, algo=self.algo, B=B, F=F, partials=p, workspace=self._ws, order=self.order,
+                          nu=cov.nu_arg)
             return p
         self._sweep_op(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
-                       float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws, self._algo_code)
+                       float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws, self._algo_code,
+                       -1.0 if cov.nu_arg is None else cov.nu_arg)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,

@@ -60,12 +60,12 @@ def test_workspace_sizes(lib):
 
 def _sweep(lib, **kw):
     a = dict(coords=1, n_points=10, dim=2, nbr=1, n_rows=10, m=15, i0=0, kind=0, sigma2=1.0, phi=1.0, tau2=0.0,
-             values=None, B=None, F=None, partials=1, workspace=256, workspace_bytes=1 << 20, algo=0, stream=None)
+             nu=-1.0, values=None, B=None, F=None, partials=1, workspace=256, workspace_bytes=1 << 20, algo=0, stream=None)
     a.update(kw)
     P = lambda v: None if v is None else ctypes.c_void_p(v)  # noqa: E731
     return lib.nngp_bf_sweep(P(a["coords"]), a["n_points"], a["dim"], P(a["nbr"]), None, a["n_rows"], a["m"], a["i0"],
                              a["kind"],
-                             a["sigma2"], a["phi"], a["tau2"], P(a["values"]), P(a["B"]), P(a["F"]), P(a.get("R")),
+                             a["sigma2"], a["phi"], a["tau2"], a["nu"], P(a["values"]), P(a["B"]), P(a["F"]), P(a.get("R")),
                              P(a["partials"]), P(a["workspace"]), a["workspace_bytes"], a["algo"], P(a["stream"]))
 
 
@@ -95,6 +95,11 @@ def _sweep(lib, **kw):
     (dict(algo=9), -1, "unknown algo"),
     (dict(workspace_bytes=16), -1, "workspace too small"),
     (dict(R=256), -1, "R (residuals) needs values"),
+    (dict(kind=5, nu=0.0), -1, "nu"),  # general-smoothness Matern: 0 < nu <= 50
+    (dict(kind=5, nu=50.5), -1, "nu"),
+    (dict(kind=5, nu=float("nan")), -1, "nu"),
+    (dict(kind=5, nu=1.2, algo=5), -4, "wavefront kernel"),
+    (dict(kind=5, nu=1.2, algo=1, m=8), -4, "wavefront kernel"),
 ])
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code
@@ -156,8 +161,9 @@ def test_check_partials_codes(lib):
 
 
 def test_resolve_algo_table(lib):
-    """auto: the blocked pair kernel for 1 <= m <= 32 at every kind and dimension, the wavefront
-    kernel above; explicit codes pass through."""
+    """auto: the blocked pair kernel for 1 <= m <= 24 and the four-lane kernel for 25..32 at kinds
+    0..4 and every dimension, the wavefront kernel above and for the general-smoothness Matern
+    kind (5) at every m; explicit codes pass through."""
     for m in (1, 15, 20, 24, 25, 32):
         for kind in range(5):
             for dim in (1, 2, 3):
@@ -165,6 +171,8 @@ def test_resolve_algo_table(lib):
     assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
     assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
     assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1
+    for m in (1, 15, 25, 40):
+        assert lib.nngp_resolve_algo(0, m, 5, 2) == 2
 
 
 def test_finalize_checks_workspace(lib):
