@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/${TAG:-r02ah}
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/${TAG:-r02ah}/tests.txt 2>&1 || exit 1
+timeout -k 10 900 python -u -m pytest -x -v --durations=25 --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/${TAG:-r02ah}/tests.txt 2>&1 || exit 1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG:-r02ah}/smoke.txt 2>&1 || exit 1
 for r in 1 2; do timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG:-r02ah}/bench_driver_$r.json 2> gpurun_out/${TAG:-r02ah}/bench_driver_$r.err || exit 1; done
 timeout -k 10 300 python bench.py > gpurun_out/${TAG:-r02ah}/bench_default.json 2> gpurun_out/${TAG:-r02ah}/bench_default.err || exit 1
