@@ -218,9 +218,13 @@ int nngp_combine_partials(const double *gathered, int32_t world, double *partial
  *   256-B aligned).  Call it again whenever B / Ft change (a new phi accepted).
  *   order: unused (accepted for compatibility; the preparation streams the reverse
  *   lists in their own order).
+ * nngp_gibbs_member_rows: member_rows[g] = (members[g], off[members[g]], off[members[g] + 1], 0)
+ *   (device int32 (n, 4), 16-B aligned) for `members` (device), the locations grouped by
+ *   colour -- built once per colouring; the colour steps then start with one coalesced
+ *   16-B load per member instead of two dependent loads.
  * nngp_gibbs_w_sweep: one sweep of w_i | rest over the colours in order;
- *   `members` (device) lists the locations grouped by colour, color_off_host
- *   (host, n_colors + 1) delimits them.  r (n,) holds the residuals
+ *   `member_rows` (nngp_gibbs_member_rows) lists the locations grouped by colour,
+ *   color_off_host (host, n_colors + 1) delimits them.  r (n,) holds the residuals
  *   w_i - B_i w_N(i) (nngp_bf_sweep's R), kept current in place with w.
  *   yres = y - X beta.  noise_w: NULL (homoscedastic noise, variance tau2) or n
  *   positive weights h_i, the noise variance of location i being tau2 / h_i (e.g.
@@ -243,10 +247,11 @@ size_t nngp_gibbs_prep_bytes(int64_t n, int32_t m);
 int nngp_gibbs_prepare(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
                        const int32_t *rev_k, const int32_t *order, int64_t n, int32_t m, void *prep,
                        size_t prep_bytes, void *stream);
-int nngp_gibbs_w_sweep(const int32_t *members, const int32_t *color_off_host, int32_t n_colors, const void *prep,
+int nngp_gibbs_member_rows(const int32_t *members, int64_t n, const int32_t *off, int32_t *member_rows, void *stream);
+int nngp_gibbs_w_sweep(const int32_t *member_rows, const int32_t *color_off_host, int32_t n_colors, const void *prep,
                        int64_t n, int32_t m, double sigma2, double tau2, const double *yres, const double *noise_w,
-                       double *w, double *r, const int32_t *off, const int32_t *rev_j, const double *z, uint64_t seed,
-                       uint64_t sweep, void *stream);
+                       double *w, double *r, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
+                       void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,

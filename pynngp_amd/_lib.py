@@ -38,6 +38,7 @@ SYMBOLS = (
     "nngp_color_moral_graph",
     "nngp_gibbs_prep_bytes",
     "nngp_gibbs_prepare",
+    "nngp_gibbs_member_rows",
     "nngp_gibbs_w_sweep",
     "nngp_gibbs_normals",
     "nngp_gibbs_stats_workspace_bytes",
@@ -107,7 +108,9 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_prep_bytes.restype = SZ
     lib.nngp_gibbs_prepare.argtypes = [P, P, P, P, P, P, I64, I32, P, SZ, P]
     lib.nngp_gibbs_prepare.restype = ctypes.c_int
-    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, P, U64, U64, P]
+    lib.nngp_gibbs_member_rows.argtypes = [P, I64, P, P, P]
+    lib.nngp_gibbs_member_rows.restype = ctypes.c_int
+    lib.nngp_gibbs_w_sweep.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P]
     lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
     lib.nngp_gibbs_normals.argtypes = [I64, U64, U64, P, P]
     lib.nngp_gibbs_normals.restype = ctypes.c_int
@@ -510,21 +513,40 @@ def _check_noise_w(noise_w: Optional[torch.Tensor], n: int) -> None:
         raise ValueError(f"noise_w must be a contiguous float64 ({n},) tensor")
 
 
+def gibbs_member_rows(members: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
+    """int32 (n, 4) rows (location, first / end reverse entry, 0) of the colour-ordered
+    ``members`` (nngp_gibbs_member_rows): build once per colouring, pass to :func:`gibbs_w_sweep`."""
+    dev = _require_gpu(members, off)
+    if members.dtype != torch.int32 or off.dtype != torch.int32 or members.dim() != 1:
+        raise ValueError("members and off must be int32, members 1-D")
+    members, off = members.contiguous(), off.contiguous()
+    rows = torch.empty((members.shape[0], 4), dtype=torch.int32, device=dev)
+    _check(load().nngp_gibbs_member_rows(_ptr(members), members.shape[0], _ptr(off), _ptr(rows), _stream(dev)),
+           "nngp_gibbs_member_rows")
+    return rows
+
+
 def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: int, sigma2: float,
                   tau2: float, yres: torch.Tensor, w: torch.Tensor, r: torch.Tensor, off: torch.Tensor,
                   rev_j: torch.Tensor, seed: int, sweep: int, z: Optional[torch.Tensor] = None,
-                  noise_w: Optional[torch.Tensor] = None) -> None:
+                  noise_w: Optional[torch.Tensor] = None, member_rows: Optional[torch.Tensor] = None) -> None:
     """One colour-ordered sweep of w_i | rest, in place on w and r (see include/nngp.h);
     ``prep`` from :func:`gibbs_prepare` for the current B / Ft; ``noise_w`` (n,) optional
-    weights h_i (noise variance tau2 / h_i)."""
+    weights h_i (noise variance tau2 / h_i); ``member_rows`` from :func:`gibbs_member_rows`
+    (built from ``members`` and ``off`` here when not given)."""
     import numpy as np
 
-    dev = _require_gpu(members, prep, yres, w, r, off, rev_j, z, noise_w)
+    dev = _require_gpu(members, prep, yres, w, r, off, rev_j, z, noise_w, member_rows)
     _check_noise_w(noise_w, w.shape[0])
+    if member_rows is None:
+        member_rows = gibbs_member_rows(members, off)
+    elif member_rows.dtype != torch.int32 or tuple(member_rows.shape) != (members.shape[0], 4) \
+            or not member_rows.is_contiguous():
+        raise ValueError("member_rows must be a contiguous int32 (n, 4) tensor from gibbs_member_rows")
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
     n = w.shape[0]
-    _check(load().nngp_gibbs_w_sweep(_ptr(members), co.ctypes.data, len(co) - 1, _ptr(prep), n, int(m),
-                                     float(sigma2), float(tau2), _ptr(yres), _ptr(noise_w), _ptr(w), _ptr(r), _ptr(off),
+    _check(load().nngp_gibbs_w_sweep(_ptr(member_rows), co.ctypes.data, len(co) - 1, _ptr(prep), n, int(m),
+                                     float(sigma2), float(tau2), _ptr(yres), _ptr(noise_w), _ptr(w), _ptr(r),
                                      _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")

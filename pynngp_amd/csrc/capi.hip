@@ -224,19 +224,29 @@ int nngp_gibbs_prepare(const double* B, const double* Ft, const int32_t* off, co
     return NNGP_OK;
 }
 
-int nngp_gibbs_w_sweep(const int32_t* members, const int32_t* color_off_host, int32_t n_colors, const void* prep,
+int nngp_gibbs_member_rows(const int32_t* members, int64_t n, const int32_t* off, int32_t* member_rows, void* stream) {
+    if (n < 0 || (n > 0 && (members == nullptr || off == nullptr || member_rows == nullptr)))
+        return fail(NNGP_EINVAL, "bad n or null pointer argument");
+    if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
+    hipError_t e = nngp::gibbs_member_rows_launch(members, n, off, member_rows, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_member_rows launch");
+    return NNGP_OK;
+}
+
+int nngp_gibbs_w_sweep(const int32_t* member_rows, const int32_t* color_off_host, int32_t n_colors, const void* prep,
                        int64_t n, int32_t m, double sigma2, double tau2, const double* yres, const double* noise_w,
-                       double* w, double* r, const int32_t* off, const int32_t* rev_j, const double* z, uint64_t seed,
-                       uint64_t sweep, void* stream) {
-    if (members == nullptr || color_off_host == nullptr || prep == nullptr || yres == nullptr || w == nullptr ||
-        r == nullptr || off == nullptr || (m > 0 && rev_j == nullptr))
+                       double* w, double* r, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
+                       void* stream) {
+    if (member_rows == nullptr || color_off_host == nullptr || prep == nullptr || yres == nullptr || w == nullptr ||
+        r == nullptr || (m > 0 && rev_j == nullptr))
         return fail(NNGP_EINVAL, "null pointer argument");
+    if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
     if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
     if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
-    hipError_t e = nngp::gibbs_w_sweep_launch(members, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres, noise_w,
-                                              w, r, off, rev_j, z, seed, sweep, (hipStream_t)stream);
+    hipError_t e = nngp::gibbs_w_sweep_launch(member_rows, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres,
+                                              noise_w, w, r, rev_j, z, seed, sweep, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
     return NNGP_OK;
 }

@@ -354,9 +354,11 @@ class SeqNNGP:
 
     def _sweep_colours(self, c0, c1):
         if c1 > c0:
+            if getattr(self, "_member_rows", None) is None:  # (location, reverse-entry range) per member, once
+                self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
             _lib.gibbs_w_sweep(self.members, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2, self.tau2,
                                self.yres, self.w, self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z,
-                               noise_w=self.noise_w)
+                               noise_w=self.noise_w, member_rows=self._member_rows)
 
     def update_wt(self):
         """w_t | w_S, y_t for the data locations outside S (nngp.py:99): the leaves of the DAG,
