@@ -328,6 +328,8 @@ def main():
                     help="ops: torch.ops.nngp.bf_sweep_out (default); ctypes: the same C ABI via ctypes (A/B)")
     ap.add_argument("--event-stride", type=int, default=10,
                     help="bracket every S-th timed sweep with HIP events for kernel_ms (1 = every sweep)")
+    ap.add_argument("--exchange-batch", type=int, default=16,
+                    help="sweeps whose (4,) partials share one all-gather (PipelinedCombine batch)")
     ap.add_argument("--force-collective", action="store_true",
                     help="exchange the partials through torch.distributed even on one rank (a one-rank RCCL group "
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
@@ -413,7 +415,7 @@ def main():
     # stream for the fold); every sweep's global partials are complete when the clock stops.
     # (Deferring the block-record fold to the side stream as well, nngp_bf_finalize, issued
     # 9x the host work per step and measured 0.35 vs 0.25 ms per step: the in-line fold stays.)
-    pipe = PipelinedCombine(sweep, args.steps)
+    pipe = PipelinedCombine(sweep, args.steps, batch=args.exchange_batch)
     t0 = time.perf_counter()
     for k in range(args.steps):
         if k in ev:
@@ -475,8 +477,9 @@ def main():
                 "write_BF": want_bf,
                 "sweep_api": "torch.ops.nngp.bf_sweep_out" if args.sweep_api == "ops" else "ctypes",
                 "global_batch": n_total,
-                "parallelism": f"dp{world} (contiguous Z-order location shards; one RCCL all-gather of 4 partials "
-                               "per sweep, overlapped with the next sweep)",
+                "parallelism": f"dp{world} (contiguous Z-order location shards; the (4,) partials of every "
+                               f"{args.exchange_batch} sweeps in one RCCL all-gather, overlapped with the next sweeps, "
+                               "then a rank-order fold)",
             },
             "roofline": {
                 "bound": "hbm",

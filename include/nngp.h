@@ -196,8 +196,14 @@ int nngp_row_order(const double *coords, int64_t n_points, int32_t dim, const in
  * partials[0..1] = sums, partials[2..3] = smallest non-negative flag or -1.
  * Every rank gets the bit-identical result.  No reference counterpart (the
  * reference is single-process).
+ * nngp_combine_partials_batch: the same fold for n_slots independent sweeps exchanged in ONE
+ * all-gather: gathered (world, n_slots, 4) rank-major (each rank contributed its (n_slots, 4)
+ * block), partials (n_slots, 4); slot k's result is bit-identical to nngp_combine_partials of
+ * that sweep alone.
  * ------------------------------------------------------------------------- */
 int nngp_combine_partials(const double *gathered, int32_t world, double *partials, void *stream);
+int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n_slots, double *partials,
+                                void *stream);
 
 /* ---------------------------------------------------------------------------
  * Gibbs sampler for the response model y = X beta + w + eps (SURVEY.md 8(f)

@@ -33,6 +33,7 @@ SYMBOLS = (
     "nngp_row_order_workspace_bytes",
     "nngp_row_order",
     "nngp_combine_partials",
+    "nngp_combine_partials_batch",
     "nngp_reverse_workspace_bytes",
     "nngp_reverse_neighbors",
     "nngp_color_moral_graph",
@@ -92,6 +93,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_row_order.argtypes = [P, I64, I32, P, I32, I64, I64, P, P, P, SZ, P]
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
+    lib.nngp_combine_partials_batch.argtypes = [P, I32, I64, P, P]
+    lib.nngp_combine_partials_batch.restype = ctypes.c_int
     lib.nngp_bf_finalize.argtypes = [P, ctypes.c_size_t, I64, I32, I32, I32, I32, P, P]
     lib.nngp_bf_finalize.restype = ctypes.c_int
     lib.nngp_resolve_algo.argtypes = [I32, I32, I32, I32]

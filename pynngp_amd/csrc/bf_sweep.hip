@@ -297,26 +297,31 @@ hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, 
     return hipGetLastError();
 }
 
-// Rank-order combination of all-gathered (world, 4) partials: sums for [0], [1],
-// smallest non-negative (else -1) for the bad-row flags [2], [3].
+// Rank-order combination of all-gathered partials: sums for [0], [1], smallest non-negative (else -1)
+// for the bad-row flags [2], [3].  g is (world, n_slots, 4) rank-major (an all-gather of each rank's
+// (n_slots, 4) block: a batch of independent sweeps in one collective); one thread per slot.
 __global__ __launch_bounds__(64) void combine_partials_kernel(const double* __restrict__ g, int world,
-                                                              double* __restrict__ out) {
-    if (threadIdx.x != 0) return;
+                                                              int64_t n_slots, double* __restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_slots) return;
     double a = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
     for (int r = 0; r < world; ++r) {
-        a += g[4 * r];
-        b += g[4 * r + 1];
-        if (g[4 * r + 2] >= 0.0) c = fmin(c, g[4 * r + 2]);
-        if (g[4 * r + 3] >= 0.0) d = fmin(d, g[4 * r + 3]);
+        const double* p = g + 4 * ((int64_t)r * n_slots + k);
+        a += p[0];
+        b += p[1];
+        if (p[2] >= 0.0) c = fmin(c, p[2]);
+        if (p[3] >= 0.0) d = fmin(d, p[3]);
     }
-    out[0] = a;
-    out[1] = b;
-    out[2] = c == INFINITY ? -1.0 : c;
-    out[3] = d == INFINITY ? -1.0 : d;
+    out[4 * k] = a;
+    out[4 * k + 1] = b;
+    out[4 * k + 2] = c == INFINITY ? -1.0 : c;
+    out[4 * k + 3] = d == INFINITY ? -1.0 : d;
 }
 
-hipError_t combine_partials_launch(const double* gathered, int world, double* out, hipStream_t s) {
-    hipLaunchKernelGGL(combine_partials_kernel, dim3(1), dim3(64), 0, s, gathered, world, out);
+hipError_t combine_partials_launch(const double* gathered, int world, int64_t n_slots, double* out, hipStream_t s) {
+    if (n_slots == 0) return hipSuccess;
+    hipLaunchKernelGGL(combine_partials_kernel, dim3((unsigned)((n_slots + 63) / 64)), dim3(64), 0, s, gathered, world,
+                       n_slots, out);
     return hipGetLastError();
 }
 

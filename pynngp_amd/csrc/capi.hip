@@ -167,12 +167,18 @@ int nngp_bf_finalize(const void* workspace, size_t workspace_bytes, int64_t n_ro
     return NNGP_OK;
 }
 
-int nngp_combine_partials(const double* gathered, int32_t world, double* partials, void* stream) {
+int nngp_combine_partials_batch(const double* gathered, int32_t world, int64_t n_slots, double* partials,
+                                void* stream) {
     if (gathered == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "gathered and partials must be non-null");
     if (world < 1) return fail(NNGP_EINVAL, "world=%d < 1", world);
-    hipError_t e = nngp::combine_partials_launch(gathered, world, partials, (hipStream_t)stream);
+    if (n_slots < 0) return fail(NNGP_EINVAL, "n_slots=%lld < 0", (long long)n_slots);
+    hipError_t e = nngp::combine_partials_launch(gathered, world, n_slots, partials, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "combine_partials launch");
     return NNGP_OK;
+}
+
+int nngp_combine_partials(const double* gathered, int32_t world, double* partials, void* stream) {
+    return nngp_combine_partials_batch(gathered, world, 1, partials, stream);
 }
 
 size_t nngp_reverse_workspace_bytes(int64_t n, int32_t m) {

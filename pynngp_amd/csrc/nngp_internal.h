@@ -103,7 +103,7 @@ int64_t bf_record_count(int64_t n_rows, int algo, int m);
 hipError_t bf_finalize_launch(const double* bpart, int64_t n_records, double* partials, hipStream_t s);
 hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, hipStream_t s);
 hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s);
-hipError_t combine_partials_launch(const double* gathered, int world, double* out, hipStream_t s);
+hipError_t combine_partials_launch(const double* gathered, int world, int64_t n_slots, double* out, hipStream_t s);
 bool bf_wave_launch(const BfArgs& a, const CovParams& P, int64_t n_blocks, hipStream_t s);
 bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t s);
 bool bf_group_supported(int m, int lanes);

@@ -206,15 +206,20 @@ std::tuple<at::Tensor, at::Tensor> row_order(const at::Tensor& coords, int64_t i
     return {order, srt};
 }
 
+// gathered (world, 4) -> out (4,), or a batch of independent sweeps: gathered (world, n_slots, 4) -> out (n_slots, 4)
 void combine_partials_out(const at::Tensor& gathered, const at::Tensor& out) {
-    TORCH_CHECK(gathered.is_cuda() && gathered.scalar_type() == at::kDouble && gathered.dim() == 2 &&
-                    gathered.size(1) == 4 && gathered.is_contiguous(),
-                "gathered must be a contiguous float64 (world, 4) GPU tensor");
+    TORCH_CHECK(gathered.is_cuda() && gathered.scalar_type() == at::kDouble &&
+                    (gathered.dim() == 2 || gathered.dim() == 3) && gathered.size(-1) == 4 && gathered.is_contiguous(),
+                "gathered must be a contiguous float64 (world, 4) or (world, n_slots, 4) GPU tensor");
     const at::OptionalDeviceGuard guard(gathered.device());
-    check_f64(out, {4}, gathered, "out");
-    check_rc(nngp_combine_partials(gathered.data_ptr<double>(), (int32_t)gathered.size(0), out.data_ptr<double>(),
-                                   stream(gathered)),
-             "nngp_combine_partials");
+    const int64_t slots = gathered.dim() == 3 ? gathered.size(1) : 1;
+    if (gathered.dim() == 3)
+        check_f64(out, {slots, 4}, gathered, "out");
+    else
+        check_f64(out, {4}, gathered, "out");
+    check_rc(nngp_combine_partials_batch(gathered.data_ptr<double>(), (int32_t)gathered.size(0), slots,
+                                         out.data_ptr<double>(), stream(gathered)),
+             "nngp_combine_partials_batch");
 }
 
 }  // namespace

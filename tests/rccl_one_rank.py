@@ -37,6 +37,17 @@ def main():
     torch.cuda.synchronize()
     for k in range(len(covs)):
         assert torch.equal(res[k], local[k]), (k, res[k], local[k])
+    # one all-gather per sweep, and 3 + 1 sweeps per all-gather (a partial last batch): the same bits
+    for batch, n_coll in ((1, 4), (3, 2)):
+        pipe = PipelinedCombine(sw, len(covs), batch=batch)
+        for k, cv in enumerate(covs):
+            sw.local_partials(cv, v, False, out=pipe.local[k])
+            pipe.exchange(k)
+        res = pipe.finish()
+        torch.cuda.synchronize()
+        assert pipe.n_collectives == n_coll
+        for k in range(len(covs)):
+            assert torch.equal(res[k], local[k]), (batch, k, res[k], local[k])
     # the blocking exchange too
     for k, cv in enumerate(covs):
         g = combine_partials(sw.local_partials(cv, v).clone(), 1, force=True)

@@ -90,6 +90,16 @@ def _worker_storage(rank, world, port, n, m, out):
         pipe.exchange(k)
     res = pipe.finish()
     assert torch.equal(res[0], res[2]) and not torch.equal(res[0], res[1])
+    # batched exchanges (2 sweeps per all-gather, a partial last batch): the same rows
+    covs5 = [cov, cov.replace(phi=4.0), cov, cov.replace(tau2=0.2), cov.replace(phi=4.0)]
+    pipe2 = PipelinedCombine(sweep, 5, batch=2)
+    for k, c in enumerate(covs5):
+        sweep.local_partials(c, values, out=pipe2.local[k])
+        pipe2.exchange(k)
+    res2 = pipe2.finish()
+    assert pipe2.n_collectives == 3
+    for k, c in enumerate(covs5):
+        assert torch.equal(res2[k], sweep.partials(c, values)), k
     out[rank] = (sweep.loglik(cov, values), sweep.rows_input.tolist(), res[0].tolist())
     dist.destroy_process_group()
 
