@@ -218,8 +218,25 @@ constexpr int kGroup = NNGP_GIBBS_GROUP;
 //            rows near j's parents in the storage order);
 //   rows:    kRowLanes lanes per location fold P_i over its contiguous reverse range
 //            (fixed order: lane-strided partial sums + a fixed xor-butterfly), 1 / Ft_i.
-// (The first version, kGroup lanes per location doing both, took 267 us at N = 1e6, m = 15:
-// half the lanes idle and every lane's chain rev_j -> B -> divide -> store serial.)
+// 0.183 ms per prepared phi at N = 1e6, m = 15 (tools/bench_prepare.py).  Measured and rejected
+// (round 3, profiles/r03k): one fused pass (NNGP_PREP_FUSED: L lanes per location, U entries per lane
+// in flight, P_i folded without re-reading Brev / Grev) at L x U = 4 x 4 / 8 x 2 / 16 x 1 / 16 x 2:
+// 0.216 / 0.181 / 0.196 / 0.233 ms; the first version, kGroup lanes per location with one entry
+// each in flight, took 267 us.
+// NNGP_PREP_FUSED 0: the two streaming passes; 1: one pass, NNGP_PREP_LANES lanes per location with
+// NNGP_PREP_UNROLL entries each in flight
+#ifndef NNGP_PREP_FUSED
+#define NNGP_PREP_FUSED 0
+#endif
+#ifndef NNGP_PREP_LANES
+#define NNGP_PREP_LANES 4
+#endif
+#ifndef NNGP_PREP_UNROLL
+#define NNGP_PREP_UNROLL 4
+#endif
+constexpr int kRowLanes = NNGP_PREP_FUSED ? NNGP_PREP_LANES : 4;
+constexpr int kPrepUnroll = NNGP_PREP_UNROLL;
+
 __global__ __launch_bounds__(256) void gibbs_prepare_entries(const double* __restrict__ B,
                                                              const double* __restrict__ Ft,
                                                              const int32_t* __restrict__ rev_j,
@@ -234,8 +251,6 @@ __global__ __launch_bounds__(256) void gibbs_prepare_entries(const double* __res
     Brev[e] = b;
     Grev[e] = b / Ft[j];
 }
-
-constexpr int kRowLanes = 4;
 
 __global__ __launch_bounds__(256) void gibbs_prepare_rows(const double* __restrict__ Ft,
                                                           const int32_t* __restrict__ off, int64_t n,
@@ -257,6 +272,56 @@ __global__ __launch_bounds__(256) void gibbs_prepare_rows(const double* __restri
         invF[i] = 1.0 / Ft[i];
     }
 }
+
+#if NNGP_PREP_FUSED
+__global__ __launch_bounds__(256) void gibbs_prepare_fused(const double* __restrict__ B, const double* __restrict__ Ft,
+                                                           const int32_t* __restrict__ rev_j,
+                                                           const int32_t* __restrict__ rev_k,
+                                                           const int32_t* __restrict__ off, int64_t n, int m,
+                                                           double* __restrict__ Brev, double* __restrict__ Grev,
+                                                           double* __restrict__ P, double* __restrict__ invF) {
+    const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const int64_t i = t / kRowLanes;
+    const int l = (int)(t % kRowLanes);
+    const bool live = i < n;
+    const int64_t ic = live ? i : n - 1;
+    const int32_t e0 = off[ic], e1 = live ? off[ic + 1] : e0;
+    double acc = 0.0;
+    double bb[kPrepUnroll], gg[kPrepUnroll];
+#pragma unroll
+    for (int u = 0; u < kPrepUnroll; ++u) {  // the first kPrepUnroll entries of this lane, loads in flight together
+        const int32_t e = e0 + l + u * kRowLanes;
+        const bool has = e < e1;
+        const int64_t j = has ? (int64_t)rev_j[e] : 0;
+        const double b = has ? B[j * m + rev_k[e]] : 0.0;
+        bb[u] = b;
+        gg[u] = has ? b / Ft[j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPrepUnroll; ++u) {
+        const int32_t e = e0 + l + u * kRowLanes;
+        if (e < e1) {
+            Brev[e] = bb[u];
+            Grev[e] = gg[u];
+        }
+        acc = fma(bb[u], gg[u], acc);
+    }
+    for (int32_t e = e0 + l + kPrepUnroll * kRowLanes; e < e1; e += kRowLanes) {
+        const int64_t j = rev_j[e];
+        const double b = B[j * m + rev_k[e]];
+        const double g = b / Ft[j];
+        Brev[e] = b;
+        Grev[e] = g;
+        acc = fma(b, g, acc);
+    }
+#pragma unroll
+    for (int o = kRowLanes / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (live && l == 0) {
+        P[i] = acc;
+        invF[i] = 1.0 / Ft[i];
+    }
+}
+#endif
 
 struct GibbsPrep {
     double *Brev, *Grev, *P, *invF;
@@ -285,6 +350,11 @@ hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t
     if (n == 0) return hipSuccess;
     const GibbsPrep g = prep_layout(prep, n, m);
     (void)order;  // both passes stream the reverse lists in storage order; no visiting order needed
+#if NNGP_PREP_FUSED
+    hipLaunchKernelGGL(gibbs_prepare_fused, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
+                       rev_k, off, n, m, g.Brev, g.Grev, g.P, g.invF);
+    return hipGetLastError();
+#endif
     const int64_t ne = n * (int64_t)m;
     if (ne > 0)
         hipLaunchKernelGGL(gibbs_prepare_entries, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
