@@ -174,6 +174,35 @@ int nngp_bf_cross(const double *ref, int64_t n_ref, int32_t dim, const double *q
                   int32_t algo, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * A covariance of the caller's own (the reference's `cov` is an arbitrary plug-in,
+ * pyNNGP/nngp.py:6,12; SURVEY.md 8(b) asks for callables): any isotropic function of
+ * distance, evaluated by the caller on the GPU, drives the same fused sweep.
+ * nngp_joint_dist: for nbr row t (location i = i0 + (order ? order[t] : t); joint rows
+ *   a = 0..m-1 the neighbour slots, row m the location, from qcoords) the packed lower
+ *   triangle of the joint block's distances, entry (a, b), b <= a, at
+ *   dist[(a (a + 1) / 2 + b) * n_rows + t] -- nngp_joint_entries(m) = (m+1)(m+2)/2 entries
+ *   per row, entry-major; 0 on the diagonal, +inf where a slot holds no point.  Distances are
+ *   sqrt of the unfused sum of squared coordinate differences.
+ * nngp_bf_sweep_blocks: the fused B/F + log-lik sweep (outputs, partials, order and values
+ *   as nngp_bf_sweep / nngp_bf_cross: values (n_points,) of the neighbours, qvalues (n_locs,)
+ *   of the locations, may be NULL) with the joint blocks' covariances read from `cov` in that
+ *   layout -- cov[e] = C(dist[e]) plus the nugget on the diagonal entries; entries of slots
+ *   without a point are ignored (decoupled exactly).  1 <= m <= 24; workspace
+ *   nngp_bf_sweep_blocks_workspace_bytes(n_rows), 256-B aligned; partials required.
+ * ------------------------------------------------------------------------- */
+/* out[k] = u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) for n arguments u >= 0 (the Matern correlation
+ * of NNGP_COV_MATERN, elementwise; 0 < nu <= 50): a building block for such covariances. */
+int nngp_matern_eval(const double *u, int64_t n, double nu, double *out, void *stream);
+int64_t nngp_joint_entries(int32_t m);
+int nngp_joint_dist(const double *coords, int64_t n_points, int32_t dim, const double *qcoords, int64_t n_locs,
+                    const int32_t *nbr, const int32_t *order, int64_t n_rows, int32_t m, int64_t i0, double *dist,
+                    void *stream);
+size_t nngp_bf_sweep_blocks_workspace_bytes(int64_t n_rows);
+int nngp_bf_sweep_blocks(const double *cov, const int32_t *nbr, const int32_t *order, int64_t n_points, int64_t n_rows,
+                         int32_t m, int64_t i0, int64_t n_locs, const double *values, const double *qvalues, double *B,
+                         double *F, double *R, double *partials, void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Visiting order for nngp_bf_sweep (a speed option; no reference counterpart:
  * the reference visits locations in input order, nngp.py:51).
  * order[t] = the t-th local row (0 .. n_rows-1) of locations i0 .. i0+n_rows-1

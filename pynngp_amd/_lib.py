@@ -34,6 +34,11 @@ SYMBOLS = (
     "nngp_row_order",
     "nngp_combine_partials",
     "nngp_combine_partials_batch",
+    "nngp_matern_eval",
+    "nngp_joint_entries",
+    "nngp_joint_dist",
+    "nngp_bf_sweep_blocks_workspace_bytes",
+    "nngp_bf_sweep_blocks",
     "nngp_reverse_workspace_bytes",
     "nngp_reverse_neighbors",
     "nngp_color_moral_graph",
@@ -94,6 +99,16 @@ def load() -> ctypes.CDLL:
     lib.nngp_row_order.restype = ctypes.c_int
     lib.nngp_combine_partials.argtypes = [P, I32, P, P]
     lib.nngp_combine_partials_batch.argtypes = [P, I32, I64, P, P]
+    lib.nngp_matern_eval.argtypes = [P, I64, D, P, P]
+    lib.nngp_matern_eval.restype = ctypes.c_int
+    lib.nngp_joint_entries.argtypes = [I32]
+    lib.nngp_joint_entries.restype = I64
+    lib.nngp_joint_dist.argtypes = [P, I64, I32, P, I64, P, P, I64, I32, I64, P, P]
+    lib.nngp_joint_dist.restype = ctypes.c_int
+    lib.nngp_bf_sweep_blocks_workspace_bytes.argtypes = [I64]
+    lib.nngp_bf_sweep_blocks_workspace_bytes.restype = SZ
+    lib.nngp_bf_sweep_blocks.argtypes = [P, P, P, I64, I64, I32, I64, I64, P, P, P, P, P, P, P, SZ, P]
+    lib.nngp_bf_sweep_blocks.restype = ctypes.c_int
     lib.nngp_combine_partials_batch.restype = ctypes.c_int
     lib.nngp_bf_finalize.argtypes = [P, ctypes.c_size_t, I64, I32, I32, I32, I32, P, P]
     lib.nngp_bf_finalize.restype = ctypes.c_int
@@ -404,6 +419,91 @@ def bf_cross(ref: torch.Tensor, query: torch.Tensor, nbr: torch.Tensor, kind: st
                              int(q0), KIND_CODES[kind], float(sigma2), float(phi), float(tau2), nu, _ptr(ref_values),
                              _ptr(query_values), _ptr(B), _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace),
                              workspace.numel(), a, _stream(dev)), "nngp_bf_cross")
+    return B, F, partials
+
+
+def joint_dist(coords: torch.Tensor, nbr: torch.Tensor, i0: int = 0, qcoords: Optional[torch.Tensor] = None,
+               order: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Distances of every joint block (nngp_joint_dist): float64 ((m+1)(m+2)/2, rows), entry
+    (a, b), b <= a, of nbr row t at ``[a (a+1)/2 + b, t]`` (row m of a block is the location
+    ``i0 + (order[t] if order else t)``, taken from ``qcoords``, default ``coords``); 0 on the
+    diagonal, +inf for slots without a point.  Map it through a covariance function and pass
+    the result to :func:`bf_sweep_blocks`."""
+    coords = _as_coords(coords)
+    qcoords = coords if qcoords is None else _as_coords(qcoords)
+    d = _same_dim(coords, qcoords)
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
+    nbr = nbr.contiguous()
+    dev = _require_gpu(coords, qcoords, nbr, order)
+    rows, m = nbr.shape
+    if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
+        raise ValueError("order must be int32 (rows,)")
+    lib = load()
+    ne = int(lib.nngp_joint_entries(m))
+    _check_out(out, "out", (ne, rows), dev)
+    out = torch.empty((ne, rows), dtype=torch.float64, device=dev) if out is None else out
+    _check(lib.nngp_joint_dist(_ptr(coords), coords.shape[0], d, _ptr(qcoords), qcoords.shape[0], _ptr(nbr),
+                               _ptr(order), rows, m, int(i0), _ptr(out), _stream(dev)), "nngp_joint_dist")
+    return out
+
+
+def matern(u: torch.Tensor, nu: float) -> torch.Tensor:
+    """u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) elementwise on the GPU (nngp_matern_eval; u >= 0, +inf -> 0),
+    e.g. ``IsotropicCovariance(lambda d: s2 * matern(phi * d, nu), tau2)``."""
+    if u.dtype != torch.float64:
+        raise ValueError("u must be float64")
+    dev = _require_gpu(u)
+    _check_kind("matern", nu)
+    u = u.contiguous()
+    out = torch.empty_like(u)
+    _check(load().nngp_matern_eval(_ptr(u), u.numel(), float(nu), _ptr(out), _stream(dev)), "nngp_matern_eval")
+    return out
+
+
+def joint_diagonal(m: int) -> torch.Tensor:
+    """Row indices a (a+1)/2 + a of the diagonal entries of a joint block (for adding a nugget)."""
+    a = torch.arange(m + 1)
+    return a * (a + 1) // 2 + a
+
+
+def bf_sweep_blocks(cov: torch.Tensor, nbr: torch.Tensor, n_points: int, i0: int = 0,
+                    values: Optional[torch.Tensor] = None, qvalues: Optional[torch.Tensor] = None,
+                    want_bf: bool = True, order: Optional[torch.Tensor] = None, R: Optional[torch.Tensor] = None,
+                    workspace: Optional[torch.Tensor] = None, n_locs: Optional[int] = None
+                    ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
+    """The fused B/F + log-lik sweep with the joint blocks' covariances given (nngp_bf_sweep_blocks):
+    ``cov`` float64 ((m+1)(m+2)/2, rows) in :func:`joint_dist`'s layout (the covariance function
+    of the distances, the nugget on the diagonal entries).  ``values`` (n_points,) at the
+    neighbours and ``qvalues`` (n_locs,) at the locations (pass ``values`` again for the S = T
+    sweep; None: 0, so R = -B v_N, minus the kriging mean).
+    Returns ``(B, F, partials)`` as :func:`bf_sweep`.  1 <= m <= 24."""
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
+    nbr = nbr.contiguous()
+    rows, m = nbr.shape
+    lib = load()
+    ne = int(lib.nngp_joint_entries(m))
+    if cov.dtype != torch.float64 or tuple(cov.shape) != (ne, rows):
+        raise ValueError(f"cov must be float64 ({ne}, {rows}) (joint_dist's layout), got {cov.dtype} {tuple(cov.shape)}")
+    cov = cov.contiguous()
+    for name, v in (("values", values), ("qvalues", qvalues)):
+        if v is not None and (v.dtype != torch.float64 or v.dim() != 1):
+            raise ValueError(f"{name} must be float64 1-D")
+    values = None if values is None else values.contiguous()
+    qvalues = None if qvalues is None else qvalues.contiguous()
+    dev = _require_gpu(cov, nbr, values, qvalues, order, R)
+    n_locs = int(n_points if n_locs is None else n_locs)
+    B = torch.empty((rows, m), dtype=torch.float64, device=dev) if want_bf else None
+    F = torch.empty((rows,), dtype=torch.float64, device=dev) if want_bf else None
+    _check_out(R, "R", (rows,), dev)
+    partials = torch.empty(4, dtype=torch.float64, device=dev)
+    need = lib.nngp_bf_sweep_blocks_workspace_bytes(rows)
+    if workspace is None or workspace.numel() < need:
+        workspace = _workspace(need, dev)
+    _check(lib.nngp_bf_sweep_blocks(_ptr(cov), _ptr(nbr), _ptr(order), int(n_points), rows, m, int(i0), n_locs,
+                                    _ptr(values), _ptr(qvalues), _ptr(B), _ptr(F), _ptr(R), _ptr(partials),
+                                    _ptr(workspace), workspace.numel(), _stream(dev)), "nngp_bf_sweep_blocks")
     return B, F, partials
 
 

@@ -123,6 +123,9 @@ constexpr bool pairb_left(int m) { return ((unsigned long long)(NNGP_PAIRB_LEFT_
 constexpr bool pairb_left3(int m) {
     return pairb_left(m) && (((unsigned long long)(NNGP_PAIRB_LEFT_3W_MASK) >> m) & 1ull);
 }
+// the same for a kernel of covariance kind `kind` (the covariance-blocks kernels are right-looking)
+constexpr bool pairb_lk(int m, int kind) { return pairb_left(m) && kind != NNGP_KIND_BLOCKS; }
+constexpr bool pairb_left3_k(int m, int kind) { return pairb_left3(m) && kind != NNGP_KIND_BLOCKS; }
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
 #define NNGP_PHASE(name)                        \
@@ -174,11 +177,12 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 #ifndef NNGP_PAIRB_THREE_WAVES_MAX
 #define NNGP_PAIRB_THREE_WAVES_MAX 13
 #endif
+// (KIND == NNGP_KIND_BLOCKS: covariances read from memory, always right-looking -- pairb_lk)
 #define NNGP_PAIRB_ATTR                                                                              \
     __attribute__((amdgpu_waves_per_eu(                                                                 \
-        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3(M)) ? 3                                         \
-         : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_left(M) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
-        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3(M)) ? 3 : 2))))
+        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3                                 \
+         : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_lk(M, KIND) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
+        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3 : 2))))
 
 // Threads per block (one tile of kPairbThreads / 2 locations per block).  256 measured fastest:
 // 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
@@ -241,6 +245,12 @@ __device__ __forceinline__ double pr_rcp(double x) {
     return fma(y, fma(e, e, e), y);
 }
 
+// KIND == NNGP_KIND_BLOCKS (nngp_bf_sweep_blocks): the joint block's covariances are read from
+// cblk instead of evaluated -- a user covariance (any isotropic function of distance, evaluated on the
+// GPU by the caller over nngp_joint_dist's distances): entry (a, b), b <= a <= M, of nbr row t at
+// cblk[(a (a + 1) / 2 + b) * n_rows + t] (entry-major: one load instruction reads 32 consecutive
+// rows).  Slots with an invalid neighbour index are decoupled exactly (0 off the diagonal, 1 on it)
+// whatever the caller's values there; sigma2 = 1 (the blocks are the covariances themselves).
 template <int M, int KIND, int D>
 __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const double* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
@@ -248,19 +258,21 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 const double* __restrict__ values, const double* __restrict__ qcoords,
                                                 const double* __restrict__ qvalues, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim) {
+                                                double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim,
+                                                const double* __restrict__ cblk) {
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
+    constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
     constexpr int DA = point_arity<D>();  // coordinates held per point
     const int ds = D == 0 ? dim : D;      // row stride of coords / qcoords
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
-    constexpr bool LEFT = pairb_left(M);
+    constexpr bool LEFT = pairb_lk(M, KIND);
     constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
     constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
                           (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
-    constexpr int KL0 = pairb_left3(M)                         ? NNGP_PAIRB_LEFT_LDS_ROWS_3W
+    constexpr int KL0 = pairb_left3_k(M, KIND)                 ? NNGP_PAIRB_LEFT_LDS_ROWS_3W
                         : M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W
                                                               : NNGP_PAIRB_LEFT_LDS_ROWS;
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
@@ -273,9 +285,11 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int kTabPer = kPairbThreads >= NNGP_EXP_TAB_N ? 1 : NNGP_EXP_TAB_N / kPairbThreads;
     static_assert(kPairbThreads >= NNGP_EXP_TAB_N || kTabPer * kPairbThreads == NNGP_EXP_TAB_N, "table fill");
     double etab_entry[kTabPer];
+    if constexpr (!CM) {
 #pragma unroll
-    for (int e = 0; e < kTabPer; ++e)
-        etab_entry[e] = nngp_exp_table_entry_unit(((int)threadIdx.x + e * kPairbThreads) & (NNGP_EXP_TAB_N - 1));
+        for (int e = 0; e < kTabPer; ++e)
+            etab_entry[e] = nngp_exp_table_entry_unit(((int)threadIdx.x + e * kPairbThreads) & (NNGP_EXP_TAB_N - 1));
+    }
 
     __shared__ double sh[1][kPairbWaves][5];
     const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -320,8 +334,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const double* pc = self ? qcoords + i * ds : (in_range ? coords + (int64_t)j * ds : far_point<DA>(a));
             const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                     : ((values != nullptr && in_range) ? values + j : kZeroValue);
-            if constexpr (D == 0) load_point_rt(pc, dim, o[s]);
-            else load_point<D>(pc, o[s]);
+            if constexpr (CM) {
+            } else if constexpr (D == 0) {
+                load_point_rt(pc, dim, o[s]);
+            } else {
+                load_point<D>(pc, o[s]);
+            }
             if constexpr (!LEFT) z[s] = *pv;  // (the left-looking kernel gathers the values late)
         }
         if constexpr (ZLDS) {
@@ -332,19 +350,58 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
+        if constexpr (!CM) {
 #pragma unroll
-        for (int e = 0; e < kTabPer; ++e)
-            if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
-                etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
-        __syncthreads();
+            for (int e = 0; e < kTabPer; ++e)
+                if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
+                    etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
+            __syncthreads();
+        }
 
         double R[NP][NP][2];
         bool bad = false;
         double Fu, res;
+        if constexpr (CM) {
+            // ---- covariances from the caller's blocks, own-parity-first order.  vm: bit a set when
+            // joint row a holds a point (a valid neighbour slot, or a = M); this lane's rows, then the
+            // partner's by one swap
+            uint32_t vm = 0;
+#pragma unroll
+            for (int s = 0; s < NP; ++s) {
+                const int a = 2 * s + q;
+                const bool ok = a == M || (a < M && (uint32_t)jn[s] < n32);
+                vm |= ok ? (1u << a) : 0u;
+            }
+            vm |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vm, 0xB1, 0xf, 0xf, true);
+            const double* cb = cblk + rl;
+            // lane 0 reads entry (a0, b0), lane 1 (a1, b1) -- compile-time after unrolling, so each load
+            // costs two selects and an address multiply-add; 0 unless both rows hold points
+            auto ldc2 = [&](int a0, int b0, int a1, int b1) -> double {
+                const int e0 = (a0 * (a0 + 1) >> 1) + b0, e1 = (a1 * (a1 + 1) >> 1) + b1;
+                const uint32_t need = q1 ? ((1u << a1) | (1u << b1)) : ((1u << a0) | (1u << b0));
+                const bool ok = (vm & need) == need;
+                const int64_t e = ok ? (q1 ? e1 : e0) : 0;  // an in-range address either way (branch-free)
+                const double v = cb[e * n_rows];
+                return ok ? v : 0.0;
+            };
+#pragma unroll
+            for (int s = 0; s < NP; ++s) {
+                const int a0 = 2 * s, a1 = 2 * s + 1;
+#pragma unroll
+                for (int t = 0; t < s; ++t) {
+                    R[s][t][0] = ldc2(a0, 2 * t, a1, 2 * t + 1);      // (a, 2t + q)
+                    R[s][t][1] = ldc2(a0, 2 * t + 1, a1, 2 * t);      // (a, 2t + 1 - q)
+                }
+                const double dg = ldc2(a0, a0, a1, a1);
+                R[s][s][0] = ((vm >> (2 * s + q)) & 1u) ? dg : 1.0;   // a decoupled row: identity
+                const double w = ldc2(a0, a0, a1, a0);               // (2s+1, 2s), read from lane 1 only
+                R[s][s][1] = q1 ? w : 0.0;
+            }
+        }
         if constexpr (!LEFT) {
         NNGP_PHASE(covariances);
         // ---- unit-variance covariances in own-parity-first order
-        {
+        if constexpr (!CM) {
             double p[NP][DA];
 #pragma unroll
             for (int t = 0; t < NP; ++t)
@@ -720,8 +777,9 @@ inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
 template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), 0, s, a.coords,
-                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, a.sigma2, a.values, a.qcoords, a.qvalues, a.B,
-                       a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), a.dim);
+                       a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
+                       a.qcoords, a.qvalues, a.B, a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), a.dim,
+                       a.cblk);
 }
 
 // m = 25..32: one instantiation per m for every kind and dimension (runtime kind NNGP_KIND_GENERIC,
@@ -731,6 +789,14 @@ template <int M>
 static bool launch_pairb_generic_if(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     if (a.m != M) return false;
     launch_pairb_mkd<M, NNGP_KIND_GENERIC, 0>(a, Pc, s);
+    return true;
+}
+
+// covariance blocks from memory (nngp_bf_sweep_blocks; instantiated by bf_pairb_inst_blocks_*.hip)
+template <int M>
+static bool launch_pairb_blocks_if(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
+    if (a.m != M) return false;
+    launch_pairb_mkd<M, NNGP_KIND_BLOCKS, 2>(a, Pc, s);
     return true;
 }
 

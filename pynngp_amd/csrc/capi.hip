@@ -145,6 +145,69 @@ int nngp_bf_cross(const double* ref, int64_t n_ref, int32_t dim, const double* q
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
 }
 
+int64_t nngp_joint_entries(int32_t m) { return m < 0 ? 0 : (int64_t)(m + 1) * (m + 2) / 2; }
+
+int nngp_joint_dist(const double* coords, int64_t n_points, int32_t dim, const double* qcoords, int64_t n_locs,
+                    const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t i0, double* dist,
+                    void* stream) {
+    if (coords == nullptr || qcoords == nullptr || dist == nullptr || (m > 0 && n_rows > 0 && nbr == nullptr))
+        return fail(NNGP_EINVAL, "coords, qcoords, dist (and nbr for m > 0) must be non-null");
+    if (dim < 1 || dim > NNGP_MAX_DIM) return fail(NNGP_EUNSUP, "dim=%d outside [1, %d]", dim, NNGP_MAX_DIM);
+    if (m < 0 || m > NNGP_MAX_M) return fail(NNGP_EUNSUP, "m=%d outside [0, %d]", m, NNGP_MAX_M);
+    if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
+        return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
+                    (long long)n_locs);
+    hipError_t e = nngp::joint_dist_launch(coords, n_points, dim, qcoords, nbr, order, n_rows, m, i0, dist,
+                                           (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "joint_dist launch");
+    return NNGP_OK;
+}
+
+int nngp_matern_eval(const double* u, int64_t n, double nu, double* out, void* stream) {
+    if (n < 0 || (n > 0 && (u == nullptr || out == nullptr))) return fail(NNGP_EINVAL, "bad n or null pointer");
+    if (!(nu > 0.0 && nu <= NNGP_MATERN_NU_MAX))
+        return fail(NNGP_EINVAL, "the matern correlation needs 0 < nu <= %g (nu=%g)", NNGP_MATERN_NU_MAX, nu);
+    hipError_t e = nngp::matern_eval_launch(u, n, nu, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "matern_eval launch");
+    return NNGP_OK;
+}
+
+size_t nngp_bf_sweep_blocks_workspace_bytes(int64_t n_rows) {
+    return n_rows < 0 ? 0 : nngp::bf_pairb_workspace_bytes(n_rows);
+}
+
+int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* order, int64_t n_points, int64_t n_rows,
+                         int32_t m, int64_t i0, int64_t n_locs, const double* values, const double* qvalues, double* B,
+                         double* F, double* R, double* partials, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    if (cov == nullptr || workspace == nullptr || partials == nullptr || (n_rows > 0 && nbr == nullptr))
+        return fail(NNGP_EINVAL, "cov, nbr, partials and workspace must be non-null");
+    if (!nngp::bf_pairb_blocks_supported(m))
+        return fail(NNGP_EUNSUP, "covariance-block sweeps need 1 <= m <= 24 (m=%d)", m);
+    if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
+        return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
+                    (long long)n_locs);
+    if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
+    if (F != nullptr && B == nullptr) return fail(NNGP_EINVAL, "F given without B");
+    if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    if (workspace_bytes < nngp_bf_sweep_blocks_workspace_bytes(n_rows))
+        return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes,
+                    nngp_bf_sweep_blocks_workspace_bytes(n_rows));
+    hipStream_t s = (hipStream_t)stream;
+    if (n_rows == 0) {
+        hipError_t e = nngp::bf_finalize_launch((const double*)workspace, 0, partials, s);
+        return e == hipSuccess ? NNGP_OK : hip_fail(e, "bf_finalize launch");
+    }
+    nngp::BfArgs args{nullptr, n_points, nbr, n_rows, i0, m, NNGP_KIND_BLOCKS, 2, 1.0, 1.0, 0.0, 0.0, order, values,
+                      nullptr, qvalues, B, F, R, partials, (double*)workspace, cov};
+    if (!nngp::bf_pairb_blocks_launch(args, s)) return fail(NNGP_EUNSUP, "no covariance-block kernel for m=%d", m);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = nngp::bf_finalize_pairb_launch(workspace, n_rows, partials, s);
+    if (e != hipSuccess) return hip_fail(e, "bf_sweep_blocks launch");
+    return NNGP_OK;
+}
+
 int nngp_bf_finalize(const void* workspace, size_t workspace_bytes, int64_t n_rows, int32_t m, int32_t kind,
                      int32_t dim, int32_t algo, double* partials, void* stream) {
     if (workspace == nullptr || partials == nullptr) return fail(NNGP_EINVAL, "workspace and partials must be non-null");

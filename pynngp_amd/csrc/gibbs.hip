@@ -235,7 +235,7 @@ constexpr int kGroup = NNGP_GIBBS_GROUP;
 #define NNGP_PREP_UNROLL 4
 #endif
 constexpr int kRowLanes = NNGP_PREP_FUSED ? NNGP_PREP_LANES : 4;
-constexpr int kPrepUnroll = NNGP_PREP_UNROLL;
+[[maybe_unused]] constexpr int kPrepUnroll = NNGP_PREP_UNROLL;
 
 __global__ __launch_bounds__(256) void gibbs_prepare_entries(const double* __restrict__ B,
                                                              const double* __restrict__ Ft,

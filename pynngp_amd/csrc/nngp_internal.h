@@ -97,6 +97,7 @@ struct BfArgs {
     double* R;                 // (n_rows,) residuals v_i - B_i v_N(i), or null
     double* partials;          // [4]
     double* bpart;             // 4 doubles per block: sum log F, sum r^2/F, first bad-pivot row, first bad-index row
+    const double* cblk = nullptr;  // NNGP_KIND_BLOCKS: the joint blocks' covariances (bf_pairb.h), entry-major
 };
 
 int64_t bf_record_count(int64_t n_rows, int algo, int m);
@@ -109,6 +110,12 @@ bool bf_group_launch(const BfArgs& a, const CovParams& P, int lanes, hipStream_t
 bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
+bool bf_pairb_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS (bf_pairb.h)
+bool bf_pairb_blocks_supported(int m);
+hipError_t matern_eval_launch(const double* u, int64_t n, double nu, double* out, hipStream_t s);
+hipError_t joint_dist_launch(const double* coords, int64_t n_points, int dim, const double* qcoords,
+                             const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int64_t i0, double* dist,
+                             hipStream_t s);
 // number of 256-thread blocks (= partial records) each kernel launches for n_rows
 int64_t bf_group_blocks(int64_t n_rows, int lanes);
 int64_t bf_lane_blocks(int64_t n_rows);

@@ -73,6 +73,8 @@ static __device__ const double kExp2Tab[256] = NNGP_EXP2_TAB;
 // p(u) e, p(u) = 1 + c1 u + c2 u^2 + c3 u^3 with u = min(phi d, umax), e = 2^(nphi256 g / 256) with
 // g = d (g = d^2 for the gaussian kind; nphi256 = 0, i.e. e = 1, for the spherical kind).
 #define NNGP_KIND_GENERIC 7
+// Covariance blocks from memory (nngp_bf_sweep_blocks: a caller-evaluated covariance; bf_pairb.h)
+#define NNGP_KIND_BLOCKS 8
 
 // Covariance parameters, built once on the host (nngp_cov_params) and passed by value.
 struct CovParams {

@@ -105,7 +105,85 @@ class Covariance:
         return e
 
 
-CovLike = Union[Covariance, Callable, None]
+@dataclasses.dataclass(frozen=True)
+class IsotropicCovariance:
+    """A covariance of the caller's own -- the reference's `cov` plug-in (nngp.py:6,12) as any
+    isotropic function of distance -- driving the fused GPU sweep: ``fn`` maps a float64 torch
+    tensor of distances (any shape, on the GPU) to covariances elementwise (without the nugget;
+    C(0) = ``fn(0)`` is the marginal variance), ``tau2`` is the nugget.  The sweep evaluates
+    ``fn`` once over every joint block's distances (``_lib.joint_dist``, +inf for slots without
+    a point, whose entries the kernel then ignores) and factorises the blocks in the
+    ``bf_pairb`` kernel reading them from memory (nngp_bf_sweep_blocks, 1 <= m <= 24).
+    Example: ``IsotropicCovariance(lambda d: 2.0 * torch.exp(-(d / 0.1) ** 1.5), tau2=0.1)``
+    (a powered exponential).  Called as ``cov(a, b)`` on coordinate rows it returns the
+    cross-covariance matrix, like a reference plug-in."""
+
+    fn: Callable
+    tau2: float = 0.0
+    name: str = "custom"
+
+    def __post_init__(self):
+        if not callable(self.fn):
+            raise TypeError("fn must be callable (a torch function of distance)")
+        if not self.tau2 >= 0:
+            raise ValueError("need tau2 >= 0")
+
+    kind = "custom"
+
+    @property
+    def sigma2(self) -> float:
+        """C(0) = fn(0)."""
+        return float(self.fn(torch.zeros(1, dtype=torch.float64)).item())
+
+    def blocks(self, dist: torch.Tensor, m: int) -> torch.Tensor:
+        """Covariance blocks for :func:`_lib.bf_sweep_blocks`: fn over the distances, tau2 on the
+        diagonal entries."""
+        c = self.fn(dist)
+        if not isinstance(c, torch.Tensor) or c.shape != dist.shape:
+            raise ValueError("fn must return a tensor of the distances' shape")
+        c = c.to(torch.float64).contiguous()
+        if self.tau2 > 0:
+            diag = _lib.joint_diagonal(m).to(c.device)
+            c[diag] += self.tau2
+        return c
+
+    def __call__(self, a, b):
+        to_np = not isinstance(a, torch.Tensor)
+        ta = torch.as_tensor(np.asarray(a, dtype=np.float64)) if to_np else a
+        tb = torch.as_tensor(np.asarray(b, dtype=np.float64)) if to_np else b
+        d = ta.shape[-1] if ta.dim() > 1 else tb.shape[-1] if tb.dim() > 1 else 1
+        ta, tb = ta.reshape(-1, d), tb.reshape(-1, d)
+        t = ta[:, None, :] - tb[None, :, :]
+        c = self.fn(torch.sqrt((t * t).sum(-1)))
+        return c.cpu().numpy() if to_np else c
+
+
+CovLike = Union[Covariance, IsotropicCovariance, Callable, None]
+
+
+def _sweep_any(cv, coords, nbr, i0=0, values=None, want_bf=True, algo="auto", order=None, R=None, qcoords=None,
+               qvalues=None):
+    """One fused sweep for either covariance form: a built-in kind (nngp_bf_sweep / nngp_bf_cross)
+    or an :class:`IsotropicCovariance` (joint distances -> fn -> nngp_bf_sweep_blocks).  ``qcoords``
+    given: the cross sweep of those query points against ``coords`` (prediction); ``qvalues``: the
+    values at the locations (S = T sweep: pass ``values``)."""
+    if isinstance(cv, IsotropicCovariance):
+        m = nbr.shape[1]
+        if m == 0:
+            raise ValueError("a custom covariance needs m >= 1")
+        if algo not in ("auto", "pairb"):
+            raise ValueError(f"a custom covariance runs on the covariance-block pairb kernel, not algo {algo!r}")
+        dist = _lib.joint_dist(coords, nbr, i0, qcoords=qcoords, order=order)
+        blocks = cv.blocks(dist, m)
+        del dist
+        nq = (coords if qcoords is None else qcoords).shape[0]
+        return _lib.bf_sweep_blocks(blocks, nbr, coords.shape[0], i0, values=values, qvalues=qvalues, want_bf=want_bf,
+                                    order=order, R=R, n_locs=nq)
+    if qcoords is not None:
+        return _lib.bf_cross(coords, qcoords, nbr, cv.kind, *cv.theta, ref_values=values, query_values=qvalues,
+                             q0=i0, algo=algo, R=R, nu=cv.nu_arg)
+    return _lib.bf_sweep(coords, nbr, i0, cv.kind, *cv.theta, values=values, want_bf=want_bf, algo=algo, order=order,
+                         R=R, nu=cv.nu_arg)
 
 
 def _default_device(device):
@@ -249,16 +327,16 @@ class NNGP:
         if nbr.shape[1] == 0:  # m = 0: the marginal
             return np.zeros(n), np.full(n, cv.sigma2 + cv.tau2)
         R = torch.empty(n, dtype=torch.float64, device=self.device)
-        _, F, p = _lib.bf_cross(self._s_dev, q, nbr, cv.kind, *cv.theta, ref_values=v, algo=algo, R=R, nu=cv.nu_arg)
+        _, F, p = _sweep_any(cv, self._s_dev, nbr, 0, values=v, algo=algo, R=R, qcoords=q)
         _raise_on_bad(p.cpu().numpy())
         return (-R).cpu().numpy(), F.cpu().numpy()
 
     # -- covariance plumbing ---------------------------------------------------
-    def _covariance(self) -> Covariance:
-        if not isinstance(self.cov, Covariance):
+    def _covariance(self):
+        if not isinstance(self.cov, (Covariance, IsotropicCovariance)):
             raise TypeError(
-                "the device B/F sweep fuses the covariance: pass cov=pynngp_amd.Covariance(kind, sigma2, phi, tau2) "
-                f"(got {type(self.cov).__name__})")
+                "the device B/F sweep needs cov=pynngp_amd.Covariance(kind, sigma2, phi, tau2[, nu]) or "
+                f"pynngp_amd.IsotropicCovariance(fn, tau2) (got {type(self.cov).__name__})")
         return self.cov
 
     def _nbr_idx(self, i):
@@ -268,7 +346,7 @@ class NNGP:
     def _call_cov(self, a, b):
         if self.cov is None:
             raise TypeError("cov is None")
-        if isinstance(self.cov, Covariance):
+        if isinstance(self.cov, (Covariance, IsotropicCovariance)):
             return self.cov(a, b)
         return self.cov(a.cpu().numpy(), b.cpu().numpy())
 
@@ -277,7 +355,7 @@ class NNGP:
         """C_{N(s_i)} (nngp.py:78-82), with the nugget on the diagonal for a Covariance."""
         x = self._s_dev[self._nbr_idx(i)]
         c = self._call_cov(x, x)
-        if isinstance(self.cov, Covariance) and self.cov.tau2 > 0:
+        if isinstance(self.cov, (Covariance, IsotropicCovariance)) and self.cov.tau2 > 0:
             c = c + self.cov.tau2 * torch.eye(x.shape[0], dtype=c.dtype, device=c.device)
         return c.cpu().numpy() if isinstance(c, torch.Tensor) else c
 
@@ -290,13 +368,13 @@ class NNGP:
         """C_{s_i, s_i} (nngp.py:92-96), with the nugget for a Covariance."""
         x = self._s_dev[i][None, :]
         c = self._call_cov(x, x)
-        if isinstance(self.cov, Covariance):
+        if isinstance(self.cov, (Covariance, IsotropicCovariance)):
             c = c + self.cov.tau2
         return c.cpu().numpy() if isinstance(c, torch.Tensor) else c
 
     def _row_bf(self, i):
         cv = self._covariance()
-        B, F, p = _lib.bf_sweep(self._s_dev, self.nbr[i: i + 1], int(i), cv.kind, *cv.theta, nu=cv.nu_arg)
+        B, F, p = _sweep_any(cv, self._s_dev, self.nbr[i: i + 1], int(i))
         _raise_on_bad(p.cpu().numpy())
         k = min(int(i), self.m)
         return B[0, :k].cpu().numpy(), float(F[0].item())
@@ -313,8 +391,7 @@ class NNGP:
     def compute_BF(self, algo: str = "auto"):
         """All B (N, m) and F (N,) as device tensors (one fused sweep)."""
         cv = self._covariance()
-        B, F, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, algo=algo, order=self._order,
-                                nu=cv.nu_arg)
+        B, F, p = _sweep_any(cv, self._s_dev, self._nbr_sorted, 0, algo=algo, order=self._order)
         _raise_on_bad(p.cpu().numpy())
         self._B, self._F = B, F
         return B, F
@@ -335,8 +412,8 @@ class NNGP:
                             dtype=torch.float64).to(self.device)
         if v.dim() != 1:
             raise ValueError("loglik needs one value per location (1-D values)")
-        _, _, p = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cv.kind, *cv.theta, values=v, want_bf=False,
-                                algo=algo, order=self._order, nu=cv.nu_arg)
+        _, _, p = _sweep_any(cv, self._s_dev, self._nbr_sorted, 0, values=v, qvalues=v, want_bf=False, algo=algo,
+                             order=self._order)
         ph = p.cpu().numpy()
         _raise_on_bad(ph)
         n = self.nbr.shape[0]
@@ -359,10 +436,9 @@ class NNGP:
         ry = torch.empty(n, dtype=torch.float64, device=self.device)
         r1 = torch.empty_like(ry)
         kw = dict(algo=algo, order=self._order)
-        kw["nu"] = cov.nu_arg
-        _, F, py = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=v, R=ry, **kw)
+        _, F, py = _sweep_any(cov, self._s_dev, self._nbr_sorted, 0, values=v, qvalues=v, R=ry, **kw)
         ones = torch.ones_like(v)
-        _, _, p1 = _lib.bf_sweep(self._s_dev, self._nbr_sorted, 0, cov.kind, *cov.theta, values=ones, R=r1, **kw)
+        _, _, p1 = _sweep_any(cov, self._s_dev, self._nbr_sorted, 0, values=ones, qvalues=ones, R=r1, **kw)
         s_y1 = torch.sum(ry * r1 / F)
         sums = torch.stack([py[0], py[1], p1[1], s_y1, py[2], py[3]]).cpu().numpy()
         _raise_on_bad(np.array([0.0, 0.0, sums[4], sums[5]]))
