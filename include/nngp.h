@@ -272,6 +272,23 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,
  *   out[2 + c] = sum_i h_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p));
  *   h_i = noise_w[i], or 1 when noise_w is NULL.
+ *
+ * One chain sharded over ranks (the w sweep's per-colour exchange;
+ * pynngp_amd.gibbs.ShardedSeqNNGP): rank r owns the storage rows [row0, row1) and keeps
+ * replicas of w and r, exact on its own rows, their out-of-shard children (halo) and the
+ * parents of both.
+ * nngp_gibbs_prepare_range: nngp_gibbs_prepare for the rows [row0, row1) only (their
+ *   reverse entries [off[row0], off[row1]), P and 1/F); B / Ft must be current on those
+ *   rows and their children.  The full range is nngp_gibbs_prepare.
+ * nngp_gibbs_w_color: ONE colour step over member_rows (n_members rows of
+ *   nngp_gibbs_member_rows, e.g. the run of one colour this rank owns), arguments as
+ *   nngp_gibbs_w_sweep; w_out (NULL or n_members doubles) receives each member's new
+ *   w, the values the other ranks replay.
+ * nngp_gibbs_w_apply: replay other ranks' draws of one colour: rows (device int32
+ *   (n_rows, 4), 16-B aligned) = (location i, off[i], off[i + 1], src); w_src[src] is the
+ *   owner's new w_i.  dw = w_src[src] - w[i] (this rank's replica: the owner's operands),
+ *   w[i] = w_src[src], r[i] += dw, r[j] -= B[j, rev_k[e]] dw over the children -- the
+ *   owner's arithmetic, so every replica stays bit-identical to the owner's values.
  * ------------------------------------------------------------------------- */
 size_t nngp_reverse_workspace_bytes(int64_t n, int32_t m);
 int nngp_reverse_neighbors(const int32_t *nbr, int64_t n, int32_t m, int32_t *off, int32_t *rev_j, int32_t *rev_k,
@@ -288,6 +305,15 @@ int nngp_gibbs_w_sweep(const int32_t *member_rows, const int32_t *color_off_host
                        double *w, double *r, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
                        void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
+int nngp_gibbs_prepare_range(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
+                             const int32_t *rev_k, int64_t n, int32_t m, int64_t row0, int64_t row1, void *prep,
+                             size_t prep_bytes, void *stream);
+int nngp_gibbs_w_color(const int32_t *member_rows, int64_t n_members, const void *prep, int64_t n, int32_t m,
+                       double sigma2, double tau2, const double *yres, const double *noise_w, double *w, double *r,
+                       const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep, double *w_out,
+                       void *stream);
+int nngp_gibbs_w_apply(const int32_t *rows, int64_t n_rows, const double *w_src, const double *B, int64_t n, int32_t m,
+                       double *w, double *r, const int32_t *rev_j, const int32_t *rev_k, void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);
 int nngp_gibbs_stats(int64_t n, const double *r, const double *Ft, const double *yres, const double *y,
                      const double *X, int32_t p, const double *w, const double *noise_w, double *out,

@@ -9,6 +9,7 @@ from ._lib import NNGPExtensionError, LIB_PATH, version  # noqa: F401
 from .nngp import NNGP, Covariance, IsotropicCovariance, NNGPNumericalError  # noqa: F401
 from .sweep import ShardedLogLik, shard_range, combine_partials  # noqa: F401
 from .gibbs import SeqNNGP, Priors  # noqa: F401
+from .gibbs_sharded import ShardedSeqNNGP  # noqa: F401
 
 __version__ = "0.1.0"
 

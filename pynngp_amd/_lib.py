@@ -47,6 +47,9 @@ SYMBOLS = (
     "nngp_gibbs_member_rows",
     "nngp_gibbs_w_sweep",
     "nngp_gibbs_normals",
+    "nngp_gibbs_prepare_range",
+    "nngp_gibbs_w_color",
+    "nngp_gibbs_w_apply",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
 )
@@ -132,6 +135,12 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_w_sweep.restype = ctypes.c_int
     lib.nngp_gibbs_normals.argtypes = [I64, U64, U64, P, P]
     lib.nngp_gibbs_normals.restype = ctypes.c_int
+    lib.nngp_gibbs_prepare_range.argtypes = [P, P, P, P, P, I64, I32, I64, I64, P, SZ, P]
+    lib.nngp_gibbs_prepare_range.restype = ctypes.c_int
+    lib.nngp_gibbs_w_color.argtypes = [P, I64, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P, P]
+    lib.nngp_gibbs_w_color.restype = ctypes.c_int
+    lib.nngp_gibbs_w_apply.argtypes = [P, I64, P, P, I64, I32, P, P, P, P, P]
+    lib.nngp_gibbs_w_apply.restype = ctypes.c_int
     lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]
     lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
@@ -608,6 +617,52 @@ def gibbs_prepare(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: t
     _check(lib.nngp_gibbs_prepare(_ptr(B), _ptr(Ft), _ptr(off), _ptr(rev_j), _ptr(rev_k), _ptr(order), n, m, _ptr(prep),
                                   prep.numel(), _stream(dev)), "nngp_gibbs_prepare")
     return prep
+
+
+def gibbs_prepare_range(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor,
+                        rev_k: torch.Tensor, row0: int, row1: int, prep: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """:func:`gibbs_prepare` for the rows [row0, row1) only (nngp_gibbs_prepare_range): a rank's
+    own shard of a sharded chain.  ``prep`` keeps the whole-field layout."""
+    dev = _require_gpu(B, Ft, off, rev_j, rev_k, prep)
+    n, m = B.shape
+    lib = load()
+    need = lib.nngp_gibbs_prep_bytes(n, m)
+    if prep is None or prep.numel() < need:
+        prep = _workspace(need, dev)
+    _check(lib.nngp_gibbs_prepare_range(_ptr(B), _ptr(Ft), _ptr(off), _ptr(rev_j), _ptr(rev_k), n, m, int(row0),
+                                        int(row1), _ptr(prep), prep.numel(), _stream(dev)), "nngp_gibbs_prepare_range")
+    return prep
+
+
+def gibbs_w_color(member_rows: torch.Tensor, prep: torch.Tensor, m: int, sigma2: float, tau2: float,
+                  yres: torch.Tensor, w: torch.Tensor, r: torch.Tensor, rev_j: torch.Tensor, seed: int, sweep: int,
+                  z: Optional[torch.Tensor] = None, noise_w: Optional[torch.Tensor] = None,
+                  w_out: Optional[torch.Tensor] = None) -> None:
+    """ONE colour step over ``member_rows`` (rows of :func:`gibbs_member_rows`), in place on w, r;
+    ``w_out`` (len(member_rows),) receives the members' new w (nngp_gibbs_w_color)."""
+    dev = _require_gpu(member_rows, prep, yres, w, r, rev_j, z, noise_w, w_out)
+    _check_noise_w(noise_w, w.shape[0])
+    k = member_rows.shape[0]
+    if member_rows.dtype != torch.int32 or member_rows.dim() != 2 or member_rows.shape[1] != 4 \
+            or not member_rows.is_contiguous():
+        raise ValueError("member_rows must be a contiguous int32 (k, 4) tensor")
+    _check_out(w_out, "w_out", (k,), dev)
+    _check(load().nngp_gibbs_w_color(_ptr(member_rows), k, _ptr(prep), w.shape[0], int(m), float(sigma2), float(tau2),
+                                     _ptr(yres), _ptr(noise_w), _ptr(w), _ptr(r), _ptr(rev_j), _ptr(z),
+                                     int(seed) & (2 ** 64 - 1), int(sweep), _ptr(w_out), _stream(dev)),
+           "nngp_gibbs_w_color")
+
+
+def gibbs_w_apply(rows: torch.Tensor, w_src: torch.Tensor, B: torch.Tensor, w: torch.Tensor, r: torch.Tensor,
+                  rev_j: torch.Tensor, rev_k: torch.Tensor) -> None:
+    """Replay other ranks' colour draws (nngp_gibbs_w_apply): rows int32 (k, 4) = (i, off[i],
+    off[i + 1], src), w_src[src] the owner's new w_i."""
+    dev = _require_gpu(rows, w_src, B, w, r, rev_j, rev_k)
+    if rows.dtype != torch.int32 or rows.dim() != 2 or rows.shape[1] != 4 or not rows.is_contiguous():
+        raise ValueError("rows must be a contiguous int32 (k, 4) tensor")
+    n, m = B.shape
+    _check(load().nngp_gibbs_w_apply(_ptr(rows), rows.shape[0], _ptr(w_src), _ptr(B), n, m, _ptr(w), _ptr(r),
+                                     _ptr(rev_j), _ptr(rev_k), _stream(dev)), "nngp_gibbs_w_apply")
 
 
 def _check_noise_w(noise_w: Optional[torch.Tensor], n: int) -> None:

@@ -293,6 +293,56 @@ int nngp_gibbs_prepare(const double* B, const double* Ft, const int32_t* off, co
     return NNGP_OK;
 }
 
+int nngp_gibbs_prepare_range(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                             const int32_t* rev_k, int64_t n, int32_t m, int64_t row0, int64_t row1, void* prep,
+                             size_t prep_bytes, void* stream) {
+    if (Ft == nullptr || off == nullptr || prep == nullptr || (m > 0 && (B == nullptr || rev_j == nullptr ||
+                                                                          rev_k == nullptr)))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n or m");
+    if (row0 < 0 || row1 < row0 || row1 > n) return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)",
+                                                         (long long)row0, (long long)row1, (long long)n);
+    if (((uintptr_t)prep & 255) != 0) return fail(NNGP_EINVAL, "prep must be 256-byte aligned");
+    if (prep_bytes < nngp::gibbs_prep_bytes(n, m))
+        return fail(NNGP_EINVAL, "prep too small: %zu < %zu bytes", prep_bytes, nngp::gibbs_prep_bytes(n, m));
+    hipError_t e = nngp::gibbs_prepare_range_launch(B, Ft, off, rev_j, rev_k, n, m, row0, row1, prep,
+                                                    (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_prepare_range launch");
+    return NNGP_OK;
+}
+
+int nngp_gibbs_w_color(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int32_t m,
+                       double sigma2, double tau2, const double* yres, const double* noise_w, double* w, double* r,
+                       const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep, double* w_out,
+                       void* stream) {
+    if (n_members < 0 || n < 0 || m < 0 || m > NNGP_MAX_M || n_members > n)
+        return fail(NNGP_EINVAL, "bad n_members, n or m");
+    if (n_members == 0) return NNGP_OK;
+    if (member_rows == nullptr || prep == nullptr || yres == nullptr || w == nullptr || r == nullptr ||
+        (m > 0 && rev_j == nullptr))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
+    if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
+        return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
+    hipError_t e = nngp::gibbs_w_color_launch(member_rows, n_members, prep, n, m, sigma2, tau2, yres, noise_w, w, r,
+                                              rev_j, z, seed, sweep, w_out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_w_color launch");
+    return NNGP_OK;
+}
+
+int nngp_gibbs_w_apply(const int32_t* rows, int64_t n_rows, const double* w_src, const double* B, int64_t n, int32_t m,
+                       double* w, double* r, const int32_t* rev_j, const int32_t* rev_k, void* stream) {
+    if (n_rows < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows, n or m");
+    if (n_rows == 0) return NNGP_OK;
+    if (rows == nullptr || w_src == nullptr || w == nullptr || r == nullptr ||
+        (m > 0 && (B == nullptr || rev_j == nullptr || rev_k == nullptr)))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (((uintptr_t)rows & 15) != 0) return fail(NNGP_EINVAL, "rows must be 16-byte aligned");
+    hipError_t e = nngp::gibbs_w_apply_launch(rows, n_rows, w_src, B, m, w, r, rev_j, rev_k, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_w_apply launch");
+    return NNGP_OK;
+}
+
 int nngp_gibbs_member_rows(const int32_t* members, int64_t n, const int32_t* off, int32_t* member_rows, void* stream) {
     if (n < 0 || (n > 0 && (members == nullptr || off == nullptr || member_rows == nullptr)))
         return fail(NNGP_EINVAL, "bad n or null pointer argument");

@@ -237,31 +237,37 @@ constexpr int kGroup = NNGP_GIBBS_GROUP;
 constexpr int kRowLanes = NNGP_PREP_FUSED ? NNGP_PREP_LANES : 4;
 [[maybe_unused]] constexpr int kPrepUnroll = NNGP_PREP_UNROLL;
 
+// Both passes cover the rows [row0, row1) -- the whole field, or the shard a rank of a sharded
+// chain owns (nngp_gibbs_prepare_range): the entries pass walks the contiguous reverse entries
+// [off[row0], off[row1]) grid-stride (their count is only known on the device).
 __global__ __launch_bounds__(256) void gibbs_prepare_entries(const double* __restrict__ B,
                                                              const double* __restrict__ Ft,
                                                              const int32_t* __restrict__ rev_j,
                                                              const int32_t* __restrict__ rev_k,
-                                                             const int32_t* __restrict__ off, int64_t n, int m,
-                                                             double* __restrict__ Brev,
+                                                             const int32_t* __restrict__ off, int64_t row0,
+                                                             int64_t row1, int m, double* __restrict__ Brev,
                                                              double* __restrict__ Grev) {
-    const int64_t e = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (e >= n * (int64_t)m || e >= (int64_t)off[n]) return;  // entries past off[n] are padding
-    const int64_t j = rev_j[e];
-    const double b = B[j * m + rev_k[e]];
-    Brev[e] = b;
-    Grev[e] = b / Ft[j];
+    const int64_t e1 = off[row1];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = off[row0] + xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x; e < e1;
+         e += stride) {
+        const int64_t j = rev_j[e];
+        const double b = B[j * m + rev_k[e]];
+        Brev[e] = b;
+        Grev[e] = b / Ft[j];
+    }
 }
 
 __global__ __launch_bounds__(256) void gibbs_prepare_rows(const double* __restrict__ Ft,
-                                                          const int32_t* __restrict__ off, int64_t n,
+                                                          const int32_t* __restrict__ off, int64_t row0, int64_t row1,
                                                           const double* __restrict__ Brev,
                                                           const double* __restrict__ Grev, double* __restrict__ P,
                                                           double* __restrict__ invF) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int64_t i = t / kRowLanes;
+    const int64_t i = row0 + t / kRowLanes;
     const int l = (int)(t % kRowLanes);
-    const bool live = i < n;
-    const int64_t ic = live ? i : n - 1;
+    const bool live = i < row1;
+    const int64_t ic = live ? i : row1 - 1;
     const int32_t e0 = off[ic], e1 = live ? off[ic + 1] : e0;
     double acc = 0.0;
     for (int32_t e = e0 + l; e < e1; e += kRowLanes) acc = fma(Brev[e], Grev[e], acc);
@@ -344,24 +350,34 @@ size_t gibbs_prep_bytes(int64_t n, int m) {
     return 2 * align256((size_t)(n * m) * 8) + 2 * align256((size_t)n * 8);
 }
 
+hipError_t gibbs_prepare_range_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                                      const int32_t* rev_k, int64_t n, int m, int64_t row0, int64_t row1, void* prep,
+                                      hipStream_t s) {
+    if (row1 <= row0) return hipSuccess;
+    const GibbsPrep g = prep_layout(prep, n, m);
+#if NNGP_PREP_FUSED
+    if (row0 == 0 && row1 == n) {
+        hipLaunchKernelGGL(gibbs_prepare_fused, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, B, Ft,
+                           rev_j, rev_k, off, n, m, g.Brev, g.Grev, g.P, g.invF);
+        return hipGetLastError();
+    }
+#endif
+    const int64_t rows = row1 - row0;
+    // grid sized for m reverse entries per row (the average); the stride loop takes the rest
+    const int64_t ne = rows * (int64_t)m;
+    if (ne > 0)
+        hipLaunchKernelGGL(gibbs_prepare_entries, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
+                           rev_k, off, row0, row1, m, g.Brev, g.Grev);
+    hipLaunchKernelGGL(gibbs_prepare_rows, dim3((unsigned)((rows * kRowLanes + 255) / 256)), dim3(256), 0, s, Ft, off,
+                       row0, row1, g.Brev, g.Grev, g.P, g.invF);
+    return hipGetLastError();
+}
+
 hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
                                 const int32_t* rev_k, const int32_t* order, int64_t n, int m, void* prep,
                                 hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const GibbsPrep g = prep_layout(prep, n, m);
     (void)order;  // both passes stream the reverse lists in storage order; no visiting order needed
-#if NNGP_PREP_FUSED
-    hipLaunchKernelGGL(gibbs_prepare_fused, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
-                       rev_k, off, n, m, g.Brev, g.Grev, g.P, g.invF);
-    return hipGetLastError();
-#endif
-    const int64_t ne = n * (int64_t)m;
-    if (ne > 0)
-        hipLaunchKernelGGL(gibbs_prepare_entries, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
-                           rev_k, off, n, m, g.Brev, g.Grev);
-    hipLaunchKernelGGL(gibbs_prepare_rows, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, Ft, off, n,
-                       g.Brev, g.Grev, g.P, g.invF);
-    return hipGetLastError();
+    return gibbs_prepare_range_launch(B, Ft, off, rev_j, rev_k, n, m, 0, n, prep, s);
 }
 
 // ---------------------------------------------------------------- colour update
@@ -399,7 +415,8 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
                                                      const double* __restrict__ noise_w,
                                                      double* __restrict__ w, double* __restrict__ r,
                                                      const int32_t* __restrict__ rev_j,
-                                                     const double* __restrict__ z, uint64_t seed, uint64_t sweep) {
+                                                     const double* __restrict__ z, uint64_t seed, uint64_t sweep,
+                                                     double* __restrict__ w_out) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
@@ -430,6 +447,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
     if (live && l == 0) {
         w[i] = wn;
         r[i] = ri + dw;
+        if (w_out != nullptr) w_out[g] = wn;  // published to the other ranks of a sharded chain
     }
     if (has) r[jf] = fma(-bf, dw, rf);
     for (int32_t e = ef + kGroup; e < e1; e += kGroup) {
@@ -449,8 +467,59 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
         const int64_t threads = (b - a) * kGroup;
         hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                            (const int4*)member_rows + a, b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2,
-                           yres, noise_w, w, r, rev_j, z, seed, sweep);
+                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr);
     }
+    return hipGetLastError();
+}
+
+hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int m,
+                                double sigma2, double tau2, const double* yres, const double* noise_w, double* w,
+                                double* r, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
+                                double* w_out, hipStream_t s) {
+    if (n_members <= 0) return hipSuccess;
+    const GibbsPrep g = prep_layout((void*)prep, n, m);
+    const int64_t threads = n_members * kGroup;
+    hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
+                       noise_w, w, r, rev_j, z, seed, sweep, w_out);
+    return hipGetLastError();
+}
+
+// Sharded chain (nngp_gibbs_w_apply): after a colour's exchange, each rank replays the updates of the
+// other ranks' members it keeps a replica of.  Row (i, e0, e1, src): w_new = wsrc[src] (the owner's
+// draw), dw = w_new - w_i computed from this rank's replica of w_i -- the owner's operands, so the
+// same bits -- then w_i = w_new, r_i += dw and r_j -= B_{j,i} dw over the children, exactly the
+// owner's scatter (B read in place: B_{j,i} = B[j, rev_k[e]], the value the owner's Brev holds).
+__global__ __launch_bounds__(256) void gibbs_w_apply_kernel(const int4* __restrict__ rows, int64_t n_rows,
+                                                            const double* __restrict__ wsrc,
+                                                            const double* __restrict__ B, int m,
+                                                            double* __restrict__ w, double* __restrict__ r,
+                                                            const int32_t* __restrict__ rev_j,
+                                                            const int32_t* __restrict__ rev_k) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = t / kGroup;
+    const int l = (int)(t % kGroup);
+    if (g >= n_rows) return;
+    const int4 a = rows[g];
+    const int64_t i = a.x;
+    const double wn = wsrc[a.w];
+    const double dw = wn - w[i];
+    for (int32_t e = a.y + l; e < a.z; e += kGroup) {
+        const int64_t j = rev_j[e];
+        r[j] = fma(-B[j * m + rev_k[e]], dw, r[j]);
+    }
+    if (l == 0) {
+        r[i] = r[i] + dw;
+        w[i] = wn;
+    }
+}
+
+hipError_t gibbs_w_apply_launch(const int32_t* rows, int64_t n_rows, const double* wsrc, const double* B, int m,
+                                double* w, double* r, const int32_t* rev_j, const int32_t* rev_k, hipStream_t s) {
+    if (n_rows <= 0) return hipSuccess;
+    const int64_t threads = n_rows * kGroup;
+    hipLaunchKernelGGL(gibbs_w_apply_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       (const int4*)rows, n_rows, wsrc, B, m, w, r, rev_j, rev_k);
     return hipGetLastError();
 }
 

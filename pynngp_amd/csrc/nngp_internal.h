@@ -160,6 +160,15 @@ hipError_t philox_normals_launch(int64_t n, uint64_t seed, uint64_t sweep, doubl
 hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
                                 const int32_t* rev_k, const int32_t* order, int64_t n, int m, void* prep,
                                 hipStream_t s);
+hipError_t gibbs_prepare_range_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
+                                      const int32_t* rev_k, int64_t n, int m, int64_t row0, int64_t row1, void* prep,
+                                      hipStream_t s);
+hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int m,
+                                double sigma2, double tau2, const double* yres, const double* noise_w, double* w,
+                                double* r, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
+                                double* w_out, hipStream_t s);
+hipError_t gibbs_w_apply_launch(const int32_t* rows, int64_t n_rows, const double* wsrc, const double* B, int m,
+                                double* w, double* r, const int32_t* rev_j, const int32_t* rev_k, hipStream_t s);
 hipError_t gibbs_member_rows_launch(const int32_t* members, int64_t n, const int32_t* off, int32_t* rows,
                                     hipStream_t s);
 hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,

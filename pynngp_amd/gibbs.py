@@ -293,7 +293,7 @@ class SeqNNGP:
         self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
         ops.load()  # the sweep goes through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
         self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
-        self._stats = z(2 + self.p)
+        self._stats_buf = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
         self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k)
         ph = self._part.cpu().numpy()
@@ -342,8 +342,7 @@ class SeqNNGP:
         u = self.rng.random()
         if not lo <= phi_p <= hi:
             return
-        self._sweep_into(phi_p, self._B2, self._Ft2, self._r2)
-        ph = self._part.cpu().numpy()
+        ph = self._propose(phi_p)
         if ph[2] >= 0:
             # the proposal's latent factor is not positive definite (near-duplicate locations
             # with tau2 = 0 and a large phi): zero density there, so the move is rejected
@@ -356,9 +355,31 @@ class SeqNNGP:
             self.B, self._B2 = self._B2, self.B
             self.Ft, self._Ft2 = self._Ft2, self.Ft
             self.r, self._r2 = self._r2, self.r
-            self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
+            self._prepare()
             self.sum_logF, self.quad = float(ph[0]), float(ph[1])
             self.n_accept += 1
+
+    def _propose(self, phi):
+        """B / F / residuals of the unit-variance field at the proposal, into the spare buffers;
+        returns the host partials (the sharded chain overrides: own rows + halo, folded over ranks)."""
+        self._sweep_into(phi, self._B2, self._Ft2, self._r2)
+        return self._part.cpu().numpy()
+
+    def _prepare(self):
+        """Fold the accepted B / F for the colour steps (the sharded chain: its own rows only)."""
+        self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
+
+    def _stats(self):
+        """[sum r^2/F, sum h (yres - w)^2, X'H(y - w)] on the host (the sharded chain: folded over ranks)."""
+        return _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats_buf,
+                                noise_w=self.noise_w).cpu().numpy()
+
+    def _assemble(self, t):
+        """A per-node (storage order) result as every rank sees it (identity on one GPU)."""
+        return t
+
+    def _assemble_unobserved(self, t):
+        return t
 
     def _sweep_colours(self, c0, c1):
         if c1 > c0:
@@ -405,8 +426,7 @@ class SeqNNGP:
         _lib.gibbs_normals(self._z, self.seed, self.iteration)
         self.update_wt()
         self.update_ws()
-        st = _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats,
-                              noise_w=self.noise_w).cpu().numpy()
+        st = self._stats()
         self.quad = float(st[0])
         # tau2 | y, beta, w (weighted residual sum of squares over the observed; held fixed on request)
         if not self.fix_tau2:
@@ -555,10 +575,10 @@ class SeqNNGP:
         res = {k: np.asarray(v) for k, v in out.items()}
         res["phi_accept_rate"] = self.n_accept / max(self.iteration, 1)
         if keep_w_mean:
-            wm = w_sum / max(kept, 1)
+            wm = self._assemble(w_sum / max(kept, 1))
             res["w_mean"] = wm[self.pos[self.node_of_t]].cpu().numpy()  # data locations, input order
             if self.n > self.n_t or self.n_s != self.n_t:
                 res["ws_mean"] = wm[self.pos[: self.n_s]].cpu().numpy()  # reference points
         if self.y_unobserved.numel():
-            res["y_unobserved_mean"] = (y_sum / max(kept, 1)).cpu().numpy()
+            res["y_unobserved_mean"] = self._assemble_unobserved(y_sum / max(kept, 1)).cpu().numpy()
         return res

@@ -1,0 +1,318 @@
+"""One Gibbs chain sharded over ranks ("for Gibbs (config 5), the w-update adds
+per-colour halo exchanges").
+
+``SeqNNGP`` runs one chain per GPU.  ``ShardedSeqNNGP`` runs ONE chain over all ranks of a
+``torch.distributed`` group (RCCL over xGMI; gloo in the CPU tests and the one-GPU rehearsal):
+
+* rank r owns the storage rows [lo, hi) of ``shard_range`` -- a spatial region of the Z-order
+  storage layout, so a location's parents and children are mostly its own;
+* every rank keeps full-length replicas of w and of the residuals r = w - B w_N, exact (bit for
+  bit equal to the owner's values) on its own rows, their out-of-shard children (the halo H) and
+  the parents of both (the set V); the rest of the replica is never read;
+* phi | w: the B/F sweep of the own rows (its partials folded over ranks in rank order) and of
+  the halo rows (a second sweep over a gathered table: same kernel, same operands, so the same
+  bits as the owner's rows);
+* per colour: the own members' colour step (``nngp_gibbs_w_color``) publishes the members' new w
+  into a send slot; ONE all-gather per colour; ``nngp_gibbs_w_apply`` replays the draws of the
+  other ranks' members in V (dw from this rank's replica = the owner's operands, so the owner's
+  bits);
+* sigma2, tau2, beta: the stats of the own rows, all-gathered and folded in rank order, so every
+  rank draws the same scalars from the same host RNG stream.
+
+The chain is the single-GPU chain: the same Philox normals (keyed by location and sweep), the same
+per-location arithmetic; only the summation order of the global sums (the log density of the
+proposal, the conjugate statistics) follows the ranks.  With one rank it is ``SeqNNGP``'s chain
+bit for bit (tests/test_gpu_gibbs_sharded.py).  Cost per iteration on top of the sharded work:
+one all-gather per colour (32 at m = 15) and the replay of the boundary members.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib, ops
+from .gibbs import SeqNNGP
+from .sweep import combine_partials, shard_range
+
+
+@dataclasses.dataclass
+class GibbsShardPlan:
+    """Host-side plan of one rank of a sharded chain (numpy; see :func:`gibbs_shard_plan`)."""
+    world: int
+    rank: int
+    lo: int
+    hi: int
+    bounds: np.ndarray      # (world + 1,) shard boundaries
+    run: np.ndarray         # (n_colors, world + 1): members[run[c, r]:run[c, r + 1]] = rank r's members of colour c
+    maxc: np.ndarray        # (n_colors,) the largest per-rank run of each colour (the all-gather slot size)
+    send_off: np.ndarray    # (n_colors + 1,) colour c's send slot: send[send_off[c]:send_off[c] + maxc[c]]
+    recv_off: np.ndarray    # (n_colors + 1,) colour c's gathered block: recv[recv_off[c]:recv_off[c + 1]]
+    halo: np.ndarray        # (n_h,) out-of-shard children of the own rows, ascending
+    replica: np.ndarray     # (n_v,) V: own rows, halo and the parents of both, ascending
+    apply_rows: np.ndarray  # (n_apply, 4) int32 (i, off[i], off[i + 1], src) of the foreign rows of V, by colour
+    apply_off: np.ndarray   # (n_colors + 1,)
+
+
+def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, rank: int) -> GibbsShardPlan:
+    """Plan rank ``rank`` of ``world`` for the DAG in storage order (host numpy arrays: nbr (n, m),
+    reverse CSR off / rev_j, colours, members grouped by colour ascending inside a colour, colour
+    offsets).  Every rank computes the same runs, slot sizes and sources."""
+    nbr = np.asarray(nbr)
+    off = np.asarray(off, dtype=np.int64)
+    rev_j = np.asarray(rev_j)
+    colors = np.asarray(colors, dtype=np.int64)
+    members = np.asarray(members, dtype=np.int64)
+    color_off = np.asarray(color_off, dtype=np.int64)
+    n = nbr.shape[0]
+    n_colors = len(color_off) - 1
+    bounds = np.array([shard_range(n, r, world)[0] for r in range(world)] + [n], dtype=np.int64)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    run = np.empty((n_colors, world + 1), dtype=np.int64)
+    for c in range(n_colors):
+        seg = members[color_off[c]:color_off[c + 1]]
+        if seg.size > 1 and not np.all(seg[1:] > seg[:-1]):
+            raise ValueError("members must ascend inside each colour (storage order)")
+        run[c] = color_off[c] + np.searchsorted(seg, bounds)
+    counts = np.diff(run, axis=1)
+    maxc = counts.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
+    send_off = np.concatenate([[0], np.cumsum(maxc)]).astype(np.int64)
+    recv_off = np.concatenate([[0], np.cumsum(maxc * world)]).astype(np.int64)
+    # halo: children of the own rows outside the shard; V: own rows, halo, parents of both
+    ch = rev_j[off[lo]:off[hi]].astype(np.int64)
+    halo = np.unique(ch[(ch < lo) | (ch >= hi)])
+    par = np.concatenate([nbr[lo:hi].ravel(), nbr[halo].ravel()]).astype(np.int64)
+    par = par[(par >= 0) & (par < n)]
+    replica = np.unique(np.concatenate([np.arange(lo, hi), halo, par]))
+    foreign = replica[(replica < lo) | (replica >= hi)]
+    pos = np.empty(n, dtype=np.int64)
+    pos[members] = np.arange(n)
+    cf = colors[foreign]
+    owner = np.searchsorted(bounds, foreign, side="right") - 1
+    k = pos[foreign] - run[cf, owner]
+    src = recv_off[cf] + owner * maxc[cf] + k
+    order = np.argsort(cf, kind="stable")
+    apply_rows = np.stack([foreign, off[foreign], off[foreign + 1], src], axis=1)[order].astype(np.int32)
+    apply_off = np.concatenate([[0], np.cumsum(np.bincount(cf, minlength=n_colors))]).astype(np.int64)
+    return GibbsShardPlan(world, rank, lo, hi, bounds, run, maxc, send_off, recv_off, halo, replica,
+                          np.ascontiguousarray(apply_rows), apply_off)
+
+
+class ColourExchange:
+    """The per-colour all-gather of a sharded chain: the own members' new w go to
+    ``send[send_off[c]:...]`` and arrive at every rank in ``recv[recv_off[c]:recv_off[c + 1]]``
+    as (world, maxc[c]) (rank-major).  Device buffers on the chain's device (RCCL), or CPU
+    tensors with gloo (the CPU tests)."""
+
+    def __init__(self, plan: GibbsShardPlan, device, group=None, active: bool = True):
+        self.plan, self.group, self.active = plan, group, active
+        self.send = torch.zeros(int(plan.send_off[-1]) + 1, dtype=torch.float64, device=device)
+        self.recv = torch.zeros(int(plan.recv_off[-1]) + 1, dtype=torch.float64, device=device)
+        self.n_collectives = 0
+
+    def send_slot(self, c: int) -> torch.Tensor:
+        a = int(self.plan.send_off[c])
+        return self.send[a:a + int(self.plan.maxc[c])]
+
+    def exchange(self, c: int) -> None:
+        p = self.plan
+        if not self.active or p.maxc[c] == 0:
+            return
+        dist.all_gather_into_tensor(self.recv[int(p.recv_off[c]):int(p.recv_off[c + 1])], self.send_slot(c),
+                                    group=self.group)
+        self.n_collectives += 1
+
+
+class ShardedSeqNNGP(SeqNNGP):
+    """One NNGP Gibbs chain over the ranks of a process group (module docstring).
+
+    Built on every rank with the same arguments as :class:`SeqNNGP` (the same data, seed and
+    settings: the DAG, colouring and storage order are computed identically everywhere), plus
+    ``rank`` / ``world`` / ``group`` (default: the initialised ``torch.distributed`` group;
+    without one, a single rank).  ``collective`` forces the exchanges through the group even at
+    one rank (the path a one-GPU box tests).  Results (``w_nodes`` / ``w_s`` / ``w_t``,
+    ``sample``) are gathered over the ranks and identical on every rank.
+    """
+
+    def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
+                 collective: Optional[bool] = None, **kwargs):
+        super().__init__(*args, **kwargs)
+        inited = dist.is_available() and dist.is_initialized()
+        self.rank = int(rank if rank is not None else (dist.get_rank(group) if inited else 0))
+        self.world = int(world if world is not None else (dist.get_world_size(group) if inited else 1))
+        self.group = group
+        self.collective = bool(collective) if collective is not None else inited
+        if self.world > 1 and not self.collective:
+            raise ValueError("a sharded chain over several ranks needs a torch.distributed process group")
+        dev = self.device
+        n, m = self.n, self.m
+        self.plan = p = gibbs_shard_plan(self.nbr.cpu().numpy(), self.off.cpu().numpy(), self.rev_j.cpu().numpy(),
+                                         self.colors, self.members.cpu().numpy(), self.color_off, self.world,
+                                         self.rank)
+        self.lo, self.hi = p.lo, p.hi
+        self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
+        self._apply_rows = torch.from_numpy(p.apply_rows).to(dev)
+        self._xchg = ColourExchange(p, dev, group, active=self.collective)
+        # halo sweep: the halo rows' own points appended to the coordinate table (row n + t = halo[t]),
+        # and w kept in a buffer of n + n_h values whose tail receives w[halo] before each sweep
+        self._halo = torch.from_numpy(p.halo).to(dev)
+        self._n_h = int(p.halo.size)
+        self._coords_ext = torch.cat([self.coords, self.coords[self._halo]]).contiguous()
+        self._nbr_h = self.nbr[self._halo].contiguous()
+        self._w_ext = torch.empty(n + self._n_h, dtype=torch.float64, device=dev)
+        self._w_ext[:n].copy_(self.w)
+        self.w = self._w_ext[:n]
+        z = lambda *s: torch.empty(s, dtype=torch.float64, device=dev)  # noqa: E731
+        self._Bh, self._Fh, self._rh, self._part_h = z(self._n_h, m), z(self._n_h), z(self._n_h), z(4)
+        self._ws_own = _lib.bf_workspace(self.hi - self.lo, m, self.algo, dev, kind=self.kind,
+                                         dim=self.coords.shape[1])
+        self._ws_h = _lib.bf_workspace(max(self._n_h, 1), m, self.algo, dev, kind=self.kind, dim=self.coords.shape[1])
+        self._stats_ws = None
+        self._L = _lib.load()
+
+    # ------------------------------------------------------------------ sharded pieces
+    def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """The full (n,) vector from every rank's own rows (exact: each row comes from its owner)."""
+        if not self.collective:
+            return t
+        b = self.plan.bounds
+        size = int(np.max(np.diff(b)))
+        send = torch.zeros(size, dtype=t.dtype, device=t.device)
+        send[: self.hi - self.lo].copy_(t[self.lo:self.hi])
+        recv = torch.empty(size * self.world, dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(recv, send, group=self.group)
+        g = recv.view(self.world, size)
+        return torch.cat([g[r, : int(b[r + 1] - b[r])] for r in range(self.world)])
+
+    def _fold_rows(self, local: torch.Tensor) -> np.ndarray:
+        """All-gather a small per-rank vector and sum it in rank order on the host."""
+        if not self.collective:
+            return local.cpu().numpy()
+        g = torch.empty((self.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(g, local.reshape((1,) + tuple(local.shape)), group=self.group)
+        rows = g.cpu().numpy()
+        acc = rows[0].copy()
+        for r in range(1, self.world):
+            acc += rows[r]
+        return acc
+
+    def _propose(self, phi):
+        lo, hi, n = self.lo, self.hi, self.n
+        torch.ops.nngp.bf_sweep_out(self.coords, self.nbr[lo:hi], None, lo, self._kind_code, 1.0, float(phi), 0.0,
+                                    self.w, self._B2[lo:hi], self._Ft2[lo:hi], self._r2[lo:hi], self._part,
+                                    self._ws_own, self._algo_code, self._nu_arg)
+        if self._n_h:
+            torch.index_select(self.w, 0, self._halo, out=self._w_ext[n:])
+            torch.ops.nngp.bf_sweep_out(self._coords_ext, self._nbr_h, None, n, self._kind_code, 1.0, float(phi), 0.0,
+                                        self._w_ext, self._Bh, self._Fh, self._rh, self._part_h, self._ws_h,
+                                        self._algo_code, self._nu_arg)
+            self._B2.index_copy_(0, self._halo, self._Bh)
+            self._Ft2.index_copy_(0, self._halo, self._Fh)
+            self._r2.index_copy_(0, self._halo, self._rh)
+        p = combine_partials(self._part, self.world, self.group, force=self.collective)
+        return p.cpu().numpy()
+
+    def _prepare(self):
+        self._prep = _lib.gibbs_prepare_range(self.B, self.Ft, self.off, self.rev_j, self.rev_k, self.lo, self.hi,
+                                              prep=self._prep)
+
+    def _stats(self):
+        lo, hi = self.lo, self.hi
+        nw = None if self.noise_w is None else self.noise_w[lo:hi]
+        if self._stats_ws is None:
+            self._stats_ws = _lib._workspace(self._L.nngp_gibbs_stats_workspace_bytes(max(hi - lo, 1), self.p),
+                                             self.device)
+        st = _lib.gibbs_stats(self.r[lo:hi], self.Ft[lo:hi], self.yres[lo:hi], self.y[lo:hi], self.X[lo:hi],
+                              self.w[lo:hi], out=self._stats_buf, workspace=self._stats_ws, noise_w=nw)
+        return self._fold_rows(st)
+
+    def _sweep_colours(self, c0, c1):
+        """Colour steps c0..c1-1: own members, one all-gather, replay of the foreign replicas."""
+        if c1 <= c0:
+            return
+        L, p, x = self._L, self.plan, self._xchg
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        mr, ap = self._member_rows.data_ptr(), self._apply_rows.data_ptr()
+        prep, yres, w, r = self._prep.data_ptr(), self.yres.data_ptr(), self.w.data_ptr(), self.r.data_ptr()
+        nw = None if self.noise_w is None else self.noise_w.data_ptr()
+        rev_j, rev_k, B, z = self.rev_j.data_ptr(), self.rev_k.data_ptr(), self.B.data_ptr(), self._z.data_ptr()
+        send, recv = x.send.data_ptr(), x.recv.data_ptr()
+        seed = self.seed & (2 ** 64 - 1)
+        n, m = self.n, self.m
+        rk = self.rank
+        for c in range(c0, c1):
+            a, b = int(p.run[c, rk]), int(p.run[c, rk + 1])
+            rc = L.nngp_gibbs_w_color(mr + 16 * a, b - a, prep, n, m, self.sigma2, self.tau2, yres, nw, w, r, rev_j,
+                                      z, seed, self.iteration, send + 8 * int(p.send_off[c]), stream)
+            if rc != 0:
+                _lib._check(rc, "nngp_gibbs_w_color")
+            x.exchange(c)
+            a2, b2 = int(p.apply_off[c]), int(p.apply_off[c + 1])
+            if b2 > a2:
+                rc = L.nngp_gibbs_w_apply(ap + 16 * a2, b2 - a2, recv, B, n, m, w, r, rev_j, rev_k, stream)
+                if rc != 0:
+                    _lib._check(rc, "nngp_gibbs_w_apply")
+
+    # ------------------------------------------------------------------ results (gathered)
+    @property
+    def w_full(self) -> torch.Tensor:
+        """w in storage order, every row from its owner."""
+        return self._gather_rows(self.w)
+
+    @property
+    def w_nodes(self) -> torch.Tensor:
+        return self.w_full[self.pos]
+
+    @property
+    def w_s(self) -> torch.Tensor:
+        return self.w_full[self.pos[: self.n_s]]
+
+    @property
+    def w_t(self) -> torch.Tensor:
+        return self.w_full[self.pos[self.node_of_t]]
+
+    def _assemble(self, t):
+        return self._gather_rows(t)
+
+    def _assemble_unobserved(self, t):
+        """Per-unobserved-node values, each from the rank owning the node (exact: x + 0)."""
+        if not self.collective or t.numel() == 0:
+            return t
+        own = (self._un_nodes >= self.lo) & (self._un_nodes < self.hi)
+        t = torch.where(own, t, torch.zeros_like(t))
+        dist.all_reduce(t, group=self.group)
+        return t
+
+    def y_unobserved_full(self) -> torch.Tensor:
+        """The current posterior-predictive draws, each from the rank that owns its node."""
+        return self._assemble_unobserved(self.y_unobserved)
+
+    def set_w(self, ws=None, wt=None):
+        SeqNNGP.set_w(self, ws, wt)  # gathers w_nodes, rebinds w, reruns the (whole-field) sweep
+        self._w_ext[: self.n].copy_(self.w)
+        self.w = self._w_ext[: self.n]
+
+    def save(self, path) -> None:
+        """Every rank calls it; rank 0 writes the gathered state (a :class:`SeqNNGP` checkpoint)."""
+        w_full, r_full = self._gather_rows(self.w), self._gather_rows(self.r)
+        y_un = self.y_unobserved_full()
+        if self.rank != 0:
+            return
+        saved = self.w, self.r, self.y_unobserved
+        self.w, self.r, self.y_unobserved = w_full, r_full, y_un
+        try:
+            SeqNNGP.save(self, path)
+        finally:
+            self.w, self.r, self.y_unobserved = saved
+
+    def restore(self, path) -> "ShardedSeqNNGP":
+        SeqNNGP.restore(self, path)  # replicated: w, r, B, F and the prep are exact on every row
+        self._w_ext[: self.n].copy_(self.w)
+        self.w = self._w_ext[: self.n]
+        return self
+
+
+__all__ = ["ShardedSeqNNGP", "GibbsShardPlan", "gibbs_shard_plan", "ColourExchange", "ops"]

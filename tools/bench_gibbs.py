@@ -4,6 +4,8 @@ One iteration = SeqNNGP.step(): MH proposal for phi (one fused B/F sweep + resid
 conjugate sigma2, the colour-ordered w sweep, tau2 and beta draws (host scalars).
 Synthetic response data y = 1 + w + eps from the seed; prints one JSON line.
     python tools/bench_gibbs.py [--n 1000000 --m 15 --iters 300 --warmup 100]
+    --single-chain: ONE chain sharded over the ranks (ShardedSeqNNGP); with --force-group on one
+    GPU a one-rank "nccl" group, so every per-colour exchange runs through RCCL
 (100 warm-up iterations: the GPU clock settles over the first ~50 ms of sustained load)
 """
 import argparse
@@ -23,44 +25,67 @@ ap.add_argument("--n", type=int, default=1_000_000)
 ap.add_argument("--m", type=int, default=15)
 ap.add_argument("--iters", type=int, default=300)
 ap.add_argument("--warmup", type=int, default=100)
+ap.add_argument("--single-chain", action="store_true")
+ap.add_argument("--force-group", action="store_true")
+ap.add_argument("--backend", default="nccl")
 args = ap.parse_args()
 # several GPUs (torchrun): independent chains, one per GPU ("replicas only")
 world = int(os.environ.get("WORLD_SIZE", "1"))
 rank = int(os.environ.get("RANK", "0"))
 dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
 torch.cuda.set_device(dev)
-if world > 1:
+grouped = world > 1 or args.force_group
+if grouped:
     import torch.distributed as dist
 
-    dist.init_process_group("nccl", device_id=dev)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29513")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(args.backend)
 rng = np.random.default_rng(2)
 coords = rng.uniform(0, 1, (args.n, 2))
 y = 1.0 + rng.standard_normal(args.n) * 0.5 + 0.3 * rng.standard_normal(args.n)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
+if args.single_chain:
+    from pynngp_amd import ShardedSeqNNGP
+
+    g = ShardedSeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev)
+else:
+    g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
 torch.cuda.synchronize()
 setup_s = time.perf_counter() - t0
 for _ in range(args.warmup):
     g.step()
 torch.cuda.synchronize()
-if world > 1:
+if grouped:
     dist.barrier()
 t0 = time.perf_counter()
 for _ in range(args.iters):
     g.step()
 torch.cuda.synchronize()
-if world > 1:
+if grouped:
     dist.barrier()
 el = time.perf_counter() - t0
-if world > 1:
+if grouped:
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 if rank == 0:
-    print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, one chain per GPU",
-                      "chains": world, "chain_iters_per_s": world * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
+    extra = {}
+    if args.single_chain:
+        extra = {"halo_rows": int(g._n_h), "replayed_rows": int(g._apply_rows.shape[0]),
+                 "collectives_per_iter": g._xchg.n_collectives / max(1, g.iteration), "group": grouped,
+                 "backend": args.backend if grouped else None}
+    chains = 1 if args.single_chain else world
+    what = "ONE chain sharded over the GPUs" if args.single_chain else "one chain per GPU"
+    print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, {what}", **extra,
+                      "chains": chains, "chain_iters_per_s": chains * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
                   "locations_per_s": args.n * args.iters / el, "setup_s": setup_s, "n_colors": int(g.n_colors),
                   "phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "accept": g.n_accept / max(1, g.iteration)}))
-if world > 1:
+if grouped:
     dist.destroy_process_group()
