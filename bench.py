@@ -196,16 +196,21 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     ("replicas only": the w sweep's per-colour halo exchange would cost more than the sweep at this
     N); a step = one full iteration (phi MH with its fused B/F sweep, sigma2, the
     colour-ordered w sweep, tau2, beta)."""
-    from pynngp_amd import Priors, SeqNNGP
+    from pynngp_amd import Priors, SeqNNGP, ShardedSeqNNGP
 
-    n = args.n
+    single = args.single_chain
+    n = args.n * world if single else args.n  # single chain: n locations per GPU, one field over all
     m = args.m
     sigma2, phi, tau2, beta = 1.0, 30.0, 0.1, (1.0, -0.5)
     coords, X, y, _ = synth_gibbs_field(n, 5, sigma2, phi, tau2, beta, dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    g = SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
-                seed=1 + rank, device=dev)
+    if single:
+        g = ShardedSeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
+                           seed=1, device=dev, collective=distributed)
+    else:
+        g = SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
+                    seed=1 + rank, device=dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     for _ in range(args.warmup):
@@ -231,7 +236,10 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     reps = 50
     e0.record(stream)
     for _ in range(reps):
-        g._sweep_into(g.phi, g._B2, g._Ft2, g._r2)
+        if single:  # own rows + halo rows, partials folded over the ranks
+            g._propose(g.phi)
+        else:
+            g._sweep_into(g.phi, g._B2, g._Ft2, g._r2)
     e1.record(stream)
     torch.cuda.synchronize()
     sweep_ms = e0.elapsed_time(e1) / reps
@@ -248,18 +256,20 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     ms_iter = 1e3 * elapsed / args.steps
     if rank == 0:
         bpl = bytes_per_location(m) + 8  # + the residual r written for the sampler
-        achieved = bpl * n / (sweep_ms * 1e-3)
+        rows = g.hi - g.lo if single else n
+        achieved = bpl * rows / (sweep_ms * 1e-3)
+        chains = 1 if single else world
         out = {
-            "metric": "NNGP Gibbs sampler iterations/sec (BASELINE config 5: N=1M, m=15, 1,000 sweeps; one chain "
-                      "per GPU)",
-            "value": world * args.steps / elapsed,
+            "metric": "NNGP Gibbs sampler iterations/sec (BASELINE config 5: N=1M, m=15, 1,000 sweeps; " + (
+                "ONE chain sharded over the GPUs)" if single else "one chain per GPU)"),
+            "value": chains * args.steps / elapsed,
             "unit": "chain-iterations/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_iter,
             "iterations_per_s_per_chain": args.steps / elapsed,
-            "locations_per_s": world * n * args.steps / elapsed,
+            "locations_per_s": chains * n * args.steps / elapsed,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -267,10 +277,12 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
             "data": "synthetic: uniform [0,1]^2 coords, y = X beta + w + e, w an exponential GP field (sigma2=1, "
                     "phi=30; random Fourier features), tau2=0.1, beta=(1, -0.5)",
             "config": {
-                "workload": f"BASELINE config 5: SeqNNGP Gibbs sampler, N={n} per chain, m={m}, exponential, "
+                "workload": f"BASELINE config 5: {'ShardedSeqNNGP' if single else 'SeqNNGP'} Gibbs sampler, "
+                            f"N={n} per chain, m={m}, exponential, "
                             f"{args.steps} timed iterations after {args.warmup} warm-up",
-                "n_per_gpu": n, "m": m, "kind": "exponential", "chains": world,
-                "parallelism": f"replicas x{world} (one independent chain per GPU)",
+                "n_per_gpu": args.n, "m": m, "kind": "exponential", "chains": chains,
+                "parallelism": (f"one chain over {world} GPU(s): storage-row shards, one all-gather per colour"
+                                if single else f"replicas x{world} (one independent chain per GPU)"),
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
@@ -280,7 +292,7 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
             "roofline": {
                 "bound": "hbm", "kernel": "fused B/F + residual sweep of a phi proposal",
                 "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                "traffic": None, "algorithmic_bytes_per_location": bpl, "kernel_ms": sweep_ms, "kernel_rows": n,
+                "traffic": None, "algorithmic_bytes_per_location": bpl, "kernel_ms": sweep_ms, "kernel_rows": rows,
             },
             "state": {"phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "beta": list(map(float, g.beta))},
             "lib": os.path.relpath(_lib.LIB_PATH, ROOT),
@@ -333,6 +345,9 @@ def main():
     ap.add_argument("--force-collective", action="store_true",
                     help="exchange the partials through torch.distributed even on one rank (a one-rank RCCL group "
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
+    ap.add_argument("--single-chain", action="store_true",
+                    help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
+                         "of one chain per GPU")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()

@@ -284,6 +284,10 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  *   nngp_gibbs_member_rows, e.g. the run of one colour this rank owns), arguments as
  *   nngp_gibbs_w_sweep; w_out (NULL or n_members doubles) receives each member's new
  *   w, the values the other ranks replay.
+ * nngp_gibbs_w_color_dev: the same step with (sigma2, tau2) read from device memory
+ *   var[0], var[1] (the kernel forms 1/var exactly as the host would: the same bits) and
+ *   the given normals z (required) -- launch arguments that stay fixed across iterations,
+ *   so a captured HIP graph of the colour loop replays with each iteration's values.
  * nngp_gibbs_w_apply: replay other ranks' draws of one colour: rows (device int32
  *   (n_rows, 4), 16-B aligned) = (location i, off[i], off[i + 1], src); w_src[src] is the
  *   owner's new w_i.  dw = w_src[src] - w[i] (this rank's replica: the owner's operands),
@@ -312,6 +316,9 @@ int nngp_gibbs_w_color(const int32_t *member_rows, int64_t n_members, const void
                        double sigma2, double tau2, const double *yres, const double *noise_w, double *w, double *r,
                        const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep, double *w_out,
                        void *stream);
+int nngp_gibbs_w_color_dev(const int32_t *member_rows, int64_t n_members, const void *prep, int64_t n, int32_t m,
+                           const double *var, const double *yres, const double *noise_w, double *w, double *r,
+                           const int32_t *rev_j, const double *z, double *w_out, void *stream);
 int nngp_gibbs_w_apply(const int32_t *rows, int64_t n_rows, const double *w_src, const double *B, int64_t n, int32_t m,
                        double *w, double *r, const int32_t *rev_j, const int32_t *rev_k, void *stream);
 size_t nngp_gibbs_stats_workspace_bytes(int64_t n, int32_t p);

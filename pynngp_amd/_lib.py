@@ -49,6 +49,7 @@ SYMBOLS = (
     "nngp_gibbs_normals",
     "nngp_gibbs_prepare_range",
     "nngp_gibbs_w_color",
+    "nngp_gibbs_w_color_dev",
     "nngp_gibbs_w_apply",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
@@ -139,6 +140,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_prepare_range.restype = ctypes.c_int
     lib.nngp_gibbs_w_color.argtypes = [P, I64, P, I64, I32, D, D, P, P, P, P, P, P, U64, U64, P, P]
     lib.nngp_gibbs_w_color.restype = ctypes.c_int
+    lib.nngp_gibbs_w_color_dev.argtypes = [P, I64, P, I64, I32, P, P, P, P, P, P, P, P, P]
+    lib.nngp_gibbs_w_color_dev.restype = ctypes.c_int
     lib.nngp_gibbs_w_apply.argtypes = [P, I64, P, P, I64, I32, P, P, P, P, P]
     lib.nngp_gibbs_w_apply.restype = ctypes.c_int
     lib.nngp_gibbs_stats_workspace_bytes.argtypes = [I64, I32]

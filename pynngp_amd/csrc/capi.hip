@@ -311,10 +311,10 @@ int nngp_gibbs_prepare_range(const double* B, const double* Ft, const int32_t* o
     return NNGP_OK;
 }
 
-int nngp_gibbs_w_color(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int32_t m,
-                       double sigma2, double tau2, const double* yres, const double* noise_w, double* w, double* r,
-                       const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep, double* w_out,
-                       void* stream) {
+static int gibbs_w_color_common(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n,
+                                int32_t m, double sigma2, double tau2, const double* var, const double* yres,
+                                const double* noise_w, double* w, double* r, const int32_t* rev_j, const double* z,
+                                uint64_t seed, uint64_t sweep, double* w_out, void* stream) {
     if (n_members < 0 || n < 0 || m < 0 || m > NNGP_MAX_M || n_members > n)
         return fail(NNGP_EINVAL, "bad n_members, n or m");
     if (n_members == 0) return NNGP_OK;
@@ -322,12 +322,29 @@ int nngp_gibbs_w_color(const int32_t* member_rows, int64_t n_members, const void
         (m > 0 && rev_j == nullptr))
         return fail(NNGP_EINVAL, "null pointer argument");
     if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
-    if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
+    if (var == nullptr && (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2)))
         return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
-    hipError_t e = nngp::gibbs_w_color_launch(member_rows, n_members, prep, n, m, sigma2, tau2, yres, noise_w, w, r,
-                                              rev_j, z, seed, sweep, w_out, (hipStream_t)stream);
+    hipError_t e = nngp::gibbs_w_color_launch(member_rows, n_members, prep, n, m, var ? 1.0 : sigma2,
+                                              var ? 1.0 : tau2, yres, noise_w, w, r, rev_j, z, seed, sweep, w_out, var,
+                                              (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_color launch");
     return NNGP_OK;
+}
+
+int nngp_gibbs_w_color(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int32_t m,
+                       double sigma2, double tau2, const double* yres, const double* noise_w, double* w, double* r,
+                       const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep, double* w_out,
+                       void* stream) {
+    return gibbs_w_color_common(member_rows, n_members, prep, n, m, sigma2, tau2, nullptr, yres, noise_w, w, r, rev_j,
+                                z, seed, sweep, w_out, stream);
+}
+
+int nngp_gibbs_w_color_dev(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int32_t m,
+                           const double* var, const double* yres, const double* noise_w, double* w, double* r,
+                           const int32_t* rev_j, const double* z, double* w_out, void* stream) {
+    if (var == nullptr || (n_members > 0 && z == nullptr)) return fail(NNGP_EINVAL, "var and z must be given");
+    return gibbs_w_color_common(member_rows, n_members, prep, n, m, 1.0, 1.0, var, yres, noise_w, w, r, rev_j, z, 0, 0,
+                                w_out, stream);
 }
 
 int nngp_gibbs_w_apply(const int32_t* rows, int64_t n_rows, const double* w_src, const double* B, int64_t n, int32_t m,

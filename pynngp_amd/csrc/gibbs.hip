@@ -416,7 +416,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
                                                      double* __restrict__ w, double* __restrict__ r,
                                                      const int32_t* __restrict__ rev_j,
                                                      const double* __restrict__ z, uint64_t seed, uint64_t sweep,
-                                                     double* __restrict__ w_out) {
+                                                     double* __restrict__ w_out, const double* __restrict__ var) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
@@ -436,6 +436,10 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
     for (int32_t e = ef + kGroup; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
 #pragma unroll
     for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (var != nullptr) {  // (sigma2, tau2) from device memory: a graph-captured step replays with new values
+        is2 = 1.0 / var[0];
+        it2 = 1.0 / var[1];
+    }
     const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i];
     const double it2i = noise_w != nullptr ? it2 * noise_w[i] : it2;  // 1 / (tau2 / h_i)
     const double prec = fma(iF + Pi, is2, it2i);
@@ -467,7 +471,7 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
         const int64_t threads = (b - a) * kGroup;
         hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                            (const int4*)member_rows + a, b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2,
-                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr);
+                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr);
     }
     return hipGetLastError();
 }
@@ -475,13 +479,13 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
 hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int m,
                                 double sigma2, double tau2, const double* yres, const double* noise_w, double* w,
                                 double* r, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
-                                double* w_out, hipStream_t s) {
+                                double* w_out, const double* var, hipStream_t s) {
     if (n_members <= 0) return hipSuccess;
     const GibbsPrep g = prep_layout((void*)prep, n, m);
     const int64_t threads = n_members * kGroup;
     hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                        (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
-                       noise_w, w, r, rev_j, z, seed, sweep, w_out);
+                       noise_w, w, r, rev_j, z, seed, sweep, w_out, var);
     return hipGetLastError();
 }
 

@@ -166,7 +166,7 @@ hipError_t gibbs_prepare_range_launch(const double* B, const double* Ft, const i
 hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, const void* prep, int64_t n, int m,
                                 double sigma2, double tau2, const double* yres, const double* noise_w, double* w,
                                 double* r, const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep,
-                                double* w_out, hipStream_t s);
+                                double* w_out, const double* var, hipStream_t s);
 hipError_t gibbs_w_apply_launch(const int32_t* rows, int64_t n_rows, const double* wsrc, const double* B, int m,
                                 double* w, double* r, const int32_t* rev_j, const int32_t* rev_k, hipStream_t s);
 hipError_t gibbs_member_rows_launch(const int32_t* members, int64_t n, const int32_t* off, int32_t* rows,

@@ -133,12 +133,13 @@ class ShardedSeqNNGP(SeqNNGP):
     settings: the DAG, colouring and storage order are computed identically everywhere), plus
     ``rank`` / ``world`` / ``group`` (default: the initialised ``torch.distributed`` group;
     without one, a single rank).  ``collective`` forces the exchanges through the group even at
-    one rank (the path a one-GPU box tests).  Results (``w_nodes`` / ``w_s`` / ``w_t``,
+    one rank (the path a one-GPU box tests).  ``graphs`` (default: on over RCCL) replays the
+    colour loop from captured HIP graphs.  Results (``w_nodes`` / ``w_s`` / ``w_t``,
     ``sample``) are gathered over the ranks and identical on every rank.
     """
 
     def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
-                 collective: Optional[bool] = None, **kwargs):
+                 collective: Optional[bool] = None, graphs: Optional[bool] = None, **kwargs):
         super().__init__(*args, **kwargs)
         inited = dist.is_available() and dist.is_initialized()
         self.rank = int(rank if rank is not None else (dist.get_rank(group) if inited else 0))
@@ -172,6 +173,13 @@ class ShardedSeqNNGP(SeqNNGP):
         self._ws_h = _lib.bf_workspace(max(self._n_h, 1), m, self.algo, dev, kind=self.kind, dim=self.coords.shape[1])
         self._stats_ws = None
         self._L = _lib.load()
+        # HIP graphs of the colour loop: over RCCL only (a gloo collective cannot be captured)
+        backend = dist.get_backend(group) if self.collective else None
+        self._use_graphs = bool(graphs) if graphs is not None else backend == "nccl"
+        if self._use_graphs and backend not in (None, "nccl"):
+            raise ValueError(f"graphs=True needs the nccl (RCCL) backend or no group, not {backend!r}")
+        self._var = torch.empty(2, dtype=torch.float64, device=dev)  # (sigma2, tau2) for the captured steps
+        self._graphs, self._graph_seen, self._coll_per_range = {}, set(), {}
 
     # ------------------------------------------------------------------ sharded pieces
     def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
@@ -230,23 +238,56 @@ class ShardedSeqNNGP(SeqNNGP):
         return self._fold_rows(st)
 
     def _sweep_colours(self, c0, c1):
-        """Colour steps c0..c1-1: own members, one all-gather, replay of the foreign replicas."""
+        """Colour steps c0..c1-1: own members, one all-gather, replay of the foreign replicas.
+
+        Over RCCL the loop is captured once per (colour range, current B / r buffers) into a HIP
+        graph and replayed: issuing a colour's three operations from the host costs ~18 us (the
+        collective's enqueue dominates), more than the colour's GPU work at N = 1e6 per GPU.  The
+        captured launches read sigma2 / tau2 from device memory (nngp_gibbs_w_color_dev), written
+        before each replay; the normals come from ``_z`` (filled each iteration)."""
         if c1 <= c0:
             return
+        if not self._use_graphs:
+            self._colour_loop(c0, c1, graph=False)
+            return
+        self._var[0].fill_(self.sigma2)
+        self._var[1].fill_(self.tau2)
+        key = (c0, c1, self.B.data_ptr(), self.r.data_ptr(), self._prep.data_ptr())
+        gr = self._graphs.get(key)
+        if gr is None:
+            if key not in self._graph_seen:  # first use: eager (communicators and buffers settle)
+                self._graph_seen.add(key)
+                self._colour_loop(c0, c1, graph=True)
+                return
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                self._colour_loop(c0, c1, graph=True)
+            self._graphs[key] = gr
+        gr.replay()
+        self._xchg.n_collectives += self._coll_per_range.setdefault((c0, c1), int(
+            sum(1 for c in range(c0, c1) if self.plan.maxc[c] > 0)) if self._xchg.active else 0)
+
+    def _colour_loop(self, c0, c1, graph):
         L, p, x = self._L, self.plan, self._xchg
         stream = torch.cuda.current_stream(self.device).cuda_stream
         mr, ap = self._member_rows.data_ptr(), self._apply_rows.data_ptr()
         prep, yres, w, r = self._prep.data_ptr(), self.yres.data_ptr(), self.w.data_ptr(), self.r.data_ptr()
         nw = None if self.noise_w is None else self.noise_w.data_ptr()
         rev_j, rev_k, B, z = self.rev_j.data_ptr(), self.rev_k.data_ptr(), self.B.data_ptr(), self._z.data_ptr()
-        send, recv = x.send.data_ptr(), x.recv.data_ptr()
+        send, recv, var = x.send.data_ptr(), x.recv.data_ptr(), self._var.data_ptr()
         seed = self.seed & (2 ** 64 - 1)
         n, m = self.n, self.m
         rk = self.rank
+        n0 = x.n_collectives
         for c in range(c0, c1):
             a, b = int(p.run[c, rk]), int(p.run[c, rk + 1])
-            rc = L.nngp_gibbs_w_color(mr + 16 * a, b - a, prep, n, m, self.sigma2, self.tau2, yres, nw, w, r, rev_j,
-                                      z, seed, self.iteration, send + 8 * int(p.send_off[c]), stream)
+            out = send + 8 * int(p.send_off[c])
+            if graph:
+                rc = L.nngp_gibbs_w_color_dev(mr + 16 * a, b - a, prep, n, m, var, yres, nw, w, r, rev_j, z, out,
+                                              stream)
+            else:
+                rc = L.nngp_gibbs_w_color(mr + 16 * a, b - a, prep, n, m, self.sigma2, self.tau2, yres, nw, w, r,
+                                          rev_j, z, seed, self.iteration, out, stream)
             if rc != 0:
                 _lib._check(rc, "nngp_gibbs_w_color")
             x.exchange(c)
@@ -255,6 +296,8 @@ class ShardedSeqNNGP(SeqNNGP):
                 rc = L.nngp_gibbs_w_apply(ap + 16 * a2, b2 - a2, recv, B, n, m, w, r, rev_j, rev_k, stream)
                 if rc != 0:
                     _lib._check(rc, "nngp_gibbs_w_apply")
+        if graph and torch.cuda.is_current_stream_capturing():
+            x.n_collectives = n0  # counted per replay instead
 
     # ------------------------------------------------------------------ results (gathered)
     @property

@@ -52,7 +52,8 @@ def main():
                  tau2=res["tau2"], phi=res["phi"],
                  meta=np.array(json.dumps({"world": world, "n_collectives": g._xchg.n_collectives,
                                            "halo": int(g._n_h), "apply": int(g._apply_rows.shape[0]),
-                                           "rows": [g.lo, g.hi], "n_accept": g.n_accept})))
+                                           "rows": [g.lo, g.hi], "n_accept": g.n_accept,
+                                           "graphs": len(g._graphs), "iterations": g.iteration})))
     dist.barrier()
     dist.destroy_process_group()
     print("GIBBS_SHARDED_OK", rank)

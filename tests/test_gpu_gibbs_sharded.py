@@ -2,7 +2,8 @@
 
 Fresh child processes (tests/gibbs_sharded_child.py) run the sharded chain; the parent runs
 the single-GPU ``SeqNNGP`` chain on the same data and seed:
-  * one rank over an RCCL ("nccl") group -- every exchange goes through the collective: the
+  * one rank over an RCCL ("nccl") group -- every exchange goes through the collective and the
+    colour loop replays from captured HIP graphs (sigma2 / tau2 read from device memory): the
     chain is SeqNNGP's bit for bit (w after a sweep and after 25 iterations, every scalar draw);
   * 2 and 3 ranks on the one GPU over gloo (the rehearsal of the N-GPU flow): one w sweep at
     fixed hyperparameters is bit-identical (each location's draw is its owner's arithmetic on
@@ -75,6 +76,7 @@ def test_one_rank_rccl_equals_single_chain(single, tmp_path):
     got = _run(1, "nccl", str(tmp_path / "r1.npz"))
     meta = json.loads(str(got["meta"]))
     assert meta["world"] == 1 and meta["n_collectives"] > 0
+    assert meta["graphs"] >= 1  # the colour loop replayed from captured HIP graphs (RCCL inside)
     assert np.array_equal(got["w_sweep"], single["w_sweep"])
     for k in ("beta", "sigma2", "tau2", "phi"):
         assert np.array_equal(got[k], single[k]), k
