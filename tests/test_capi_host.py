@@ -199,3 +199,30 @@ def test_blocks_entry_points_reject(lib):
     assert lib.nngp_joint_dist(P(256), 10, 4, P(256), 10, P(256), None, 10, 5, 0, P(256), None) == -4
     assert lib.nngp_joint_dist(P(256), 10, 2, P(256), 10, P(256), None, 11, 5, 0, P(256), None) == -1
 
+
+
+def test_sharded_gibbs_entries_reject(lib):
+    """The sharded-chain entries validate before any device call (no GPU here)."""
+    P = ctypes.c_void_p
+    prep = P(256)
+    # prepare_range: rows outside [0, n), null pointers, a short prep buffer
+    assert lib.nngp_gibbs_prepare_range(P(8), P(8), P(8), P(8), P(8), 10, 3, 5, 11, prep, 1 << 20, None) == -1
+    assert lib.nngp_gibbs_prepare_range(P(8), P(8), P(8), P(8), P(8), 10, 3, 6, 5, prep, 1 << 20, None) == -1
+    assert lib.nngp_gibbs_prepare_range(P(8), None, P(8), P(8), P(8), 10, 3, 0, 10, prep, 1 << 20, None) == -1
+    assert lib.nngp_gibbs_prepare_range(P(8), P(8), P(8), P(8), P(8), 10, 3, 0, 10, prep, 8, None) == -1
+    assert b"prep too small" in lib.nngp_last_error()
+    # one colour step: bad sizes, nulls, non-positive variances; zero members is a no-op
+    args = (P(16), 4, prep, 10, 3, 1.0, 0.5, P(8), None, P(8), P(8), P(8), None, 0, 0, None, None)
+    assert lib.nngp_gibbs_w_color(*args[:1], 11, *args[2:]) == -1
+    assert lib.nngp_gibbs_w_color(*args[:5], 0.0, *args[6:]) == -1
+    assert lib.nngp_gibbs_w_color(None, *args[1:]) == -1
+    assert lib.nngp_gibbs_w_color(*args[:1], 0, *args[2:]) == 0
+    # the device-scalar variant needs var and z
+    assert lib.nngp_gibbs_w_color_dev(P(16), 4, prep, 10, 3, None, P(8), None, P(8), P(8), P(8), P(8), None,
+                                      None) == -1
+    assert lib.nngp_gibbs_w_color_dev(P(16), 4, prep, 10, 3, P(8), P(8), None, P(8), P(8), P(8), None, None,
+                                      None) == -1
+    # replay: misaligned rows, nulls; zero rows is a no-op
+    assert lib.nngp_gibbs_w_apply(P(4), 3, P(8), P(8), 10, 3, P(8), P(8), P(8), P(8), None) == -1
+    assert lib.nngp_gibbs_w_apply(P(16), 3, None, P(8), 10, 3, P(8), P(8), P(8), P(8), None) == -1
+    assert lib.nngp_gibbs_w_apply(P(16), 0, None, None, 10, 3, None, None, None, None, None) == 0

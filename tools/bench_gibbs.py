@@ -28,6 +28,7 @@ ap.add_argument("--warmup", type=int, default=100)
 ap.add_argument("--single-chain", action="store_true")
 ap.add_argument("--force-group", action="store_true")
 ap.add_argument("--backend", default="nccl")
+ap.add_argument("--graphs", type=int, default=None, help="single chain: 1/0 forces the HIP-graph colour loop on/off")
 args = ap.parse_args()
 # several GPUs (torchrun): independent chains, one per GPU ("replicas only")
 world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -54,7 +55,8 @@ t0 = time.perf_counter()
 if args.single_chain:
     from pynngp_amd import ShardedSeqNNGP
 
-    g = ShardedSeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev)
+    g = ShardedSeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev,
+                       graphs=None if args.graphs is None else bool(args.graphs))
 else:
     g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
 torch.cuda.synchronize()
@@ -80,7 +82,7 @@ if rank == 0:
     if args.single_chain:
         extra = {"halo_rows": int(g._n_h), "replayed_rows": int(g._apply_rows.shape[0]),
                  "collectives_per_iter": g._xchg.n_collectives / max(1, g.iteration), "group": grouped,
-                 "backend": args.backend if grouped else None}
+                 "backend": args.backend if grouped else None, "graphs": len(g._graphs)}
     chains = 1 if args.single_chain else world
     what = "ONE chain sharded over the GPUs" if args.single_chain else "one chain per GPU"
     print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, {what}", **extra,
