@@ -212,6 +212,40 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
 #endif
 constexpr int kGroup = NNGP_GIBBS_GROUP;
 
+// Sum over the G lanes of an aligned group, the xor butterfly's value in every lane, bit for bit:
+// after the steps of distance 1 and 2 all lanes of a quad hold the same value, so a partner in the
+// other half of the 8- (16-) lane group may be taken by the DPP half-row (row) mirror, l ^ 7
+// (l ^ 15), instead of l ^ 4 (l ^ 8) -- the same two operands in the same order.  The quad steps and
+// the mirrors are DPP moves on the VALU; l ^ 16 is one ds_swizzle (bit mode) and l ^ 32 a
+// ds_bpermute: one LDS round trip instead of five.
+// (NNGP_GIBBS_DPP 0: the descending __shfl_xor butterfly, ds_bpermute per step -- the A/B baseline)
+#ifndef NNGP_GIBBS_DPP
+#define NNGP_GIBBS_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ double gdpp(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffll), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+template <int G>
+__device__ __forceinline__ double group_sum(double v) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group of 2^k <= 64 lanes");
+    if constexpr (G >= 2) v += gdpp<0xB1>(v);   // quad_perm [1,0,3,2]: l ^ 1
+    if constexpr (G >= 4) v += gdpp<0x4E>(v);   // quad_perm [2,3,0,1]: l ^ 2
+    if constexpr (G >= 8) v += gdpp<0x141>(v);  // row_half_mirror: l ^ 7
+    if constexpr (G >= 16) v += gdpp<0x140>(v); // row_mirror: l ^ 15
+    if constexpr (G >= 32) {                    // ds_swizzle bit mode, and 0x1f, xor 0x10: l ^ 16
+        const long long u = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_ds_swizzle((int)(u & 0xffffffffll), 0x401F);
+        const int hi = __builtin_amdgcn_ds_swizzle((int)(u >> 32), 0x401F);
+        v += __hiloint2double(hi, lo);
+    }
+    if constexpr (G >= 64) v += __shfl_xor(v, 32);
+    return v;
+}
+
 // Two passes, both streaming:
 //   entries: one thread per reverse entry e: Brev[e] = B[j, k], Grev[e] = Brev[e] / Ft[j]
 //            (coalesced rev_j / rev_k reads and Brev / Grev writes, B / Ft gathered from
@@ -416,7 +450,8 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
                                                      double* __restrict__ w, double* __restrict__ r,
                                                      const int32_t* __restrict__ rev_j,
                                                      const double* __restrict__ z, uint64_t seed, uint64_t sweep,
-                                                     double* __restrict__ w_out, const double* __restrict__ var) {
+                                                     double* __restrict__ w_out, const double* __restrict__ var,
+                                                     int64_t m_cap) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
@@ -424,27 +459,48 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
     const int4 mr = member_rows[live ? g : n_members - 1];
     const int64_t i = mr.x;
     const int32_t e0 = mr.y, e1 = live ? mr.z : mr.y;
-    // first kGroup children in registers (child index, B, r_j): the scatter below reuses
-    // them without reloading (no other member of this colour touches r_j); more children
-    // than lanes (rare) take the generic loops
-    const int32_t ef = e0 + l;
-    const bool has = ef < e1;
-    const int64_t jf = has ? (int64_t)rev_j[ef] : 0;
-    const double bf = has ? Brev[ef] : 0.0;
-    const double rf = has ? r[jf] : 0.0;
-    double acc = has ? Grev[ef] * rf : 0.0;
-    for (int32_t e = ef + kGroup; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
-#pragma unroll
-    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    // every load that depends only on the member row is issued at once, branch-free: the
+    // member's own operands and its first child's reverse entry in one memory round trip, then
+    // the child's r_j in a second (a guarded load per operand made the compiler wait for each
+    // before issuing the next).  r_i is safe to read early: no other member of the colour is a
+    // parent of i, so nothing else writes it during the step.
+    const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i], yi = yres[i];
+    const double hi = noise_w != nullptr ? noise_w[i] : 1.0;
+    const double zl = z != nullptr ? z[i] : 0.0;
     if (var != nullptr) {  // (sigma2, tau2) from device memory: a graph-captured step replays with new values
         is2 = 1.0 / var[0];
         it2 = 1.0 / var[1];
     }
-    const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i];
-    const double it2i = noise_w != nullptr ? it2 * noise_w[i] : it2;  // 1 / (tau2 / h_i)
+    // first kGroup children in registers (child index, B, r_j): the scatter below reuses
+    // them without reloading (no other member of this colour touches r_j); more children
+    // than lanes (rare) take the generic loops.  A lane without a child reads entry 0 (in the
+    // n*m-entry reverse arrays whenever m > 0) and r_i, and discards them.
+    const int32_t ef = e0 + l;
+    const bool has = ef < e1;
+    const int64_t es = has ? ef : 0;
+    int64_t jf = i;
+    double bf = 0.0, gf = 0.0;
+    if (m_cap > 0) {  // kernel argument: wave-uniform
+        const int32_t jr = rev_j[es];
+        bf = Brev[es];
+        gf = Grev[es];
+        jf = has ? (int64_t)jr : i;
+    }
+    const double rl = r[jf];
+    const double rf = has ? rl : 0.0;
+    bf = has ? bf : 0.0;
+    double acc = has ? gf * rf : 0.0;
+    for (int32_t e = ef + kGroup; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
+#if NNGP_GIBBS_DPP
+    acc = group_sum<kGroup>(acc);
+#else
+#pragma unroll
+    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+#endif
+    const double it2i = noise_w != nullptr ? it2 * hi : it2;  // 1 / (tau2 / h_i)
     const double prec = fma(iF + Pi, is2, it2i);
-    const double lin = fma(yres[i], it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
-    const double zi = z != nullptr ? z[i] : philox_normal(seed, (uint64_t)i, sweep);
+    const double lin = fma(yi, it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
+    const double zi = z != nullptr ? zl : philox_normal(seed, (uint64_t)i, sweep);
     const double sd = nngp_rsqrt(prec);
     const double wn = fma(zi, sd, lin / prec);
     const double dw = wn - wi;
@@ -471,7 +527,7 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
         const int64_t threads = (b - a) * kGroup;
         hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                            (const int4*)member_rows + a, b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2,
-                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr);
+                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr, n * (int64_t)m);
     }
     return hipGetLastError();
 }
@@ -485,7 +541,7 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
     const int64_t threads = n_members * kGroup;
     hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                        (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
-                       noise_w, w, r, rev_j, z, seed, sweep, w_out, var);
+                       noise_w, w, r, rev_j, z, seed, sweep, w_out, var, n * (int64_t)m);
     return hipGetLastError();
 }
 
