@@ -210,7 +210,17 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
 #ifndef NNGP_GIBBS_GROUP
 #define NNGP_GIBBS_GROUP 32
 #endif
+// ... each lane holding NNGP_GIBBS_PER children with their loads in flight together.  Fewer lanes
+// per member with more children each (fewer waves, no second round trip for the members with more
+// children than lanes) measured slower (round 3, profiles/r03s, ms per iteration at N = 1e6):
+// 32 x 1 0.799, 32 x 2 0.801, 16 x 2 0.859, 8 x 4 1.012 -- the steps want every gather in its own
+// lane (memory-level parallelism), not fewer waves.
+#ifndef NNGP_GIBBS_PER
+#define NNGP_GIBBS_PER 1
+#endif
 constexpr int kGroup = NNGP_GIBBS_GROUP;
+constexpr int kPer = NNGP_GIBBS_PER;
+constexpr int kSpan = kGroup * kPer;
 
 // Sum over the G lanes of an aligned group, the xor butterfly's value in every lane, bit for bit:
 // after the steps of distance 1 and 2 all lanes of a quad hold the same value, so a partner in the
@@ -471,26 +481,39 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
         is2 = 1.0 / var[0];
         it2 = 1.0 / var[1];
     }
-    // first kGroup children in registers (child index, B, r_j): the scatter below reuses
-    // them without reloading (no other member of this colour touches r_j); more children
-    // than lanes (rare) take the generic loops.  A lane without a child reads entry 0 (in the
-    // n*m-entry reverse arrays whenever m > 0) and r_i, and discards them.
-    const int32_t ef = e0 + l;
-    const bool has = ef < e1;
-    const int64_t es = has ? ef : 0;
-    int64_t jf = i;
-    double bf = 0.0, gf = 0.0;
-    if (m_cap > 0) {  // kernel argument: wave-uniform
-        const int32_t jr = rev_j[es];
-        bf = Brev[es];
-        gf = Grev[es];
-        jf = has ? (int64_t)jr : i;
+    // the first kSpan = kGroup * kPer children in registers (child index, B, r_j), kPer per lane
+    // (children l, l + kGroup, ...), their loads issued together: the scatter below reuses them
+    // without reloading (no other member of this colour touches r_j); more children (rare) take
+    // the generic loops.  A slot without a child reads entry 0 (in the n*m-entry reverse arrays
+    // whenever m > 0) and r_i, and discards them.
+    int64_t jf[kPer];
+    double bf[kPer], gf[kPer], rf[kPer];
+    bool has[kPer];
+#pragma unroll
+    for (int c = 0; c < kPer; ++c) {
+        const int32_t ef = e0 + l + c * kGroup;
+        has[c] = ef < e1;
+        const int64_t es = has[c] ? ef : 0;
+        jf[c] = i;
+        bf[c] = 0.0;
+        gf[c] = 0.0;
+        if (m_cap > 0) {  // kernel argument: wave-uniform
+            const int32_t jr = rev_j[es];
+            bf[c] = Brev[es];
+            gf[c] = Grev[es];
+            jf[c] = has[c] ? (int64_t)jr : i;
+        }
     }
-    const double rl = r[jf];
-    const double rf = has ? rl : 0.0;
-    bf = has ? bf : 0.0;
-    double acc = has ? gf * rf : 0.0;
-    for (int32_t e = ef + kGroup; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
+#pragma unroll
+    for (int c = 0; c < kPer; ++c) rf[c] = r[jf[c]];
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < kPer; ++c) {
+        rf[c] = has[c] ? rf[c] : 0.0;
+        bf[c] = has[c] ? bf[c] : 0.0;
+        acc = c == 0 ? (has[0] ? gf[0] * rf[0] : 0.0) : (has[c] ? fma(gf[c], rf[c], acc) : acc);
+    }
+    for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
 #if NNGP_GIBBS_DPP
     acc = group_sum<kGroup>(acc);
 #else
@@ -509,8 +532,10 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
         r[i] = ri + dw;
         if (w_out != nullptr) w_out[g] = wn;  // published to the other ranks of a sharded chain
     }
-    if (has) r[jf] = fma(-bf, dw, rf);
-    for (int32_t e = ef + kGroup; e < e1; e += kGroup) {
+#pragma unroll
+    for (int c = 0; c < kPer; ++c)
+        if (has[c]) r[jf[c]] = fma(-bf[c], dw, rf[c]);
+    for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) {
         const int64_t j = rev_j[e];
         r[j] = fma(-Brev[e], dw, r[j]);
     }

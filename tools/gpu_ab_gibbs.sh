@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/abg
+rm -rf gpurun_out/abg; mkdir -p gpurun_out/abg
 for rep in $(seq 1 ${REPS:-2}); do
   for v in $VARIANTS; do
     label=${v%%:*}; lib=${v#*:}
