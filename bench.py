@@ -333,7 +333,7 @@ def main():
     ap.add_argument("--no-order", action="store_true", help="visit rows in index order (no Z-order; natural layout)")
     ap.add_argument("--layout", default="storage", choices=["storage", "natural"],
                     help="storage: per-location arrays relabelled into Z-order storage (default); natural: input rows")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget in seconds of CPU work (a bounded sample; 0 = skip)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="testing only: every rank on cuda:0 with gloo collectives (the N-rank flow on one GPU)")
     ap.add_argument("--sweep-api", default="ops", choices=["ops", "ctypes"],
