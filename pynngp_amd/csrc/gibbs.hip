@@ -222,8 +222,9 @@ constexpr int kGroup = NNGP_GIBBS_GROUP;
 constexpr int kPer = NNGP_GIBBS_PER;
 constexpr int kSpan = kGroup * kPer;
 
-// Sum over the G lanes of an aligned group, the xor butterfly's value in every lane, bit for bit:
-// after the steps of distance 1 and 2 all lanes of a quad hold the same value, so a partner in the
+// Sum over the G lanes of an aligned group, in every lane the bits of the ASCENDING xor butterfly
+// (distances 1, 2, 4, ...; the round-2 kernel summed descending, so its sums differ in the last
+// bits): after the steps of distance 1 and 2 all lanes of a quad hold the same value, so a partner in the
 // other half of the 8- (16-) lane group may be taken by the DPP half-row (row) mirror, l ^ 7
 // (l ^ 15), instead of l ^ 4 (l ^ 8) -- the same two operands in the same order.  The quad steps and
 // the mirrors are DPP moves on the VALU; l ^ 16 is one ds_swizzle (bit mode) and l ^ 32 a
