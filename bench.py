@@ -205,22 +205,55 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     coords, X, y, _ = synth_gibbs_field(n, 5, sigma2, phi, tau2, beta, dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if single:
-        g = ShardedSeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
-                           seed=1, device=dev, collective=distributed)
-    else:
-        g = SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01,
-                    seed=1 + rank, device=dev)
+    # --chains-per-gpu C > 1 (replica mode only): C independent chains per GPU, each on its own HIP
+    # stream driven by its own host thread -- one chain leaves the GPU idle in its colour steps' launch
+    # floors and its host synchronisations (tools/bench_gibbs_streams.py)
+    cpg = 1 if single else max(1, args.chains_per_gpu)
+    streams = [torch.cuda.current_stream(dev)] if cpg == 1 else [torch.cuda.Stream(dev) for _ in range(cpg)]
+    chains = []
+    for k in range(cpg):
+        with torch.cuda.stream(streams[k]):
+            if single:
+                chains.append(ShardedSeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi,
+                                             phi_tuning=0.01, seed=1, device=dev, collective=distributed))
+            else:
+                chains.append(SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi,
+                                      phi_tuning=0.01, seed=1 + rank * cpg + k, device=dev))
+    g = chains[0]
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
-    for _ in range(args.warmup):
-        g.step()
+
+    def run_chains(iters):
+        if cpg == 1:
+            for _ in range(iters):
+                g.step()
+            return
+        import threading
+
+        errors = []
+
+        def one(k):
+            try:
+                with torch.cuda.stream(streams[k]):
+                    for _ in range(iters):
+                        chains[k].step()
+            except BaseException as e:  # re-raised below: a failed chain must fail the run
+                errors.append(e)
+
+        th = [threading.Thread(target=one, args=(k,)) for k in range(cpg)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errors:
+            raise errors[0]
+
+    run_chains(args.warmup)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        g.step()
+    run_chains(args.steps)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -258,18 +291,18 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
         bpl = bytes_per_location(m) + 8  # + the residual r written for the sampler
         rows = g.hi - g.lo if single else n
         achieved = bpl * rows / (sweep_ms * 1e-3)
-        chains = 1 if single else world
+        n_chains = 1 if single else world * cpg
         out = {
             "metric": "NNGP Gibbs sampler iterations/sec (BASELINE config 5: N=1M, m=15, 1,000 sweeps; " + (
                 "ONE chain sharded over the GPUs)" if single else "one chain per GPU)"),
-            "value": chains * args.steps / elapsed,
+            "value": n_chains * args.steps / elapsed,
             "unit": "chain-iterations/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_iter,
             "iterations_per_s_per_chain": args.steps / elapsed,
-            "locations_per_s": chains * n * args.steps / elapsed,
+            "locations_per_s": n_chains * n * args.steps / elapsed,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -280,9 +313,10 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                 "workload": f"BASELINE config 5: {'ShardedSeqNNGP' if single else 'SeqNNGP'} Gibbs sampler, "
                             f"N={n} per chain, m={m}, exponential, "
                             f"{args.steps} timed iterations after {args.warmup} warm-up",
-                "n_per_gpu": args.n, "m": m, "kind": "exponential", "chains": chains,
+                "n_per_gpu": args.n, "m": m, "kind": "exponential", "chains": n_chains, "chains_per_gpu": cpg,
                 "parallelism": (f"one chain over {world} GPU(s): storage-row shards, one all-gather per colour"
-                                if single else f"replicas x{world} (one independent chain per GPU)"),
+                                if single else f"replicas x{world * cpg} ({cpg} independent chain(s) per GPU"
+                                + ("" if cpg == 1 else ", each on its own stream") + ")"),
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
@@ -345,6 +379,8 @@ def main():
     ap.add_argument("--force-collective", action="store_true",
                     help="exchange the partials through torch.distributed even on one rank (a one-rank RCCL group "
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
+    ap.add_argument("--chains-per-gpu", type=int, default=1,
+                    help="config 5 replica mode: independent chains per GPU, one stream and host thread each")
     ap.add_argument("--single-chain", action="store_true",
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")

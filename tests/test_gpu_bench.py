@@ -56,3 +56,9 @@ def test_bench_config5_contract(dev):
     assert d["unit"] == "chain-iterations/s" and d["config"]["chains"] == 1
     b = d["breakdown"]
     assert b["n_colors"] > 0 and b["bf_sweep_ms"] > 0 and b["w_sweep_ms"] > 0  # (no timing bounds: a tiny N)
+
+
+def test_bench_config5_two_chains_per_gpu(dev):
+    d = _run("--config", "5", "--steps", "5", "--warmup", "2", "--n", "20000", "--cpu-seconds", "0",
+             "--chains-per-gpu", "2")
+    assert d["steps"] == 5 and d["value"] > 0 and d["config"]["chains"] == 2 and d["config"]["chains_per_gpu"] == 2
