@@ -14,6 +14,8 @@ separately (``neighbor_build_s``).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py --config {2,4,5}              # the other BASELINE presets (5: the Gibbs sampler;
+                                                   # --chains-per-gpu C, --single-chain)
 """
 import argparse
 import json
