@@ -64,8 +64,16 @@ int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim);
 #define NNGP_MAX_M 63
 #define NNGP_MAX_DIM 3
 
-/* Library version string, e.g. "pynngp_amd 0.1.0 gfx950". */
+/* Library version string, e.g. "pynngp_amd 0.2.0 gfx950". */
 const char *nngp_version(void);
+
+/* ABI revision of this header (NNGP_ABI_VERSION), for a caller built against an older one to
+ * refuse a library whose signatures moved.  Revision 2 (library 0.2.0) changed, relative to 1
+ * (0.1.0): nngp_bf_finalize takes workspace_bytes as its 2nd argument; nngp_gibbs_w_sweep reads
+ * (n, 4) member rows (nngp_gibbs_member_rows) and lost its `off` argument; nngp_bf_sweep /
+ * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32. */
+#define NNGP_ABI_VERSION 2
+int32_t nngp_abi_version(void);
 
 /* Message for the last error returned on the calling thread. */
 const char *nngp_last_error(void);
@@ -175,8 +183,10 @@ int nngp_bf_cross(const double *ref, int64_t n_ref, int32_t dim, const double *q
 
 /* ---------------------------------------------------------------------------
  * A covariance of the caller's own (the reference's `cov` is an arbitrary plug-in,
- * pyNNGP/nngp.py:6,12; SURVEY.md 8(b) asks for callables): any isotropic function of
- * distance, evaluated by the caller on the GPU, drives the same fused sweep.
+ * pyNNGP/nngp.py:6,12, called on coordinate rows at :82,:96; SURVEY.md 8(b) asks for callables):
+ * the caller evaluates its function on every joint block -- an isotropic function of
+ * nngp_joint_dist's distances, or any cov(a, b) on the blocks' gathered coordinates -- and the
+ * blocks drive the same fused sweep.
  * nngp_joint_dist: for nbr row t (location i = i0 + (order ? order[t] : t); joint rows
  *   a = 0..m-1 the neighbour slots, row m the location, from qcoords) the packed lower
  *   triangle of the joint block's distances, entry (a, b), b <= a, at
@@ -187,7 +197,8 @@ int nngp_bf_cross(const double *ref, int64_t n_ref, int32_t dim, const double *q
  *   as nngp_bf_sweep / nngp_bf_cross: values (n_points,) of the neighbours, qvalues (n_locs,)
  *   of the locations, may be NULL) with the joint blocks' covariances read from `cov` in that
  *   layout -- cov[e] = C(dist[e]) plus the nugget on the diagonal entries; entries of slots
- *   without a point are ignored (decoupled exactly).  1 <= m <= 24; workspace
+ *   without a point are ignored (decoupled exactly).  1 <= m <= 32 (the two-lane blocked
+ *   kernel up to 24, the four-lane kernel for 25..32); workspace
  *   nngp_bf_sweep_blocks_workspace_bytes(n_rows), 256-B aligned; partials required.
  * ------------------------------------------------------------------------- */
 /* out[k] = u^nu K_nu(u) / (2^(nu-1) Gamma(nu)) for n arguments u >= 0 (the Matern correlation

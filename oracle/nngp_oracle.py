@@ -229,6 +229,47 @@ def bf_sweep(coords, nbr, kind, theta, values=None, i0=0):
     return B, F, partials
 
 
+def bf_sweep_callable(coords, nbr, cov, values=None, i0=0, qcoords=None, qvalues=None):
+    """The same algebra with the reference's plug-in ``cov(a, b)`` as it is called there: on the
+    neighbours' coordinate rows, ``C_N = cov(X_N, X_N)`` (``_CNs``, ``nngp.py:78-82``, with rows
+    where the reference passes indices), ``c = cov(x_i, X_N)`` (``_Ccross``, ``nngp.py:84-86``) and
+    ``C_ii = cov(x_i, x_i)`` (``_Cs``, ``nngp.py:92-96``), then one dense solve per location
+    (``np.linalg.solve``, not a Cholesky: an independent route to ``_Bsi`` / ``_Fsi``,
+    ``nngp.py:73-76,88-90``): B_i = C_N^{-1} c, F_i = C_ii - c^T B_i, r_i = v_i - B_i v_N(i).
+    ``qcoords`` given: the locations are those points (prediction; ``qvalues`` their values).
+    Returns ``(B (n, m) padded with 0, F (n,), partials [sum log F, sum r^2/F])``.  Plain
+    per-location Python: for the small parity cases only."""
+    coords = np.ascontiguousarray(coords, dtype=np.float64)
+    nbr = np.asarray(nbr)
+    q = coords if qcoords is None else np.ascontiguousarray(qcoords, dtype=np.float64)
+    qv = values if qcoords is None else qvalues
+    n, m = nbr.shape
+    B = np.zeros((n, m))
+    F = np.empty(n)
+    resid = np.zeros(n)
+    for r in range(n):
+        i = i0 + r
+        ok = (nbr[r] >= 0) & (nbr[r] < coords.shape[0])
+        idx = nbr[r][ok].astype(np.int64)
+        xi = q[i][None, :]
+        Cii = float(np.asarray(cov(xi, xi)).reshape(-1)[0])
+        if idx.size == 0:
+            F[r] = Cii
+            b = np.zeros(0)
+        else:
+            xs = coords[idx]
+            CN = np.asarray(cov(xs, xs), dtype=np.float64).reshape(idx.size, idx.size)
+            c = np.asarray(cov(xi, xs), dtype=np.float64).reshape(idx.size)
+            b = np.linalg.solve(CN, c)
+            B[r, ok] = b
+            F[r] = Cii - c @ b
+        if values is not None:
+            vi = 0.0 if qv is None else float(np.asarray(qv)[i])
+            resid[r] = vi - (b @ np.asarray(values)[idx] if idx.size else 0.0)
+    partials = np.array([np.log(F).sum(), (resid * resid / F).sum()])
+    return B, F, partials
+
+
 def loglik_from_partials(partials, n):
     return -0.5 * (n * LOG_2PI + partials[0] + partials[1])
 

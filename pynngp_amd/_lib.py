@@ -18,6 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NNGP_LIB") or os.path.join(_HERE, "_build", "libnngp_hip.so")
 SYMBOLS = (
     "nngp_version",
+    "nngp_abi_version",
     "nngp_last_error",
     "nngp_knn_workspace_bytes",
     "nngp_knn_prior",
@@ -60,6 +61,8 @@ MATERN_NU_MAX = 50.0
 ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
+ABI_VERSION = 2  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
+BLOCKS_MAX_M = 32  # nngp_bf_sweep_blocks: 1 <= m <= 32
 
 
 class NNGPExtensionError(RuntimeError):
@@ -82,6 +85,10 @@ def load() -> ctypes.CDLL:
     lib = ctypes.CDLL(LIB_PATH)
     P, I32, I64, D, SZ = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
     lib.nngp_version.restype = ctypes.c_char_p
+    lib.nngp_abi_version.restype = I32
+    if lib.nngp_abi_version() != ABI_VERSION:
+        raise NNGPExtensionError(f"{LIB_PATH} has C ABI revision {lib.nngp_abi_version()}, this binding needs "
+                                 f"{ABI_VERSION}: rebuild the library")
     lib.nngp_last_error.restype = ctypes.c_char_p
     lib.nngp_knn_workspace_bytes.argtypes = [I64, I32, I32]
     lib.nngp_knn_workspace_bytes.restype = SZ
@@ -489,7 +496,9 @@ def bf_sweep_blocks(cov: torch.Tensor, nbr: torch.Tensor, n_points: int, i0: int
     of the distances, the nugget on the diagonal entries).  ``values`` (n_points,) at the
     neighbours and ``qvalues`` (n_locs,) at the locations (pass ``values`` again for the S = T
     sweep; None: 0, so R = -B v_N, minus the kriging mean).
-    Returns ``(B, F, partials)`` as :func:`bf_sweep`.  1 <= m <= 24."""
+    Returns ``(B, F, partials)`` as :func:`bf_sweep`.  1 <= m <= 32 (the two-lane kernel up to 24,
+    the four-lane kernel above).  The C ABI takes raw pointers, so every length is checked here:
+    ``values`` (n_points,), ``qvalues`` (n_locs,), ``order`` int32 (rows,)."""
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
         raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
     nbr = nbr.contiguous()
@@ -499,13 +508,17 @@ def bf_sweep_blocks(cov: torch.Tensor, nbr: torch.Tensor, n_points: int, i0: int
     if cov.dtype != torch.float64 or tuple(cov.shape) != (ne, rows):
         raise ValueError(f"cov must be float64 ({ne}, {rows}) (joint_dist's layout), got {cov.dtype} {tuple(cov.shape)}")
     cov = cov.contiguous()
-    for name, v in (("values", values), ("qvalues", qvalues)):
-        if v is not None and (v.dtype != torch.float64 or v.dim() != 1):
-            raise ValueError(f"{name} must be float64 1-D")
+    n_locs = int(n_points if n_locs is None else n_locs)
+    for name, v, n in (("values", values, n_points), ("qvalues", qvalues, n_locs)):
+        if v is not None and (v.dtype != torch.float64 or tuple(v.shape) != (int(n),)):
+            raise ValueError(f"{name} must be float64 of shape ({int(n)},), got {v.dtype} {tuple(v.shape)}")
+    if order is not None:
+        if order.dtype != torch.int32 or tuple(order.shape) != (rows,):
+            raise ValueError(f"order must be int32 of shape ({rows},), got {order.dtype} {tuple(order.shape)}")
+        order = order.contiguous()
     values = None if values is None else values.contiguous()
     qvalues = None if qvalues is None else qvalues.contiguous()
     dev = _require_gpu(cov, nbr, values, qvalues, order, R)
-    n_locs = int(n_points if n_locs is None else n_locs)
     B = torch.empty((rows, m), dtype=torch.float64, device=dev) if want_bf else None
     F = torch.empty((rows,), dtype=torch.float64, device=dev) if want_bf else None
     _check_out(R, "R", (rows,), dev)

@@ -64,21 +64,27 @@ __device__ __forceinline__ double grp_sum(double v) {
 
 // D = 2: 2-D ordinates (one 16-byte load per point); D = 0: runtime dimension 1..3 held as three
 // coordinates, with KIND = NNGP_KIND_GENERIC the runtime-kind covariance (nngp_math.h) -- the
-// m = 25..32 kernels for every kind and dimension
+// m = 25..32 kernels for every kind and dimension.  KIND = NNGP_KIND_BLOCKS: the joint block's
+// covariances are read from cblk (nngp_bf_sweep_blocks at m = 25..32; the layout bf_pairb.h's
+// blocks kernel reads: entry (a, b), b <= a <= M, of nbr row t at cblk[(a (a+1)/2 + b) n_rows + t]),
+// no coordinates are gathered, and slots without a point decouple exactly (0 off the diagonal, 1 on
+// it) whatever the caller stored there.
 template <int M, int KIND, int P, int D = 2>
 __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0,
                                                 const CovParams Pc, const double* __restrict__ values, const double* __restrict__ qcoords, const double* __restrict__ qvalues,
                                                 double* __restrict__ Bout, double* __restrict__ Fout, double* __restrict__ Rout,
-                                                double* __restrict__ bpart, int dim) {
+                                                double* __restrict__ bpart, int dim, const double* __restrict__ cblk) {
     static_assert(D == 0 || D == 2, "bf_group: 2-D or runtime dimension");
+    constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
+    static_assert(!CM || M <= 32, "the validity mask holds one bit per neighbour slot");
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
     constexpr int DA = point_arity<D>();
     const int ds = D == 0 ? dim : 2;
     __shared__ double etab[NNGP_EXP_TAB_N];
-    nngp_exp_table_load(etab, Pc.sigma2);
+    if constexpr (!CM) nngp_exp_table_load(etab, Pc.sigma2);
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
     const int64_t tid = blk * blockDim.x + threadIdx.x;
     const int q = (int)(threadIdx.x % P);
@@ -112,14 +118,48 @@ __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coord
         const double* pc = self ? qcoords + i * ds : (in_range ? coords + (int64_t)j * ds : far_point<DA>(a));
         const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                 : ((values != nullptr && in_range) ? values + j : kZeroValue);
-        if constexpr (D == 0) load_point_rt(pc, dim, o[s]);
-        else load_point<D>(pc, o[s]);
+        if constexpr (CM) {
+        } else if constexpr (D == 0) {
+            load_point_rt(pc, dim, o[s]);
+        } else {
+            load_point<D>(pc, o[s]);
+        }
         z[s] = *pv;
     }
 
     // ---- joint block rows: R[s][b], b < min(P*s + P, NR)
     double R[S][NR];
-    {
+    if constexpr (CM) {
+        // vm: bit a set when neighbour slot a < M holds a point (this lane's slots, then the group's
+        // by two DPP ORs); row M (the location) always does, padding rows a > M never
+        uint32_t vm = 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int a = P * s + q;
+            vm |= (a < M && oval[s]) ? (1u << (a & 31)) : 0u;
+        }
+        if constexpr (P > 1) vm |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vm, 0xB1, 0xf, 0xf, true);
+        if constexpr (P > 2) vm |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vm, 0x4E, 0xf, 0xf, true);
+        auto has = [&](int a) -> bool { return a == M || (a < M && ((vm >> (a & 31)) & 1u)); };
+        const double* cb = cblk + rl;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int a = P * s + q;
+            const bool ha = has(a);
+#pragma unroll
+            for (int b = 0; b < NR; ++b) {
+                if (b >= P * s + P) continue;  // beyond this local row's width
+                if (b > a) {                   // (diagonal block, upper part)
+                    R[s][b] = 0.0;
+                    continue;
+                }
+                const bool ok = ha && has(b);
+                const int64_t e = ok ? (int64_t)((a * (a + 1)) / 2 + b) : 0;  // in range either way
+                const double v = cb[e * n_rows];
+                R[s][b] = ok ? v : (b == a ? 1.0 : 0.0);
+            }
+        }
+    } else {
         double X[NR][DA];
 #pragma unroll
         for (int b = 0; b < NR; ++b)
@@ -224,7 +264,8 @@ template <int M, int KIND, int P, int D = 2>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
     hipLaunchKernelGGL((bf_group<M, KIND, P, D>), dim3((unsigned)blocks), dim3(256), 0, s, a.coords, a.n_points, a.nbr,
-                       a.order, a.n_rows, a.i0, Pc, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart, a.dim);
+                       a.order, a.n_rows, a.i0, Pc, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart, a.dim,
+                       a.cblk);
 }
 
 // one (M, P): the 2-D exponential / Matern-3/2 kernels, and one runtime-kind, runtime-dimension
@@ -238,6 +279,14 @@ static bool launch_group_if(const BfArgs& a, const CovParams& Pc, hipStream_t s)
         launch_group_mkp<M, 0, P>(a, Pc, s);
     else
         launch_group_mkp<M, NNGP_KIND_GENERIC, P, 0>(a, Pc, s);
+    return true;
+}
+
+// covariance blocks from memory at m = 25..32 (nngp_bf_sweep_blocks; bf_quad_blocks.hip)
+template <int M>
+static bool launch_group_blocks_if(const BfArgs& a, hipStream_t s) {
+    if (a.m != M) return false;
+    launch_group_mkp<M, NNGP_KIND_BLOCKS, 4>(a, nngp_cov_params(0, 1.0, 1.0, 0.0), s);
     return true;
 }
 

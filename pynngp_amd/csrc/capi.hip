@@ -49,7 +49,9 @@ int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_coun
 
 extern "C" {
 
-const char* nngp_version(void) { return "pynngp_amd 0.1.0 gfx950"; }
+const char* nngp_version(void) { return "pynngp_amd 0.2.0 gfx950"; }
+
+int32_t nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 
 const char* nngp_last_error(void) { return g_err; }
 
@@ -173,7 +175,12 @@ int nngp_matern_eval(const double* u, int64_t n, double nu, double* out, void* s
 }
 
 size_t nngp_bf_sweep_blocks_workspace_bytes(int64_t n_rows) {
-    return n_rows < 0 ? 0 : nngp::bf_pairb_workspace_bytes(n_rows);
+    // enough for either kernel: bf_pairb's tile records (m <= 24) or the four-lane kernel's block
+    // records (m = 25..32)
+    if (n_rows < 0) return 0;
+    const size_t pb = nngp::bf_pairb_workspace_bytes(n_rows);
+    const size_t gb = align256((size_t)nngp::bf_group_blocks(n_rows, 4) * 4 * sizeof(double));
+    return pb > gb ? pb : gb;
 }
 
 int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* order, int64_t n_points, int64_t n_rows,
@@ -182,8 +189,9 @@ int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* o
                          void* stream) {
     if (cov == nullptr || workspace == nullptr || partials == nullptr || (n_rows > 0 && nbr == nullptr))
         return fail(NNGP_EINVAL, "cov, nbr, partials and workspace must be non-null");
-    if (!nngp::bf_pairb_blocks_supported(m))
-        return fail(NNGP_EUNSUP, "covariance-block sweeps need 1 <= m <= 24 (m=%d)", m);
+    const bool group = nngp::bf_group_blocks_supported(m);
+    if (!nngp::bf_pairb_blocks_supported(m) && !group)
+        return fail(NNGP_EUNSUP, "covariance-block sweeps need 1 <= m <= 32 (m=%d)", m);
     if (n_points < 1 || n_rows < 0 || i0 < 0 || i0 + n_rows > n_locs)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld)", (long long)i0, (long long)(i0 + n_rows),
                     (long long)n_locs);
@@ -201,9 +209,12 @@ int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* o
     }
     nngp::BfArgs args{nullptr, n_points, nbr, n_rows, i0, m, NNGP_KIND_BLOCKS, 2, 1.0, 1.0, 0.0, 0.0, order, values,
                       nullptr, qvalues, B, F, R, partials, (double*)workspace, cov};
-    if (!nngp::bf_pairb_blocks_launch(args, s)) return fail(NNGP_EUNSUP, "no covariance-block kernel for m=%d", m);
+    if (!(group ? nngp::bf_group_blocks_launch(args, s) : nngp::bf_pairb_blocks_launch(args, s)))
+        return fail(NNGP_EUNSUP, "no covariance-block kernel for m=%d", m);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = nngp::bf_finalize_pairb_launch(workspace, n_rows, partials, s);
+    if (e == hipSuccess)
+        e = group ? nngp::bf_finalize_launch((const double*)workspace, nngp::bf_group_blocks(n_rows, 4), partials, s)
+                  : nngp::bf_finalize_pairb_launch(workspace, n_rows, partials, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep_blocks launch");
     return NNGP_OK;
 }

@@ -112,6 +112,8 @@ bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
 bool bf_pairb_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS (bf_pairb.h)
 bool bf_pairb_blocks_supported(int m);
+bool bf_group_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS at m = 25..32 (bf_group.h)
+bool bf_group_blocks_supported(int m);
 hipError_t matern_eval_launch(const double* u, int64_t n, double nu, double* out, hipStream_t s);
 hipError_t joint_dist_launch(const double* coords, int64_t n_points, int dim, const double* qcoords,
                              const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int64_t i0, double* dist,

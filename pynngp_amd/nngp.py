@@ -8,11 +8,13 @@ neighbour sets, the B/F algebra and the log-likelihood run on the MI355X through
 and ``loglik()``, the sweep the reference's ``oneSample`` (nngp.py:98-101) needs.
 
 Differences from the reference, all deliberate:
-* ``cov`` is a :class:`Covariance` (kind + theta) for the device path; a plain
-  Python callable is still accepted and used by ``_CNs/_Ccross/_Cs`` with the
-  coordinate convention (the reference passes index arrays at nngp.py:82, a
-  bug), but ``_Bsi/_Fsi/loglik`` need a :class:`Covariance` because the kernel
-  fuses the covariance.  ``cov=None`` (the reference test) builds neighbour sets only.
+* ``cov`` is a :class:`Covariance` (kind + theta: the covariance fused into the kernel, the
+  fast path), an :class:`IsotropicCovariance` (a torch function of distance), or -- as in the
+  reference -- any Python callable ``cov(a, b)`` on coordinate rows (the reference passes index
+  arrays at nngp.py:82, a bug; here the rows).  A callable drives ``_CNs/_Ccross/_Cs`` directly
+  and ``_Bsi/_Fsi/compute_BF/loglik/predict`` through :class:`CallableCovariance` (its joint
+  blocks evaluated, then factorised on the GPU by the covariance-block kernels, 1 <= m <= 32).
+  ``cov=None`` (the reference test) builds neighbour sets only.
 * exact distance ties are ordered by lower index (the reference's is arbitrary).
 * tuple ``refType`` values work as the reference's comments describe
   (nngp.py:23-27, with the same ``np.random`` calls as nngp.py:36-40, so a seeded
@@ -132,8 +134,18 @@ class IsotropicCovariance:
 
     @property
     def sigma2(self) -> float:
-        """C(0) = fn(0)."""
-        return float(self.fn(torch.zeros(1, dtype=torch.float64)).item())
+        """C(0) = fn(0), evaluated on the GPU when there is one (``fn`` may be a GPU-only function,
+        e.g. one built on ``_lib.matern``)."""
+        return self.variance("cuda" if torch.cuda.is_available() else "cpu")
+
+    def variance(self, device) -> float:
+        """C(0) = fn(0) evaluated on ``device``."""
+        return float(self.fn(torch.zeros(1, dtype=torch.float64, device=device)).item())
+
+    def marginal(self, points: torch.Tensor) -> torch.Tensor:
+        """C(x, x) + tau2 at every point (the m = 0 prediction variance)."""
+        return torch.full((points.shape[0],), self.variance(points.device) + self.tau2, dtype=torch.float64,
+                          device=points.device)
 
     def blocks(self, dist: torch.Tensor, m: int) -> torch.Tensor:
         """Covariance blocks for :func:`_lib.bf_sweep_blocks`: fn over the distances, tau2 on the
@@ -158,24 +170,169 @@ class IsotropicCovariance:
         return c.cpu().numpy() if to_np else c
 
 
-CovLike = Union[Covariance, IsotropicCovariance, Callable, None]
+class CallableCovariance:
+    """The reference's ``cov`` plug-in as it stands (``pyNNGP/nngp.py:6,12``): any callable
+    ``fn(a, b)`` that maps two sets of coordinate rows (k_a, d) and (k_b, d) to their
+    cross-covariance matrix (k_a, k_b) -- the call ``_CNs`` makes on the neighbours' rows
+    (``nngp.py:82``) and ``_Cs`` on a location's row (``nngp.py:96``).  No isotropy or other
+    structure is assumed (e.g. an anisotropic exponential exp(-sqrt((a-b)^T A (a-b)))).
+
+    It drives the device sweep through the covariance-block kernels: for every location the joint
+    block ``fn(X, X)`` of X = [its neighbours' rows; its own row] is evaluated, packed into
+    ``_lib.bf_sweep_blocks``'s layout (lower triangle, entry-major) and factorised on the GPU
+    (``nngp_bf_sweep_blocks``: B, F, residuals and the log-likelihood partials; 1 <= m <= 32).
+    Evaluation, chosen once per object by probing ``fn`` on a few rows against one call per row:
+      * ``"torch"``: ``fn`` broadcasts over a leading batch dimension of torch tensors on the GPU --
+        one call per chunk of rows with X of shape (rows, m+1, d), on the device;
+      * ``"numpy"``: the same with numpy arrays (host evaluation of the user's function, one call
+        per chunk; the blocks then go to the GPU);
+      * ``"loop"``: one call per location with the (m+1, d) numpy rows the reference passes.
+    ``batch`` forces a mode.  The covariance values are the caller's code; everything after them
+    (the factorisation, B, F, the log-likelihood) runs on the GPU, with no CPU path.
+    ``tau2`` is an optional nugget added to the diagonal (0: ``fn``'s own values are C)."""
+
+    kind = "custom"
+    MODES = ("torch", "numpy", "loop", "loop_torch")
+
+    def __init__(self, fn: Callable, tau2: float = 0.0, batch: Optional[str] = None, chunk_bytes: int = 1 << 28):
+        if not callable(fn):
+            raise TypeError("cov must be callable as cov(a, b) on coordinate rows")
+        if not tau2 >= 0:
+            raise ValueError("need tau2 >= 0")
+        if batch is not None and batch not in self.MODES:
+            raise ValueError(f"batch must be one of {self.MODES} or None")
+        self.fn, self.tau2, self.batch, self.chunk_bytes = fn, float(tau2), batch, int(chunk_bytes)
+        self.mode = batch
+
+    def __call__(self, a, b):
+        return self.fn(a, b)
+
+    # -- evaluation modes --------------------------------------------------------
+    def _eval(self, X: torch.Tensor, mode: str) -> torch.Tensor:
+        """fn's joint blocks (r, k, k) on X's device for X (r, k, d)."""
+        if mode == "torch":
+            C = self.fn(X, X)
+            if not isinstance(C, torch.Tensor):
+                raise TypeError("not a torch tensor")
+            return C.to(device=X.device, dtype=torch.float64)
+        Xh = X.detach().cpu().numpy()
+        if mode == "numpy":
+            C = np.asarray(self.fn(Xh, Xh), dtype=np.float64)
+        elif mode == "loop":
+            C = np.stack([np.asarray(self.fn(x, x), dtype=np.float64).reshape(x.shape[0], x.shape[0]) for x in Xh]) \
+                if Xh.shape[0] else np.zeros((0, X.shape[1], X.shape[1]))
+        else:  # loop_torch: one call per location with torch rows on the device
+            return torch.stack([torch.as_tensor(self.fn(x, x), dtype=torch.float64, device=X.device).reshape(
+                x.shape[0], x.shape[0]) for x in X]) if X.shape[0] else X.new_zeros((0, X.shape[1], X.shape[1]))
+        return torch.from_numpy(np.ascontiguousarray(C)).to(X.device)
+
+    def resolve_mode(self, X: torch.Tensor) -> str:
+        """Pick (once) the fastest evaluation that reproduces one call per location on sample rows X
+        (r, k, d): relative 1e-13 (a batched expression may round in a different order)."""
+        if self.mode is not None:
+            return self.mode
+        ref, ref_mode = None, None
+        for lm in ("loop", "loop_torch"):
+            try:
+                ref = self._eval(X, lm).cpu().numpy()
+                ref_mode = lm
+                break
+            except Exception:  # noqa: BLE001 -- the plug-in decides what it accepts
+                continue
+        if ref is None:
+            raise TypeError("cov(a, b) failed on the joint blocks' coordinate rows (numpy and torch (k, d) inputs)")
+        k = X.shape[1]
+        if ref.shape != (X.shape[0], k, k) or not np.all(np.isfinite(ref)):
+            raise ValueError(f"cov(a, b) must return a finite ({k}, {k}) matrix for two ({k}, d) row sets")
+        scale = float(np.max(np.abs(ref))) if ref.size else 1.0
+        for bm in ("torch", "numpy"):
+            try:
+                C = self._eval(X, bm)
+            except Exception:  # noqa: BLE001
+                continue
+            if tuple(C.shape) == ref.shape and np.allclose(C.cpu().numpy(), ref, rtol=1e-13, atol=1e-15 * scale):
+                self.mode = bm
+                return bm
+        self.mode = ref_mode
+        return ref_mode
+
+    def blocks(self, coords: torch.Tensor, nbr: torch.Tensor, i0: int = 0, qcoords: Optional[torch.Tensor] = None,
+               order: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Joint blocks in :func:`_lib.bf_sweep_blocks`'s layout ((m+1)(m+2)/2, rows): fn over
+        [neighbour rows; the location's row] for every nbr row (a slot without a point repeats the
+        location's row -- the kernel ignores its entries), tau2 on the diagonal entries."""
+        m = nbr.shape[1]
+        rows = nbr.shape[0]
+        dev = nbr.device
+        ne = (m + 1) * (m + 2) // 2
+        out = torch.empty((ne, rows), dtype=torch.float64, device=dev)
+        if rows == 0:
+            return out
+        a = torch.arange(m + 1, device=dev)
+        ta = torch.repeat_interleave(a, a + 1)  # entry e = a (a+1)/2 + b: rows a, then b = 0..a
+        tb = torch.cat([torch.arange(int(k) + 1, device=dev) for k in range(m + 1)])
+        per_row = (m + 1) * (m + 1) * 8 * 3 + (m + 1) * coords.shape[1] * 8
+        chunk = max(1, min(rows, self.chunk_bytes // per_row))
+        mode = self.resolve_mode(joint_points(coords, nbr[:min(rows, 4)], i0, qcoords, None if order is None else
+                                              order[:min(rows, 4)]))
+        if mode.startswith("loop"):
+            chunk = min(chunk, 4096)
+        for r0 in range(0, rows, chunk):
+            r1 = min(rows, r0 + chunk)
+            X = joint_points(coords, nbr[r0:r1], i0, qcoords, None if order is None else order[r0:r1])
+            C = self._eval(X, mode)
+            if tuple(C.shape) != (r1 - r0, m + 1, m + 1):
+                raise ValueError(f"cov(a, b) returned {tuple(C.shape)} for {r1 - r0} joint blocks of {m + 1} rows")
+            out[:, r0:r1] = C[:, ta, tb].t()
+        if self.tau2 > 0:
+            out[_lib.joint_diagonal(m).to(dev)] += self.tau2
+        return out
+
+    def marginal(self, points: torch.Tensor) -> torch.Tensor:
+        """C(x, x) + tau2 at every point (the m = 0 prediction variance): fn on each row alone."""
+        X = points[:, None, :]
+        return self._eval(X, self.resolve_mode(X[:4]))[:, 0, 0] + self.tau2
+
+
+def joint_points(coords: torch.Tensor, nbr: torch.Tensor, i0: int = 0, qcoords: Optional[torch.Tensor] = None,
+                 order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Coordinates of every joint block, (rows, m+1, d): slots 0..m-1 the neighbours ``coords[nbr]``
+    (a slot without a point -- index -1 or out of range -- repeats the location's row), slot m the
+    location ``qcoords[i0 + (order[t] if order else t)]`` (``qcoords`` defaults to ``coords``)."""
+    q = coords if qcoords is None else qcoords
+    rows = nbr.shape[0]
+    loc = (torch.arange(rows, device=nbr.device) if order is None else order.long()) + int(i0)
+    xi = q[loc]
+    idx = nbr.long()
+    ok = (idx >= 0) & (idx < coords.shape[0])
+    xn = coords[torch.where(ok, idx, torch.zeros_like(idx))]
+    xn = torch.where(ok[..., None], xn, xi[:, None, :])
+    return torch.cat([xn, xi[:, None, :]], dim=1)
+
+
+CovLike = Union[Covariance, IsotropicCovariance, CallableCovariance, Callable, None]
 
 
 def _sweep_any(cv, coords, nbr, i0=0, values=None, want_bf=True, algo="auto", order=None, R=None, qcoords=None,
-               qvalues=None):
-    """One fused sweep for either covariance form: a built-in kind (nngp_bf_sweep / nngp_bf_cross)
-    or an :class:`IsotropicCovariance` (joint distances -> fn -> nngp_bf_sweep_blocks).  ``qcoords``
+               qvalues=None, blocks=None):
+    """One fused sweep for any covariance form: a built-in kind (nngp_bf_sweep / nngp_bf_cross),
+    an :class:`IsotropicCovariance` (joint distances -> fn -> nngp_bf_sweep_blocks) or a
+    :class:`CallableCovariance` (fn(a, b) on the joint blocks' rows -> nngp_bf_sweep_blocks;
+    ``blocks``: already evaluated blocks of these rows, e.g. cached).  ``qcoords``
     given: the cross sweep of those query points against ``coords`` (prediction); ``qvalues``: the
     values at the locations (S = T sweep: pass ``values``)."""
-    if isinstance(cv, IsotropicCovariance):
+    if isinstance(cv, (IsotropicCovariance, CallableCovariance)):
         m = nbr.shape[1]
-        if m == 0:
-            raise ValueError("a custom covariance needs m >= 1")
-        if algo not in ("auto", "pairb"):
-            raise ValueError(f"a custom covariance runs on the covariance-block pairb kernel, not algo {algo!r}")
-        dist = _lib.joint_dist(coords, nbr, i0, qcoords=qcoords, order=order)
-        blocks = cv.blocks(dist, m)
-        del dist
+        if not 1 <= m <= _lib.BLOCKS_MAX_M:
+            raise ValueError(f"a custom covariance needs 1 <= m <= {_lib.BLOCKS_MAX_M} (the covariance-block kernels)")
+        if algo not in ("auto", "pairb", "quad"):
+            raise ValueError(f"a custom covariance runs on the covariance-block kernels, not algo {algo!r}")
+        if blocks is None and isinstance(cv, CallableCovariance):
+            blocks = cv.blocks(coords, nbr, i0, qcoords=qcoords, order=order)
+        elif blocks is None:
+            dist = _lib.joint_dist(coords, nbr, i0, qcoords=qcoords, order=order)
+            blocks = cv.blocks(dist, m)
+            del dist
         nq = (coords if qcoords is None else qcoords).shape[0]
         return _lib.bf_sweep_blocks(blocks, nbr, coords.shape[0], i0, values=values, qvalues=qvalues, want_bf=want_bf,
                                     order=order, R=R, n_locs=nq)
@@ -267,6 +424,7 @@ class NNGP:
         self._order, self._nbr_sorted = _lib.row_order(self._s_dev, nbr=self.nbr)
         self._Ns = None
         self._B = self._F = None
+        self._blk_cache = None
 
     def _make_t_neighbor_sets(self):
         """'S=T': Nt aliases Ns (nngp.py:65-67); otherwise the m nearest points of S to
@@ -310,7 +468,7 @@ class NNGP:
         var_t = F_t (conditional variance; includes tau2 like C_tt = sigma2 + tau2).
         Neighbours: the m nearest points of S to each query point (for query = t with
         refType != 'S=T' these are ``Nt``)."""
-        cv = cov if cov is not None else self._covariance()
+        cv = self._covariance(cov)
         v = self.ws if values is None else values
         v = torch.as_tensor(np.asarray(v, dtype=np.float64) if not isinstance(v, torch.Tensor) else v,
                             dtype=torch.float64).to(self.device)
@@ -325,19 +483,45 @@ class NNGP:
             nbr = _lib.knn_query(self._s_dev, q, k)
         n = q.shape[0]
         if nbr.shape[1] == 0:  # m = 0: the marginal
-            return np.zeros(n), np.full(n, cv.sigma2 + cv.tau2)
+            if isinstance(cv, Covariance):
+                return np.zeros(n), np.full(n, cv.sigma2 + cv.tau2)
+            return np.zeros(n), cv.marginal(q).cpu().numpy()
         R = torch.empty(n, dtype=torch.float64, device=self.device)
         _, F, p = _sweep_any(cv, self._s_dev, nbr, 0, values=v, algo=algo, R=R, qcoords=q)
         _raise_on_bad(p.cpu().numpy())
         return (-R).cpu().numpy(), F.cpu().numpy()
 
     # -- covariance plumbing ---------------------------------------------------
-    def _covariance(self):
-        if not isinstance(self.cov, (Covariance, IsotropicCovariance)):
-            raise TypeError(
-                "the device B/F sweep needs cov=pynngp_amd.Covariance(kind, sigma2, phi, tau2[, nu]) or "
-                f"pynngp_amd.IsotropicCovariance(fn, tau2) (got {type(self.cov).__name__})")
-        return self.cov
+    def _covariance(self, cov=None):
+        """The covariance the device sweeps use: ``cov`` (default ``self.cov``); a plain callable
+        ``cov(a, b)`` becomes a :class:`CallableCovariance` (one per callable, so its evaluation mode
+        is probed once)."""
+        c = self.cov if cov is None else cov
+        if isinstance(c, (Covariance, IsotropicCovariance, CallableCovariance)):
+            return c
+        if c is None or not callable(c):
+            raise TypeError("the device B/F sweep needs a covariance: pynngp_amd.Covariance(kind, sigma2, phi, tau2[, "
+                            f"nu]), IsotropicCovariance(fn, tau2) or a callable cov(a, b) (got {type(c).__name__})")
+        wrapped = getattr(self, "_wrapped_cov", None)
+        if wrapped is None or wrapped.fn is not c:
+            wrapped = CallableCovariance(c)
+            self._wrapped_cov = wrapped
+        return wrapped
+
+    def _field_blocks(self, cv):
+        """Joint blocks of the whole field (Z-order rows) for a :class:`CallableCovariance`: its
+        evaluation is the caller's code and the most expensive step, and it depends only on the
+        covariance and the neighbour sets, so it is kept for the next sweep (8 (m+1)(m+2)/2 bytes
+        per location of device memory); None for the other covariance forms."""
+        if not isinstance(cv, CallableCovariance):
+            return None
+        hit = getattr(self, "_blk_cache", None)
+        if hit is not None and hit[0] is cv and hit[1] is self._nbr_sorted:
+            return hit[2]
+        self._blk_cache = None
+        blk = cv.blocks(self._s_dev, self._nbr_sorted, 0, order=self._order)
+        self._blk_cache = (cv, self._nbr_sorted, blk)
+        return blk
 
     def _nbr_idx(self, i):
         row = self.nbr[i]
@@ -348,7 +532,7 @@ class NNGP:
             raise TypeError("cov is None")
         if isinstance(self.cov, (Covariance, IsotropicCovariance)):
             return self.cov(a, b)
-        return self.cov(a.cpu().numpy(), b.cpu().numpy())
+        return self.cov(a.cpu().numpy(), b.cpu().numpy())  # the reference's rows are numpy (nngp.py:7,31)
 
     # -- per-location algebra (nngp.py:73-96) ----------------------------------
     def _CNs(self, i):
@@ -391,7 +575,8 @@ class NNGP:
     def compute_BF(self, algo: str = "auto"):
         """All B (N, m) and F (N,) as device tensors (one fused sweep)."""
         cv = self._covariance()
-        B, F, p = _sweep_any(cv, self._s_dev, self._nbr_sorted, 0, algo=algo, order=self._order)
+        B, F, p = _sweep_any(cv, self._s_dev, self._nbr_sorted, 0, algo=algo, order=self._order,
+                             blocks=self._field_blocks(cv))
         _raise_on_bad(p.cpu().numpy())
         self._B, self._F = B, F
         return B, F
@@ -406,14 +591,14 @@ class NNGP:
 
     def loglik(self, values=None, cov: Optional[Covariance] = None, algo: str = "auto") -> float:
         """NNGP log density of ``values`` (default ``y``): -1/2 sum [log 2pi + log F + r^2/F]."""
-        cv = cov if cov is not None else self._covariance()
+        cv = self._covariance(cov)
         v = self.y if values is None else values
         v = torch.as_tensor(np.asarray(v, dtype=np.float64) if not isinstance(v, torch.Tensor) else v,
                             dtype=torch.float64).to(self.device)
-        if v.dim() != 1:
-            raise ValueError("loglik needs one value per location (1-D values)")
+        if v.dim() != 1 or v.shape[0] != self.nbr.shape[0]:
+            raise ValueError(f"loglik needs one value per location ({self.nbr.shape[0]}, 1-D)")
         _, _, p = _sweep_any(cv, self._s_dev, self._nbr_sorted, 0, values=v, qvalues=v, want_bf=False, algo=algo,
-                             order=self._order)
+                             order=self._order, blocks=self._field_blocks(cv))
         ph = p.cpu().numpy()
         _raise_on_bad(ph)
         n = self.nbr.shape[0]
@@ -435,7 +620,8 @@ class NNGP:
         n = v.shape[0]
         ry = torch.empty(n, dtype=torch.float64, device=self.device)
         r1 = torch.empty_like(ry)
-        kw = dict(algo=algo, order=self._order)
+        cov = self._covariance(cov)
+        kw = dict(algo=algo, order=self._order, blocks=self._field_blocks(cov))
         _, F, py = _sweep_any(cov, self._s_dev, self._nbr_sorted, 0, values=v, qvalues=v, R=ry, **kw)
         ones = torch.ones_like(v)
         _, _, p1 = _sweep_any(cov, self._s_dev, self._nbr_sorted, 0, values=ones, qvalues=ones, R=r1, **kw)
@@ -509,6 +695,10 @@ class NNGP:
             from .gibbs import SeqNNGP
 
             cv = self._covariance()
+            if not isinstance(cv, Covariance):
+                raise TypeError("the Gibbs sampler (SeqNNGP) needs a built-in covariance kind, "
+                                "pynngp_amd.Covariance(kind, sigma2, phi, tau2[, nu]): its phi update re-evaluates the "
+                                f"fused kernel at proposed phi values (got {type(cv).__name__})")
             tau2 = cv.tau2 if cv.tau2 > 0 else 0.1 * cv.sigma2
             if "eps" not in sampler_kw and self.eps is not None:
                 ev = np.asarray(self.eps, dtype=np.float64)

@@ -189,12 +189,16 @@ def test_blocks_entry_points_reject(lib):
     """Covariance-block sweeps (a caller's own covariance): argument checks without a GPU."""
     P = ctypes.c_void_p
     assert lib.nngp_joint_entries(15) == 136 and lib.nngp_joint_entries(0) == 1
-    assert lib.nngp_bf_sweep_blocks_workspace_bytes(1_000_000) == lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0,
-                                                                                                      2, 5)
+    # enough for the two-lane kernel's tile records (m <= 24) and the four-lane kernel's block records (25..32)
+    need = lib.nngp_bf_sweep_blocks_workspace_bytes(1_000_000)
+    assert need == max(lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 5),
+                       lib.nngp_bf_sweep_workspace_bytes(1_000_000, 28, 0, 2, 4))
     args = lambda **kw: [kw.get("cov", P(256)), P(256), None, 10, 10, kw.get("m", 15), 0, 10, None, None, None, None,  # noqa: E731
                          None, P(256), P(256), 1 << 20, None]
-    assert lib.nngp_bf_sweep_blocks(*args(m=25)) == -4
-    assert "m <= 24" in lib.nngp_last_error().decode()
+    assert lib.nngp_bf_sweep_blocks(*args(m=33)) == -4
+    assert "m <= 32" in lib.nngp_last_error().decode()
+    assert lib.nngp_bf_sweep_blocks(*args(m=0)) == -4
+    assert lib.nngp_abi_version() == 2 and b"0.2.0" in lib.nngp_version()
     assert lib.nngp_bf_sweep_blocks(*args(cov=None)) == -1
     assert lib.nngp_joint_dist(P(256), 10, 4, P(256), 10, P(256), None, 10, 5, 0, P(256), None) == -4
     assert lib.nngp_joint_dist(P(256), 10, 2, P(256), 10, P(256), None, 11, 5, 0, P(256), None) == -1

@@ -85,10 +85,17 @@ def test_callable_cov_and_errors(dev):
 
     model = NNGP(t, y, None, "S=T", 4, user_cov)
     assert model._CNs(10).shape == (4, 4)
-    with pytest.raises(TypeError):
-        model._Bsi(10)
-    with pytest.raises(TypeError):  # the sampler needs a Covariance (fused kernel)
+    # the plug-in drives the device sweep (CallableCovariance -> nngp_bf_sweep_blocks)
+    from oracle import nngp_oracle as O
+
+    Bo, Fo, po = O.bf_sweep_callable(t, model.nbr.cpu().numpy(), user_cov, y)
+    np.testing.assert_allclose(model._Bsi(10), Bo[10], rtol=0, atol=1e-10)
+    assert abs(model._Fsi(10) - Fo[10]) <= 1e-10 * Fo[10]
+    assert abs(model.loglik() - O.loglik_from_partials(po, 100)) <= 1e-12 * abs(O.loglik_from_partials(po, 100))
+    with pytest.raises(TypeError, match="built-in covariance"):  # the sampler needs a fused kind
         model.oneSample()
+    with pytest.raises(TypeError, match="needs a covariance"):
+        NNGP(t, y, None, "S=T", 4, None).loglik()
     with pytest.raises(ValueError):
         NNGP(t, y, None, ("grid", 10), 4, None)
     with pytest.raises(ValueError):

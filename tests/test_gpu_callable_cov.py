@@ -1,0 +1,201 @@
+"""GPU parity: the reference's own covariance plug-in ``cov(a, b)`` (pyNNGP/nngp.py:6,12, called on
+coordinate rows at :82, :96) driving B / F / the log-likelihood on the device
+(CallableCovariance: joint blocks fn(X, X) -> nngp_bf_sweep_blocks; the two-lane blocked kernel for
+m <= 24, the four-lane kernel for 25..32).
+
+Oracle: ``oracle.nngp_oracle.bf_sweep_callable`` -- the same plug-in called as the reference calls
+it (C_N = cov(X_N, X_N), c = cov(x_i, X_N), C_ii = cov(x_i, x_i)) and one dense solve per location.
+Parity is unpinned by the reference (its _Bsi / _Fsi are stubs); the tolerances are DESIGN.md 2's:
+F <= 1e-10 relative, B <= 1e-9 (1 + |B|), log-lik <= 1e-12 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nngp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _aniso(s2, A, tau2=0.0):
+    """Anisotropic exponential s2 exp(-sqrt((a-b)^T A (a-b))) (+ tau2 where a == b) -- a covariance
+    no built-in kind or isotropic function expresses; broadcasts over leading dimensions in numpy
+    and in torch."""
+    A = np.asarray(A, dtype=np.float64)
+
+    def cov(a, b):
+        lib = torch if isinstance(a, torch.Tensor) else np
+        t = a[..., :, None, :] - b[..., None, :, :]
+        At = torch.as_tensor(A, dtype=t.dtype, device=t.device) if lib is torch else A
+        q = ((t @ At) * t).sum(-1)
+        c = s2 * lib.exp(-lib.sqrt(q))
+        return c + tau2 * (q == 0) if tau2 else c
+
+    return cov
+
+
+def _np_only(s2, A, tau2=0.0):
+    """The same covariance in numpy only (host evaluation)."""
+    f = _aniso(s2, A, tau2)
+    return lambda a, b: f(np.asarray(a), np.asarray(b))
+
+
+def _loop_only(s2, A, tau2=0.0):
+    """... and written for 2-D row sets only, as a reference user would (one call per location)."""
+    A = np.asarray(A, dtype=np.float64)
+
+    def cov(a, b):
+        a, b = np.atleast_2d(np.asarray(a)), np.atleast_2d(np.asarray(b))
+        out = np.empty((a.shape[0], b.shape[0]))
+        for k in range(a.shape[0]):
+            t = b - a[k]
+            q = np.einsum("ij,jk,ik->i", t, A, t)
+            out[k] = s2 * np.exp(-np.sqrt(q)) + tau2 * (q == 0)
+        return out
+
+    return cov
+
+
+A1 = [[400.0, 150.0], [150.0, 100.0]]
+
+
+def _check(B, F, p, Bo, Fo, po, n):
+    np.testing.assert_allclose(F.cpu().numpy(), Fo, rtol=1e-10, atol=0)
+    Bg = B.cpu().numpy()
+    assert np.all(np.abs(Bg - Bo) <= 1e-9 * (1 + np.abs(Bo)))
+    ll, llo = O.loglik_from_partials(p.cpu().numpy(), n), O.loglik_from_partials(po, n)
+    assert abs(ll - llo) <= 1e-12 * abs(llo), (ll, llo)
+
+
+@pytest.mark.parametrize("form", ["torch", "numpy", "loop"])
+@pytest.mark.parametrize("m", [1, 6, 15, 24, 25, 28, 32])
+def test_callable_sweep_vs_oracle(dev, form, m):
+    from pynngp_amd import CallableCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    if form == "loop" and m not in (6, 28):
+        pytest.skip("one-call-per-location plug-in: two sizes suffice")
+    rng = np.random.default_rng(100 + m)
+    n = 1500
+    x = rng.uniform(size=(n, 2))
+    y = rng.standard_normal(n)
+    mk = {"torch": _aniso, "numpy": _np_only, "loop": _loop_only}[form]
+    fn = mk(1.4, A1, 0.05)
+    cc = CallableCovariance(fn)
+    c = torch.from_numpy(x).to(dev)
+    v = torch.from_numpy(y).to(dev)
+    nb = _lib.knn_prior(c, m)
+    B, F, p = _sweep_any(cc, c, nb, 0, values=v, qvalues=v)
+    assert cc.mode == form
+    assert p[2].item() == -1 and p[3].item() == -1
+    Bo, Fo, po = O.bf_sweep_callable(x, nb.cpu().numpy(), _aniso(1.4, A1, 0.05), y)
+    _check(B, F, p, Bo, Fo, po, n)
+
+
+@pytest.mark.parametrize("m", [10, 27])
+def test_callable_visiting_order_and_bits(dev, m):
+    """Z-order visiting order gives the same bits per row; two runs give the same bits."""
+    from pynngp_amd import CallableCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    rng = np.random.default_rng(7 + m)
+    x = rng.uniform(size=(5000, 2))
+    y = rng.standard_normal(5000)
+    c, v = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    nb = _lib.knn_prior(c, m)
+    cc = CallableCovariance(_aniso(1.0, [[90.0, -20.0], [-20.0, 30.0]], 0.1))
+    B1, F1, p1 = _sweep_any(cc, c, nb, 0, values=v, qvalues=v)
+    order, nbs = _lib.row_order(c, nbr=nb)
+    B2, F2, p2 = _sweep_any(cc, c, nbs, 0, values=v, qvalues=v, order=order)
+    assert torch.equal(F1, F2) and torch.equal(B1, B2)
+    B3, F3, p3 = _sweep_any(cc, c, nbs, 0, values=v, qvalues=v, order=order)
+    assert torch.equal(p2, p3) and torch.equal(F2, F3)
+    np.testing.assert_allclose(p1[:2].cpu().numpy(), p2[:2].cpu().numpy(), rtol=1e-12)
+
+
+@pytest.mark.parametrize("m", [12, 30])
+def test_callable_bad_index_flag(dev, m):
+    from pynngp_amd import CallableCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    rng = np.random.default_rng(3)
+    x = torch.from_numpy(rng.uniform(size=(800, 2))).to(dev)
+    nb = _lib.knn_prior(x, m)
+    nb[400, 3] = 800  # out of range
+    _, _, p = _sweep_any(CallableCovariance(_aniso(1.0, A1, 0.1)), x, nb, 0)
+    assert p[3].item() == 400
+
+
+def test_nngp_class_with_reference_style_callable(dev):
+    """NNGP(t, y, eps, 'S=T', m, cov) with a plain callable: _CNs / _Ccross / _Cs are the plug-in's
+    values, _Bsi / _Fsi / compute_BF / loglik come from the device sweep and match the oracle."""
+    from pynngp_amd import NNGP
+
+    rng = np.random.default_rng(11)
+    n, m = 1200, 12
+    t = rng.uniform(size=(n, 2))
+    y = rng.standard_normal(n)
+    user_cov = _np_only(2.0, A1, 0.1)
+    model = NNGP(t, y, None, "S=T", m, user_cov)
+    nbr = model.nbr.cpu().numpy()
+    Bo, Fo, po = O.bf_sweep_callable(t, nbr, user_cov, y)
+    for i in (0, 1, 5, 600, n - 1):
+        k = min(i, m)
+        idx = nbr[i, :k]
+        np.testing.assert_allclose(model._CNs(i), user_cov(t[idx], t[idx]), rtol=1e-15)
+        np.testing.assert_allclose(np.ravel(model._Cs(i))[0], 2.1, rtol=1e-15)
+        Bi, Fi = model._Bsi(i), model._Fsi(i)
+        assert Bi.shape == (k,)
+        np.testing.assert_allclose(Bi, Bo[i, :k], rtol=0, atol=1e-9)
+        assert abs(Fi - Fo[i]) <= 1e-10 * Fo[i]
+    B, F = model.compute_BF()
+    np.testing.assert_allclose(F.cpu().numpy(), Fo, rtol=1e-10)
+    assert np.all(np.abs(B.cpu().numpy() - Bo) <= 1e-9 * (1 + np.abs(Bo)))
+    ll = model.loglik()
+    want = O.loglik_from_partials(po, n)
+    assert abs(ll - want) <= 1e-12 * abs(want)
+    assert model._blk_cache is not None  # the plug-in's blocks are kept for the next sweep
+    assert model.loglik() == ll
+    y2 = rng.standard_normal(n)
+    _, _, p2 = O.bf_sweep_callable(t, nbr, user_cov, y2)
+    assert abs(model.loglik(y2) - O.loglik_from_partials(p2, n)) <= 1e-12 * abs(model.loglik(y2))
+
+
+def test_predict_with_callable(dev):
+    """Kriging at points outside S with a plug-in (the cross sweep through the blocks kernel) vs the
+    oracle with the location rows taken from the query points."""
+    from pynngp_amd import NNGP
+
+    rng = np.random.default_rng(12)
+    n, m = 900, 10
+    t = rng.uniform(size=(n, 2))
+    y = rng.standard_normal(n)
+    user_cov = _aniso(1.5, A1, 0.02)
+    model = NNGP(t, y, None, "S=T", m, user_cov)
+    q = rng.uniform(size=(300, 2))
+    mean, var = model.predict(values=y, query=q)
+    nq = O.knn_all(q, t, m)
+    Bo, Fo, _ = O.bf_sweep_callable(t, nq, user_cov, y, qcoords=q, qvalues=np.zeros(300))
+    np.testing.assert_allclose(var, Fo, rtol=1e-10)
+    np.testing.assert_allclose(mean, (Bo * y[nq]).sum(1), rtol=0, atol=1e-9)
+    with pytest.raises(TypeError, match="built-in covariance"):
+        model.oneSample()
+
+
+def test_isotropic_and_callable_agree_at_m28(dev):
+    """The four-lane blocks kernel (m = 25..32) with an isotropic function equals the fused
+    exponential kernel, as the two-lane blocks kernel does for m <= 24."""
+    from pynngp_amd import Covariance, IsotropicCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    rng = np.random.default_rng(13)
+    x = rng.uniform(size=(4000, 2))
+    y = rng.standard_normal(4000)
+    c, v = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    nb = _lib.knn_prior(c, 28)
+    B1, F1, p1 = _sweep_any(IsotropicCovariance(lambda d: 1.2 * torch.exp(-20.0 * d), 0.1), c, nb, 0, values=v,
+                            qvalues=v)
+    B2, F2, p2 = _sweep_any(Covariance("exponential", 1.2, 20.0, 0.1), c, nb, 0, values=v, qvalues=v)
+    np.testing.assert_allclose(F1.cpu().numpy(), F2.cpu().numpy(), rtol=1e-10)
+    assert torch.all((B1 - B2).abs() <= 1e-9 * (1 + B2.abs()))
+    assert abs(p1[1].item() - p2[1].item()) <= 1e-11 * abs(p2[1].item())

@@ -146,10 +146,12 @@ def test_custom_order_bad_index_and_limits(lib, dev):
     bad[777, 3] = -2
     _, _, pb = _sweep(lib, cov, c, bad, v)
     assert pb[3].item() == 777.0
-    # m past the blocks kernels
-    nb25 = lib.knn_prior(c[:2000], 25)
-    with pytest.raises(lib.NNGPExtensionError, match="m <= 24"):
-        _sweep(lib, cov, c[:2000], nb25)
+    # m past the blocks kernels (the two-lane kernel serves 1..24, the four-lane kernel 25..32)
+    nb33 = lib.knn_prior(c[:2000], 33)
+    with pytest.raises(ValueError, match="m <= 32"):
+        _sweep(lib, cov, c[:2000], nb33)
+    with pytest.raises(lib.NNGPExtensionError, match="m <= 32"):
+        lib.bf_sweep_blocks(torch.zeros((34 * 35 // 2, 2000), dtype=torch.float64, device=dev), nb33, 2000)
 
 
 def test_matern_elementwise_and_custom_matern(lib, dev, c_oracle):
