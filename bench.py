@@ -83,8 +83,24 @@ def committed_profile(args, want_bf):
     except (OSError, ValueError, KeyError):
         return None
     for e in entries:
+        if e.get("preset") is not None or e.get("role", "sweep") != "sweep":
+            continue  # the Gibbs preset's kernels (gibbs_profile)
         if (e["n_per_gpu"] == args.n and e["m"] == args.m and e["kind"] == args.kind and e["layout"] == args.layout
                 and e["write_BF"] == want_bf and args.algo == "auto"):
+            return e
+    return None
+
+
+def gibbs_profile(args, role):
+    """The committed rocprofv3 entry of config 5's kernel `role` ("sweep": the phi proposal's fused
+    B/F sweep, "colour": the w sweep's colour step) at this N and m, or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            entries = json.load(f)["entries"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for e in entries:
+        if e.get("preset") == 5 and e.get("role") == role and e["n_per_gpu"] == args.n and e["m"] == args.m:
             return e
     return None
 
@@ -121,6 +137,22 @@ def valu_roofline(prof, rows, kern_ms):
            "frac": achieved / VALU_LANE_OPS_PEAK, "valu_lane_ops_per_location": per_loc,
            "source": prof["source"] + " (SQ_INSTS_VALU / SQ_WAVES)"}
     for k in ("valu_active_cycles_per_instr", "simd_valu_busy", "valu_source"):
+        if k in prof:
+            out[k] = prof[k]
+    return out
+
+
+def colour_roofline(prof):
+    """The w sweep's colour step (config 5's largest kernel-time share) from its committed rocprofv3
+    passes: average launch time, HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) and VALU issue.
+    Its members' children are gathered at random, so it is latency bound, not HBM bound: the
+    fraction is reported against 8 TB/s for scale only."""
+    if prof is None or "bytes_per_launch" not in prof:
+        return None
+    bw = prof["bytes_per_launch"] / (prof["avg_ns"] * 1e-9)
+    out = {"kernel": prof["kernel"], "avg_us": prof["avg_ns"] / 1e3, "traffic": prof["bytes_per_launch"],
+           "hbm_GBps": bw / 1e9, "hbm_frac": bw / HBM_PEAK, "source": prof["source"]}
+    for k in ("valu_per_wave", "valu_active_cycles_per_instr", "simd_valu_busy"):
         if k in prof:
             out[k] = prof[k]
     return out
@@ -290,6 +322,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     g.r.copy_(r_save)
     ms_iter = 1e3 * elapsed / args.steps
     if rank == 0:
+        sweep_prof = gibbs_profile(args, "sweep") if not single else None
+        colour_prof = gibbs_profile(args, "colour") if not single else None
         bpl = bytes_per_location(m) + 8  # + the residual r written for the sampler
         rows = g.hi - g.lo if single else n
         achieved = bpl * rows / (sweep_ms * 1e-3)
@@ -328,8 +362,13 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
             "roofline": {
                 "bound": "hbm", "kernel": "fused B/F + residual sweep of a phi proposal",
                 "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": achieved / HBM_PEAK,
-                "traffic": None, "algorithmic_bytes_per_location": bpl, "kernel_ms": sweep_ms, "kernel_rows": rows,
+                "traffic": sweep_prof.get("bytes_per_launch") if sweep_prof else None,
+                "traffic_source": (f'{sweep_prof["source"]} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, '
+                                   f'{sweep_prof["kernel"]})') if sweep_prof else None,
+                "algorithmic_bytes_per_location": bpl, "kernel_ms": sweep_ms, "kernel_rows": rows,
             },
+            "roofline_valu": valu_roofline(sweep_prof, rows, sweep_ms) if sweep_prof else None,
+            "roofline_colour": colour_roofline(colour_prof),
             "state": {"phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "beta": list(map(float, g.beta))},
             "lib": os.path.relpath(_lib.LIB_PATH, ROOT),
         }

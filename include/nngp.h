@@ -46,20 +46,26 @@ extern "C" {
 #define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
 #define NNGP_COV_MATERN 5      /* sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), 0 < nu <= 50: spNNGP's
                                   "matern" of any smoothness nu (the `nu` argument of the sweeps;
-                                  ignored by the other kinds).  Served by the wavefront kernel. */
+                                  ignored by the other kinds).  m <= 24: the pair kernel evaluating
+                                  rho from a per-launch table in (phi d)^2 (nu >= ~0.45, whose table
+                                  fits 160 octaves); smaller nu and m > 24: the wavefront kernel's
+                                  direct Bessel evaluation. */
 
 /* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE serves 2-D
- * exponential / Matern-3/2 only, PAIRB, QUAD and WAVE kinds 0..4 in every dimension, WAVE also
- * NNGP_COV_MATERN (AUTO sends it there for every m).  (3 and 7 were
- * comparison-only kernels of earlier builds; they are rejected as unknown.) */
-#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above (and matern)  */
+ * exponential / Matern-3/2 only, QUAD kinds 0..4 in every dimension, PAIRB and WAVE every kind
+ * (PAIRB: NNGP_COV_MATERN with nu >= ~0.45).  (3 and 7 were comparison-only kernels of earlier
+ * builds; they are rejected as unknown.) */
+#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above (matern: see kind 5) */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
 #define NNGP_ALGO_QUAD 4  /* four lanes per location (25 <= m <= 32)                         */
 #define NNGP_ALGO_PAIRB 5 /* two lanes per location, 2x2-blocked (1 <= m <= 24)              */
 
-/* the kernel NNGP_ALGO_AUTO (or an explicit code, returned as is) resolves to for (m, kind, dim) */
+/* the kernel NNGP_ALGO_AUTO (or an explicit code, returned as is) resolves to for (m, kind, dim);
+ * for NNGP_COV_MATERN the choice depends on nu: nngp_resolve_algo_nu (nngp_resolve_algo assumes a nu
+ * the pair kernel's table covers).  nngp_bf_finalize of a matern sweep needs the resolved code. */
 int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim);
+int32_t nngp_resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim, double nu);
 
 #define NNGP_MAX_M 63
 #define NNGP_MAX_DIM 3

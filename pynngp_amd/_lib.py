@@ -29,6 +29,7 @@ SYMBOLS = (
     "nngp_bf_cross",
     "nngp_bf_finalize",
     "nngp_resolve_algo",
+    "nngp_resolve_algo_nu",
     "nngp_loglik_from_partials",
     "nngp_check_partials",
     "nngp_row_order_workspace_bytes",
@@ -125,6 +126,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_bf_finalize.restype = ctypes.c_int
     lib.nngp_resolve_algo.argtypes = [I32, I32, I32, I32]
     lib.nngp_resolve_algo.restype = I32
+    lib.nngp_resolve_algo_nu.argtypes = [I32, I32, I32, I32, D]
+    lib.nngp_resolve_algo_nu.restype = I32
     lib.nngp_combine_partials.restype = ctypes.c_int
     U64 = ctypes.c_uint64
     lib.nngp_reverse_workspace_bytes.argtypes = [I64, I32]
@@ -168,9 +171,13 @@ def version() -> str:
     return load().nngp_version().decode()
 
 
-def resolve_algo(algo: str, m: int, kind: str, dim: int) -> str:
-    """The kernel ``algo`` ("auto" or explicit) runs as for (m, kind, dim) (nngp_resolve_algo)."""
-    code = load().nngp_resolve_algo(ALGO_CODES[algo], int(m), KIND_CODES[kind], int(dim))
+def resolve_algo(algo: str, m: int, kind: str, dim: int, nu: Optional[float] = None) -> str:
+    """The kernel ``algo`` ("auto" or explicit) runs as for (m, kind, dim) (nngp_resolve_algo; with ``nu``
+    for the ``matern`` kind, whose pair-kernel table covers nu >= ~0.45: nngp_resolve_algo_nu)."""
+    if nu is not None:
+        code = load().nngp_resolve_algo_nu(ALGO_CODES[algo], int(m), KIND_CODES[kind], int(dim), float(nu))
+    else:
+        code = load().nngp_resolve_algo(ALGO_CODES[algo], int(m), KIND_CODES[kind], int(dim))
     names = {v: k for k, v in ALGO_CODES.items()}
     return names.get(code, str(code))
 

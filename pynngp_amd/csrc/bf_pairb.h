@@ -124,7 +124,9 @@ constexpr bool pairb_left3(int m) {
     return pairb_left(m) && (((unsigned long long)(NNGP_PAIRB_LEFT_3W_MASK) >> m) & 1ull);
 }
 // the same for a kernel of covariance kind `kind` (the covariance-blocks kernels are right-looking)
-constexpr bool pairb_lk(int m, int kind) { return pairb_left(m) && kind != NNGP_KIND_BLOCKS; }
+constexpr bool pairb_lk(int m, int kind) {
+    return pairb_left(m) && kind != NNGP_KIND_BLOCKS && kind != NNGP_KIND_MATERN;
+}
 constexpr bool pairb_left3_k(int m, int kind) { return pairb_left3(m) && kind != NNGP_KIND_BLOCKS; }
 // static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
 #ifdef NNGP_PAIRB_PHASES
@@ -177,7 +179,8 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 #ifndef NNGP_PAIRB_THREE_WAVES_MAX
 #define NNGP_PAIRB_THREE_WAVES_MAX 13
 #endif
-// (KIND == NNGP_KIND_BLOCKS: covariances read from memory, always right-looking -- pairb_lk)
+// (KIND == NNGP_KIND_BLOCKS: covariances read from memory; NNGP_KIND_MATERN: the Matern table in LDS
+// -- both always right-looking, pairb_lk)
 #define NNGP_PAIRB_ATTR                                                                              \
     __attribute__((amdgpu_waves_per_eu(                                                                 \
         ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3                                 \
@@ -263,6 +266,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
+    constexpr bool MT = KIND == NNGP_KIND_MATERN;  // cblk: the launch's Matern table (matern_table.hip)
     constexpr int DA = point_arity<D>();  // coordinates held per point
     const int ds = D == 0 ? dim : D;      // row stride of coords / qcoords
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
@@ -279,13 +283,15 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     __shared__ double lrow[KL > 0 ? KL * (KL + 1) : 1][KL > 0 ? kPairbThreads : 1];
     constexpr bool ZLDS = NOZ && M >= NNGP_PAIRB_ZLDS_MIN;
     __shared__ double zsh[ZLDS ? NP : 1][ZLDS ? kPairbThreads : 1];
-    __shared__ double etab[NNGP_EXP_TAB_N];
+    __shared__ double etab[MT ? 1 : NNGP_EXP_TAB_N];
+    extern __shared__ double4 pairb_mtab[];  // MT: the Matern table (dynamic LDS, NNGP_MT_BYTES(noct))
+    const double* ctab = MT ? (const double*)pairb_mtab : etab;  // the covariance evaluation's table
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)
     constexpr int kTabPer = kPairbThreads >= NNGP_EXP_TAB_N ? 1 : NNGP_EXP_TAB_N / kPairbThreads;
     static_assert(kPairbThreads >= NNGP_EXP_TAB_N || kTabPer * kPairbThreads == NNGP_EXP_TAB_N, "table fill");
     double etab_entry[kTabPer];
-    if constexpr (!CM) {
+    if constexpr (!CM && !MT) {
 #pragma unroll
         for (int e = 0; e < kTabPer; ++e)
             etab_entry[e] = nngp_exp_table_entry_unit(((int)threadIdx.x + e * kPairbThreads) & (NNGP_EXP_TAB_N - 1));
@@ -350,7 +356,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
-        if constexpr (!CM) {
+        if constexpr (MT) {
+            const int n4 = Pc.mt_noct * (NNGP_MT_K * NNGP_MT_NC / 4);
+            const double4* g = (const double4*)cblk;
+            for (int k = (int)threadIdx.x; k < n4; k += kPairbThreads) pairb_mtab[k] = g[k];
+            __syncthreads();
+        } else if constexpr (!CM) {
 #pragma unroll
             for (int e = 0; e < kTabPer; ++e)
                 if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
@@ -411,8 +422,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             for (int s = 0; s < NP; ++s) {
 #pragma unroll
                 for (int t = 0; t < s; ++t) {
-                    R[s][t][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], o[t]));
-                    R[s][t][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], p[t]));
+                    R[s][t][0] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s], o[t]));
+                    R[s][t][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s], p[t]));
                 }
                 R[s][s][0] = Pc.diag;
             }
@@ -429,12 +440,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                         a[k] = pr_pick(mask1, o[s1][k], o[s0][k]);
                         b[k] = pr_pick(mask1, p[s1][k], p[s0][k]);
                     }
-                    const double c = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(a, b));
+                    const double c = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(a, b));
                     R[s1][s1][1] = c;
                     R[s0][s0][1] = pr_from0(c);
                 } else {
-                    R[s0][s0][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s0], p[s0]));
-                    if (s1 < NP) R[s1][s1][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s1], p[s1]));
+                    R[s0][s0][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s0], p[s0]));
+                    if (s1 < NP) R[s1][s1][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s1], p[s1]));
                 }
             }
         }
@@ -579,8 +590,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 for (int k = 0; k < DA; ++k) pu[k] = (u % 2 == 1) ? pnext[k] : pr_swap(o[u][k]);
 #pragma unroll
                 for (int s = u + 1; s < NP; ++s) {
-                    R[s][u][0] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], o[u]));
-                    R[s][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[s], pu));
+                    R[s][u][0] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s], o[u]));
+                    R[s][u][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[s], pu));
                 }
                 R[u][u][0] = Pc.diag;
                 // the within-pair entry (2u+1, 2u) is read from lane 1 only: for pairs u, u+1 (u even)
@@ -594,12 +605,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                         a[k] = pr_pick(mask1, o[u + 1][k], o[u][k]);
                         b[k] = pr_pick(mask1, pnext[k], pu[k]);
                     }
-                    wpnext = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(a, b));
+                    wpnext = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(a, b));
                     R[u][u][1] = pr_from0(wpnext);
                 } else if (u % 2 == 1) {
                     R[u][u][1] = wpnext;
                 } else {
-                    R[u][u][1] = nngp_cov_unit<KIND>(Pc, etab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
+                    R[u][u][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
                 }
 #pragma unroll
                 for (int t = 0; t < u; ++t) {
@@ -776,7 +787,8 @@ inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
 
 template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
-    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), 0, s, a.coords,
+    const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
+    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), lds, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
                        a.qcoords, a.qvalues, a.B, a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), a.dim,
                        a.cblk);
@@ -810,6 +822,7 @@ static bool launch_pairb_if(const BfArgs& a, const CovParams& Pc, hipStream_t s)
         case 2: launch_pairb_mkd<M, 2, D>(a, Pc, s); return true;
         case 3: launch_pairb_mkd<M, 3, D>(a, Pc, s); return true;
         case 4: launch_pairb_mkd<M, 4, D>(a, Pc, s); return true;
+        case NNGP_KIND_MATERN: launch_pairb_mkd<M, NNGP_KIND_MATERN, D>(a, Pc, s); return true;
         default: return false;
     }
 }

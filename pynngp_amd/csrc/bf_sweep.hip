@@ -379,7 +379,19 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         nb = bf_lane_blocks(a.n_rows);
     } else if (algo == kAlgoPairB) {
         // unit-variance factorisation (nngp_cov_unit), F scaled by sigma2 in the kernel
-        ok = bf_pairb_launch(a, nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2), s);
+        CovParams Pu = nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2);
+        BfArgs b = a;
+        if (a.kind == NNGP_KIND_MATERN) {
+            // the launch's Matern table (a function of nu only: t = phi^2 d^2) after the tile records
+            nngp_matern_setup(Pu, a.nu);
+            Pu.mphi2 = a.phi * a.phi;
+            if (!matern_table_extent(a.nu, &Pu.mt_e0, &Pu.mt_noct)) return hipErrorInvalidValue;
+            double* tab = (double*)((char*)a.bpart + bf_pairb_workspace_bytes(a.n_rows));
+            hipError_t e = matern_table_launch(Pu, tab, s);
+            if (e != hipSuccess) return e;
+            b.cblk = tab;
+        }
+        ok = bf_pairb_launch(b, Pu, s);
         if (!ok) return hipErrorInvalidValue;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || a.partials == nullptr) return e;

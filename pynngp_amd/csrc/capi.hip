@@ -37,11 +37,21 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
-    // general-smoothness Matern: the Bessel function's loops stay out of the unrolled register kernels
-    if (kind == NNGP_COV_MATERN) return nngp::kAlgoWave;
+    // general-smoothness Matern: the pair kernel with the launch's table for m <= 24 (nu >= NNGP_MT_NU_MIN;
+    // resolve_algo_nu decides for a given nu), the wavefront kernel (the direct Bessel evaluation) above
+    if (kind == NNGP_COV_MATERN) return m >= 1 && m <= 24 ? nngp::kAlgoPairB : nngp::kAlgoWave;
     if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
     if (m >= 25 && m <= 32) return nngp::kAlgoQuad;
     return nngp::kAlgoWave;
+}
+
+// ... for a given smoothness: the Matern table must fit NNGP_MT_MAX_OCT octaves (nu >= ~0.45), else the
+// wavefront kernel
+int resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim, double nu) {
+    const int a = resolve_algo(algo, m, kind, dim);
+    if (algo != NNGP_ALGO_AUTO || kind != NNGP_COV_MATERN || a != nngp::kAlgoPairB) return a;
+    int e0, noct;
+    return nu > 0.0 && nu <= NNGP_MATERN_NU_MAX && nngp::matern_table_extent(nu, &e0, &noct) ? a : nngp::kAlgoWave;
 }
 
 int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_count(n_rows, algo, m); }
@@ -56,6 +66,10 @@ int32_t nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 const char* nngp_last_error(void) { return g_err; }
 
 int32_t nngp_resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) { return resolve_algo(algo, m, kind, dim); }
+
+int32_t nngp_resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim, double nu) {
+    return resolve_algo_nu(algo, m, kind, dim, nu);
+}
 
 int nngp_check_partials(const double* p, int64_t* first_bad_row, int64_t* first_bad_index) {
     if (p == nullptr) return fail(NNGP_EINVAL, "partials must be non-null");
@@ -73,6 +87,14 @@ double nngp_loglik_from_partials(const double* p, int64_t n_rows) {
 size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, int32_t dim, int32_t algo) {
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return 0;
     const int a = resolve_algo(algo, m, kind, dim);
+    const int64_t nbw = n_rows > 0 ? bf_blocks(n_rows, nngp::kAlgoWave, m) : 0;
+    if (kind == NNGP_COV_MATERN && a == nngp::kAlgoPairB) {
+        // tile records + exponent sums + the Matern table; AUTO (nu unknown here) also covers the
+        // wavefront kernel's records, which serve nu below the table's range
+        const size_t pb = nngp::bf_pairb_workspace_bytes(n_rows) + align256(NNGP_MT_BYTES(NNGP_MT_MAX_OCT));
+        const size_t wb = align256((size_t)nbw * 4 * sizeof(double));
+        return algo == NNGP_ALGO_AUTO && wb > pb ? wb : pb;
+    }
     if (a == nngp::kAlgoPairB) return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + exponent sums
     const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a, m) : 0;
     return align256((size_t)nb * 4 * sizeof(double));
@@ -100,12 +122,18 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     if (F != nullptr && B == nullptr && m > 0 && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
     if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
     if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
-    int a = resolve_algo(algo, m, kind, dim);
+    int a = resolve_algo_nu(algo, m, kind, dim, nu);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
         return fail(NNGP_EINVAL, "unknown algo %d", algo);
-    if (kind == NNGP_COV_MATERN && a != nngp::kAlgoWave)
-        return fail(NNGP_EUNSUP, "the matern kind runs on the wavefront kernel (NNGP_ALGO_AUTO or WAVE), not algo %d",
+    if (kind == NNGP_COV_MATERN && a != nngp::kAlgoWave && a != nngp::kAlgoPairB)
+        return fail(NNGP_EUNSUP, "the matern kind runs on the pair kernel (m <= 24) or the wavefront kernel, not algo %d",
                     algo);
+    if (kind == NNGP_COV_MATERN && a == nngp::kAlgoPairB) {
+        int e0, noct;
+        if (!nngp::matern_table_extent(nu, &e0, &noct))
+            return fail(NNGP_EUNSUP, "matern nu=%g needs %d table octaves (> %d; nu below ~%g): use NNGP_ALGO_AUTO or "
+                                     "WAVE", nu, noct, NNGP_MT_MAX_OCT, NNGP_MT_NU_MIN);
+    }
     const bool classic = dim == 2 && kind <= NNGP_COV_MATERN32;
     if (a == nngp::kAlgoLane && !classic)
         return fail(NNGP_EUNSUP, "the lane kernel serves 2-D exponential and Matern-3/2 only "
@@ -225,6 +253,9 @@ int nngp_bf_finalize(const void* workspace, size_t workspace_bytes, int64_t n_ro
     if (n_rows < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_rows or m");
     if (dim < 1 || dim > NNGP_MAX_DIM || kind < NNGP_COV_EXPONENTIAL || kind > NNGP_COV_MATERN)
         return fail(NNGP_EINVAL, "bad kind %d or dim %d", kind, dim);
+    if (kind == NNGP_COV_MATERN && algo == NNGP_ALGO_AUTO)
+        return fail(NNGP_EINVAL, "the matern kind's kernel depends on nu: pass the sweep's resolved algo "
+                                 "(nngp_resolve_algo_nu), not NNGP_ALGO_AUTO");
     const int a = resolve_algo(algo, m, kind, dim);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
         return fail(NNGP_EINVAL, "unknown algo %d", algo);

@@ -92,6 +92,10 @@ struct CovParams {
     // Gamma(1 + mu), Gamma(1 - mu), mu pi / sin(mu pi), and the scale 2^(1 - nl) / Gamma(nu)
     double nu, mu, mg1, mg2, mgp, mgm, mfac, mscale;
     int mnl;
+    // NNGP_KIND_MATERN on the fused pair kernel (nngp_matern_table_setup, nngp_matern_tab): t = mphi2 d^2,
+    // the table's first octave exponent and octave count
+    double mphi2;
+    int mt_e0, mt_noct;
 };
 
 NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double tau2) {
@@ -265,6 +269,125 @@ NNGP_HD double nngp_matern_rho(const CovParams& P, double u) {
     return P.mscale * j1;
 }
 
+// ---------------------------------------------------------------- Matern-nu by table (bf_pairb)
+// The fused pair kernel evaluates rho from a per-launch table in t = u^2 = phi^2 d^2 (no square root,
+// no Bessel loop).  Octave o of t -- t in [2^(e0+o-1), 2^(e0+o)), o = (frexp exponent of t) - e0 -- is
+// split into NNGP_MT_K bins by its top mantissa bits; each bin holds a degree-(NNGP_MT_NC - 1)
+// polynomial in the bin's local variable f in [0, 1): the Chebyshev interpolant of rho at NNGP_MT_NC
+// nodes (values from nngp_matern_rho), in monomial form.  Octave 0 holds rho = 1 (every t below it
+// has 1 - rho < NNGP_MT_EPS) and octave noct - 1 holds rho = 0 (rho < NNGP_MT_EPS beyond): coincident
+// points give exactly 1, far-away padding points exactly 0 (decoupled).  Interpolation error against
+// mpmath (nu = 0.5 .. 50, 4 bins per octave, degree 13): <= 1.2e-17 absolute; the table inherits the
+// accuracy of nngp_matern_rho (<= 1.3e-15 absolute).  Per covariance: 11 VALU for the index and the
+// local variable, 13 FMAs, NNGP_MT_NC / 2 LDS reads of 16 B.  The octaves from 1 - rho < eps to
+// rho < eps fit NNGP_MT_MAX_OCT for nu >= NNGP_MT_NU_MIN; smaller nu stay on the wavefront kernel.
+#define NNGP_MT_K 4
+#define NNGP_MT_NC 14
+#define NNGP_MT_MAX_OCT 160
+#define NNGP_MT_EPS 1e-18
+#define NNGP_MT_NU_MIN 0.4
+#define NNGP_MT_BYTES(noct) ((size_t)(noct) * NNGP_MT_K * NNGP_MT_NC * sizeof(double))
+
+// a bound on 1 - rho(sqrt(t)) for small t from the expansion rho = 1 - A t^nu - t / (4 (1 - nu)) + ...,
+// A = Gamma(1 - nu) / (4^nu Gamma(1 + nu)) (u^nu K_nu(u) through I_-nu and I_nu), with margin; near
+// nu = 1, where the two terms cancel into (t / 4) ln(1 / t), a bound of that form
+NNGP_HD double nngp_matern_small_bound(double nu, double t) {
+    const double d1 = fabs(1.0 - nu);
+    if (d1 < 0.05) return 6.0 * pow(t, fmin(nu, 1.0)) * (fabs(log(t)) + 5.0);
+    double b = 0.25 * t / d1;
+    if (nu < 1.95) b += fabs(tgamma(1.0 - nu)) / (pow(4.0, nu) * tgamma(1.0 + nu)) * pow(t, nu);
+    return 2.0 * b;
+}
+
+// table extent for P (nngp_matern_setup done): returns false when it would exceed NNGP_MT_MAX_OCT
+NNGP_HD bool nngp_matern_table_setup(CovParams& p) {
+    p.mphi2 = p.phi * p.phi;
+    int ez = 1;  // smallest E with rho(sqrt(2^E)) < eps (rho decreases)
+    while (ez < 1100 && !(nngp_matern_rho(p, sqrt(ldexp(1.0, ez))) < NNGP_MT_EPS)) ++ez;
+    int e0 = 0;  // largest E <= 0 with the small-t bound below eps at 2^E (the bound increases with t)
+    while (e0 > -1074 && !(nngp_matern_small_bound(p.nu, ldexp(1.0, e0)) < NNGP_MT_EPS)) --e0;
+    p.mt_e0 = e0;
+    p.mt_noct = ez - e0 + 2;
+    return p.mt_noct <= NNGP_MT_MAX_OCT;
+}
+
+// Chebyshev nodes of a bin in its local variable f: (1 + cos(pi (k + 1/2) / NC)) / 2, k = 0 .. NC-1
+NNGP_HD double nngp_matern_node(int k) { return 0.5 * (1.0 + cos(3.141592653589793 * (k + 0.5) / NNGP_MT_NC)); }
+
+// t at local variable f of bin b (octave o = b / K, j = b % K): 2^(e0 + o - 1) (1 + (j + f) / K)
+NNGP_HD double nngp_matern_bin_t(const CovParams& p, int b, double f) {
+    const int o = b / NNGP_MT_K, j = b % NNGP_MT_K;
+    return ldexp(1.0 + (j + f) / NNGP_MT_K, p.mt_e0 + o - 1);
+}
+
+// costab[j NC + k] = cos(pi j (k + 1/2) / NC): the discrete cosine transform of the node values
+NNGP_HD void nngp_matern_costab(double* costab) {
+    for (int j = 0; j < NNGP_MT_NC; ++j)
+        for (int k = 0; k < NNGP_MT_NC; ++k) costab[j * NNGP_MT_NC + k] = cos(3.141592653589793 * j * (k + 0.5) / NNGP_MT_NC);
+}
+
+// monomial coefficients in f of bin b's interpolant from rho at the bin's nodes (rho_nodes[k] at
+// nngp_matern_node(k)); octave 0 = 1, the last octave = 0
+NNGP_HD void nngp_matern_bin_fit(const CovParams& p, int b, const double* rho_nodes, const double* costab,
+                                 double* coef) {
+    const int o = b / NNGP_MT_K;
+    for (int k = 0; k < NNGP_MT_NC; ++k) coef[k] = 0.0;
+    if (o == 0) {
+        coef[0] = 1.0;
+        return;
+    }
+    if (o >= p.mt_noct - 1) return;
+    // Chebyshev coefficients c_j in x = 2 f - 1, then sum_j c_j T_j(2 f - 1) in powers of f.  The transform
+    // runs on the deviations from a middle node's value, which is added to the constant term last: every
+    // c_j then carries rounding noise of the bin's variation only, not of rho itself (transforming rho
+    // directly left ~NC ulp of noise in the sum over j, 2.5e-15 near rho = 1)
+    const double vref = rho_nodes[NNGP_MT_NC / 2];
+    double tprev[NNGP_MT_NC], tcur[NNGP_MT_NC], tnext[NNGP_MT_NC];
+    for (int k = 0; k < NNGP_MT_NC; ++k) tprev[k] = tcur[k] = 0.0;
+    tprev[0] = 1.0;             // T_0 = 1
+    tcur[0] = -1.0;             // T_1 = 2 f - 1
+    tcur[1] = 2.0;
+    for (int j = 0; j < NNGP_MT_NC; ++j) {
+        double c = 0.0;
+        for (int k = 0; k < NNGP_MT_NC; ++k) c = fma(rho_nodes[k] - vref, costab[j * NNGP_MT_NC + k], c);
+        c *= (j == 0 ? 1.0 : 2.0) / NNGP_MT_NC;
+        const double* T = j == 0 ? tprev : tcur;
+        for (int k = 0; k < NNGP_MT_NC; ++k) coef[k] = fma(c, T[k], coef[k]);
+        if (j >= 1) {  // T_{j+1} = 2 (2 f - 1) T_j - T_{j-1}
+            for (int k = 0; k < NNGP_MT_NC; ++k)
+                tnext[k] = 4.0 * (k > 0 ? tcur[k - 1] : 0.0) - 2.0 * tcur[k] - tprev[k];
+            for (int k = 0; k < NNGP_MT_NC; ++k) {
+                tprev[k] = tcur[k];
+                tcur[k] = tnext[k];
+            }
+        }
+    }
+    coef[0] += vref;
+}
+
+// rho(phi d) from the table (tab: the launch's table, 16-B aligned), d2 = d^2 from the distance
+NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2) {
+    const double t = d2 * P.mphi2;
+#ifdef NNGP_MATH_HOST
+    int ex;
+    const double mant = frexp(t, &ex);
+    const double s = mant * (2.0 * NNGP_MT_K);  // [K, 2K)
+    const double f = s - floor(s);
+#else
+    const int ex = __builtin_amdgcn_frexp_exp(t);
+    const double s = __builtin_amdgcn_frexp_mant(t) * (2.0 * NNGP_MT_K);
+    const double f = __builtin_amdgcn_fract(s);
+#endif
+    const int j = (int)s - NNGP_MT_K;
+    int o = ex - P.mt_e0;
+    o = o < 0 ? 0 : (o > P.mt_noct - 1 ? P.mt_noct - 1 : o);
+    const double* c = tab + (o * NNGP_MT_K + j) * NNGP_MT_NC;
+    double r = c[NNGP_MT_NC - 1];
+#pragma unroll
+    for (int k = NNGP_MT_NC - 2; k >= 0; --k) r = fma(r, f, c[k]);
+    return r;
+}
+
 #ifndef NNGP_MATH_HOST
 // Fill the block's LDS table tab[j] = sigma2 2^(j/256) (every thread of the block calls it).
 NNGP_FN void nngp_exp_table_load(double* tab, double sigma2) {
@@ -410,6 +533,7 @@ NNGP_FN double nngp_exp_unit(const CovParams& P, const double* tab, double u) {
 // unit-variance covariance of kind KIND at squared distance d2 (tab: nngp_exp_table_load_unit)
 template <int KIND>
 NNGP_FN double nngp_cov_unit(const CovParams& P, const double* tab, double d2) {
+    if (KIND == NNGP_KIND_MATERN) return nngp_matern_tab(P, tab, d2);  // tab: the Matern table
     const double x = fmin(d2, P.d2max);
     if (KIND == NNGP_KIND_GAUSSIAN) return nngp_exp_unit(P, tab, x);
     const double d = nngp_sqrt(x);

@@ -263,11 +263,13 @@ class SeqNNGP:
         self.phi_tuning = float(phi_tuning)
         self.yres = self._residual_y(self.beta)
         if w_init is None:
-            # the reference's state initialisation (_init_ws, nngp.py:45-47: the uniform 5-NN mean of
-            # the responses, KNeighborsRegressor(5).fit(t, y).predict(s)) applied to the responses
-            # less their least-squares mean X beta (the reference has no covariates; the mean stays
-            # with beta, which mixes slowly against a w that carries it): a zero start instead lets
-            # sigma2 | w = 0 collapse towards 0 and the chain stalls there
+            # every node starts at the uniform 5-NN mean of the responses less their least-squares
+            # mean X beta -- the reference's initialiser of ws (_init_ws, nngp.py:45-47,
+            # KNeighborsRegressor(5).fit(t, y).predict(s)) used for all nodes.  (The reference starts
+            # wt, the data locations' state, at y itself, _init_wt nngp.py:42-43; here the 5-NN mean
+            # of y - X beta, so that w does not carry the mean, which stays with beta.)  A zero start
+            # instead lets sigma2 | w = 0 collapse towards 0 and the chain stalls there.
+            # NNGP.oneSample passes ws / wt explicitly (SeqNNGP.set_w), the reference's own starts.
             obs_idx = np.nonzero(observed)[0]
             t_obs = t_dev[torch.from_numpy(obs_idx).to(dev)]
             k = min(5, self.n_obs)
@@ -514,7 +516,12 @@ class SeqNNGP:
             for k, v in meta.get("settings", {}).items():
                 if mine.get(k) != v:
                     raise ValueError(f"checkpoint setting {k}={v!r} does not match this sampler's {mine.get(k)!r}")
-            if meta.get("fingerprint") != self._fingerprint():
+            if "fingerprint" not in meta:
+                import warnings
+
+                warnings.warn("checkpoint predates the data fingerprint (pynngp_amd < 0.2): only sizes, kind, seed "
+                              "and settings were compared -- make sure it was written on the same data", stacklevel=2)
+            elif meta["fingerprint"] != self._fingerprint():
                 raise ValueError("checkpoint was written by a sampler built on different data (coordinates, "
                                  "responses, covariates, noise weights or neighbour sets) or settings")
             to = lambda a: torch.as_tensor(a).to(self.device)  # noqa: E731

@@ -98,8 +98,9 @@ def _sweep(lib, **kw):
     (dict(kind=5, nu=0.0), -1, "nu"),  # general-smoothness Matern: 0 < nu <= 50
     (dict(kind=5, nu=50.5), -1, "nu"),
     (dict(kind=5, nu=float("nan")), -1, "nu"),
-    (dict(kind=5, nu=1.2, algo=5), -4, "wavefront kernel"),
-    (dict(kind=5, nu=1.2, algo=1, m=8), -4, "wavefront kernel"),
+    (dict(kind=5, nu=0.3, algo=5), -4, "table octaves"),  # the pair kernel's Matern table: nu >= ~0.45
+    (dict(kind=5, nu=1.2, algo=1, m=8), -4, "pair kernel (m <= 24) or the wavefront kernel"),
+    (dict(kind=5, nu=1.2, algo=4, m=28), -4, "pair kernel (m <= 24) or the wavefront kernel"),
 ])
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code
@@ -162,8 +163,9 @@ def test_check_partials_codes(lib):
 
 def test_resolve_algo_table(lib):
     """auto: the blocked pair kernel for 1 <= m <= 24 and the four-lane kernel for 25..32 at kinds
-    0..4 and every dimension, the wavefront kernel above and for the general-smoothness Matern
-    kind (5) at every m; explicit codes pass through."""
+    0..4 and every dimension, the wavefront kernel above; the general-smoothness Matern kind (5): the
+    pair kernel with its table for m <= 24 when nu's table fits (nu >= ~0.45), else and above m = 24
+    the wavefront kernel; explicit codes pass through."""
     for m in (1, 15, 20, 24, 25, 32):
         for kind in range(5):
             for dim in (1, 2, 3):
@@ -171,8 +173,15 @@ def test_resolve_algo_table(lib):
     assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
     assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
     assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1
-    for m in (1, 15, 25, 40):
-        assert lib.nngp_resolve_algo(0, m, 5, 2) == 2
+    for m in (1, 15, 24):
+        assert lib.nngp_resolve_algo(0, m, 5, 2) == 5
+        for nu in (0.45, 0.5, 1.0, 2.5, 49.0):
+            assert lib.nngp_resolve_algo_nu(0, m, 5, 2, nu) == 5
+        for nu in (0.05, 0.3, 0.4):
+            assert lib.nngp_resolve_algo_nu(0, m, 5, 2, nu) == 2
+    for m in (25, 40):
+        assert lib.nngp_resolve_algo(0, m, 5, 2) == 2 and lib.nngp_resolve_algo_nu(0, m, 5, 2, 1.5) == 2
+    assert lib.nngp_resolve_algo_nu(2, 15, 5, 2, 1.5) == 2 and lib.nngp_resolve_algo_nu(0, 15, 0, 2, 1.5) == 5
 
 
 def test_finalize_checks_workspace(lib):
@@ -183,6 +192,12 @@ def test_finalize_checks_workspace(lib):
     assert lib.nngp_bf_finalize(P(256), need, 100_000, 15, 9, 2, 0, P(512), None) == -1
     assert lib.nngp_bf_finalize(P(256), need, 100_000, 15, 0, 2, 3, P(512), None) == -1
     assert lib.nngp_bf_finalize(None, need, 100_000, 15, 0, 2, 0, P(512), None) == -1
+    # a matern sweep's records depend on nu (pair kernel with its table, or the wavefront kernel): AUTO is refused
+    need5 = lib.nngp_bf_sweep_workspace_bytes(100_000, 15, 5, 2, 0)
+    assert need5 >= lib.nngp_bf_sweep_workspace_bytes(100_000, 15, 5, 2, 2)
+    assert need5 >= lib.nngp_bf_sweep_workspace_bytes(100_000, 15, 5, 2, 5) > need
+    assert lib.nngp_bf_finalize(P(256), need5, 100_000, 15, 5, 2, 0, P(512), None) == -1
+    assert "resolved algo" in lib.nngp_last_error().decode()
 
 
 def test_blocks_entry_points_reject(lib):

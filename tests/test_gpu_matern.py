@@ -1,4 +1,6 @@
-"""GPU parity: the general-smoothness Matern kind (NNGP_COV_MATERN) on the wavefront kernel.
+"""GPU parity: the general-smoothness Matern kind (NNGP_COV_MATERN): the pair kernel evaluating rho
+from the launch's table (m <= 24, nu >= ~0.45, `auto`) and the wavefront kernel's direct Bessel
+evaluation (smaller nu, m > 24, or algo="wave").
 
 Against the C oracle (oracle/nngp_oracle.c: K_nu by a long-double trapezoidal integral, a method
 independent of the kernel's Temme series / continued fraction) on the same neighbour sets, with
@@ -32,10 +34,10 @@ def _field(n, seed, dim=2):
     return rng.uniform(0.0, 1.0, (n, dim)), rng.standard_normal(n)
 
 
-def _check(dev, lib, O, coords, nbr, theta, nu, y):
+def _check(dev, lib, O, coords, nbr, theta, nu, y, algo="auto"):
     c = torch.from_numpy(coords).to(dev)
     v = None if y is None else torch.from_numpy(y).to(dev)
-    B, F, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", *theta, values=v, nu=nu)
+    B, F, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", *theta, values=v, nu=nu, algo=algo)
     Bo, Fo, po = O.c_bf_sweep(coords, nbr, "matern", tuple(theta) + (nu,), y)
     B, F, p = B.cpu().numpy(), F.cpu().numpy(), p.cpu().numpy()
     assert p[2] == -1 and p[3] == -1
@@ -58,24 +60,38 @@ def _check(dev, lib, O, coords, nbr, theta, nu, y):
     (1.3, (1.0, 10.0, 0.1), 15, 3),
     (2.2, (1.0, 18.0, 0.1), 40, 2),  # the NR = 64 instantiation
     (11.0, (1.0, 60.0, 0.3), 5, 2),
+    (0.45, (1.0, 15.0, 0.05), 15, 2),  # the smallest nu whose table fits
+    (35.0, (1.0, 80.0, 0.1), 20, 2),
+    (1.0, (1.0, 12.0, 0.1), 24, 3),
 ])
-def test_matern_sweep_vs_oracle(lib, dev, c_oracle, nu, theta, m, dim):
+@pytest.mark.parametrize("algo", ["auto", "wave"])
+def test_matern_sweep_vs_oracle(lib, dev, c_oracle, nu, theta, m, dim, algo):
     coords, y = _field(2000, 21 + m, dim)
     nbr = c_oracle.c_knn_prior(coords, m)
-    _check(dev, lib, c_oracle, coords, nbr, theta, nu, y)
+    _check(dev, lib, c_oracle, coords, nbr, theta, nu, y, algo)
 
 
-def test_matern_auto_is_wave_and_explicit_others_fail(lib, dev):
-    assert lib.resolve_algo("auto", 15, "matern", 2) == "wave"
-    coords, y = _field(500, 2)
+def test_matern_kernel_choice_and_explicit(lib, dev):
+    """auto: the pair kernel with the table for m <= 24 and nu >= ~0.45, the wavefront kernel for smaller
+    nu and m > 24; the two kernels agree within the parity tolerances; lane / an uncovered nu on the pair
+    kernel are refused."""
+    assert lib.resolve_algo("auto", 15, "matern", 2, nu=1.2) == "pairb"
+    assert lib.resolve_algo("auto", 15, "matern", 2, nu=0.3) == "wave"
+    assert lib.resolve_algo("auto", 40, "matern", 2, nu=1.2) == "wave"
+    coords, y = _field(5000, 2)
     c = torch.from_numpy(coords).to(dev)
+    v = torch.from_numpy(y).to(dev)
     nb = lib.knn_prior(c, 10)
-    Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=1.2, algo="wave")
-    Ba, Fa, pa = lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=1.2)
-    assert torch.equal(Bw, Ba) and torch.equal(Fw, Fa)
-    for algo in ("pairb", "lane"):
-        with pytest.raises(lib.NNGPExtensionError, match="wavefront kernel"):
-            lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=1.2, algo=algo)
+    Bw, Fw, pw = lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, values=v, nu=1.2, algo="wave")
+    Ba, Fa, pa = lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, values=v, nu=1.2)
+    Bp, Fp, pp = lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, values=v, nu=1.2, algo="pairb")
+    assert torch.equal(Ba, Bp) and torch.equal(Fa, Fp) and torch.equal(pa, pp)
+    assert torch.all((Fa - Fw).abs() <= RTOL_F * Fw) and torch.all((Ba - Bw).abs() <= ATOL_B * (1 + Bw.abs()))
+    assert abs(pa[1].item() - pw[1].item()) <= 1e-11 * abs(pw[1].item())
+    with pytest.raises(lib.NNGPExtensionError, match="pair kernel"):
+        lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=1.2, algo="lane")
+    with pytest.raises(lib.NNGPExtensionError, match="table octaves"):
+        lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=0.3, algo="pairb")
     with pytest.raises(ValueError, match="nu"):
         lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1)
 
@@ -87,8 +103,9 @@ def test_matern_m1_covariance_vs_mpmath(lib, dev, c_oracle):
     sigma2, phi, tau2 = 1.3, 9.0, 0.4
     c = torch.from_numpy(coords).to(dev)
     mp.mp.dps = 40
-    for nu in (0.4, 1.0, 2.3, 7.5):
-        B, _, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", sigma2, phi, tau2, nu=nu)
+    for nu, algo in ((0.4, "auto"), (0.6, "auto"), (1.0, "auto"), (2.3, "auto"), (7.5, "auto"), (42.0, "auto"),
+                     (1.0, "wave"), (7.5, "wave")):  # 0.4: the wavefront kernel; the others through the table
+        B, _, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", sigma2, phi, tau2, nu=nu, algo=algo)
         cov = B.cpu().numpy()[1:, 0] * (sigma2 + tau2)
         j = nbr[1:, 0]
         d2 = (coords[1:, 0] - coords[j, 0]) ** 2 + (coords[1:, 1] - coords[j, 1]) ** 2

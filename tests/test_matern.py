@@ -86,6 +86,52 @@ def test_kernel_rho_limits(kernel_rho):
     assert all(a > b for a, b in zip(r, r[1:]))
 
 
+@pytest.fixture(scope="module")
+def table_rho(tmp_path_factory):
+    """The fused pair kernel's Matern-nu path (nngp_matern_tab over the per-launch table), host build."""
+    exe = str(tmp_path_factory.mktemp("matern_tab") / "matern_table_check")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-std=c++17",
+                    os.path.join(HERE, "host", "matern_table_check.cpp"), "-o", exe, "-lm"], check=True)
+
+    def run(pairs):
+        inp = "\n".join(f"{nu!r} {u!r}" for nu, u in pairs) + "\n"
+        out = subprocess.run([exe], input=inp, check=True, capture_output=True, text=True).stdout.split("\n")
+        rows = [r.split() for r in out if r.strip()]
+        assert len(rows) == len(pairs)
+        return [float.fromhex(r[0]) if r[0] != "nan" else float("nan") for r in rows], [int(r[1]) for r in rows]
+
+    return run
+
+
+TABLE_NUS = tuple(nu for nu in NUS if nu >= 0.45) + (0.45, 1.0000001, 1.97, 2.0, 3.0)
+
+
+def test_table_rho_vs_mpmath(table_rho):
+    """Table path (bins of t = u^2: 4 per octave, degree 13) against mpmath: the same 2e-15 absolute bound as
+    the direct evaluation it is built from, over u from 1e-8 to 20 and at the clamps (u = 0, far)."""
+    rng = np.random.default_rng(9)
+    worst = 0.0
+    for nu in TABLE_NUS:
+        us = list(10 ** rng.uniform(-8, 1.3, 60)) + [1e-30, 1e-3, 0.7, 1.0, 1.5, 2.0, 30.0, 300.0]
+        got, noct = table_rho([(float(nu), float(u)) for u in us])
+        assert all(0 < k <= 160 for k in noct), (nu, noct[0])
+        for u, g in zip(us, got):
+            worst = max(worst, float(abs(g - _ref(nu, u))))
+    assert worst <= 2e-15, worst
+
+
+def test_table_rho_limits_and_range(table_rho):
+    """Coincident points give exactly 1, far points exactly 0 (exact decoupling of padding); nu below the
+    table's range (its octaves from 1 - rho < 1e-18 to rho < 1e-18 exceed 160) reports no table (the
+    sweep then runs the wavefront kernel); rho decreases along a fine grid."""
+    got, noct = table_rho([(1.3, 0.0), (1.3, 1e-200), (1.3, 1e6), (0.7, 0.0), (0.7, 5e3), (0.3, 1.0), (0.05, 1.0)])
+    assert got[0] == 1.0 and got[1] == 1.0 and got[2] == 0.0 and got[3] == 1.0 and got[4] == 0.0
+    assert np.isnan(got[5]) and np.isnan(got[6]) and noct[5] == 0
+    us = np.linspace(0.001, 30.0, 400).tolist()
+    r, _ = table_rho([(2.2, u) for u in us])
+    assert all(a > b for a, b in zip(r, r[1:]))
+
+
 def test_c_oracle_rho_vs_mpmath(c_oracle):
     worst = 0.0
     for nu, u in _grid(5)[::3]:
