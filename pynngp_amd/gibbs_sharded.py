@@ -13,9 +13,11 @@ per-colour halo exchanges").
   the halo rows (a second sweep over a gathered table: same kernel, same operands, so the same
   bits as the owner's rows);
 * per colour: the own members' colour step (``nngp_gibbs_w_color``) publishes the members' new w
-  into a send slot; ONE all-gather per colour; ``nngp_gibbs_w_apply`` replays the draws of the
-  other ranks' members in V (dw from this rank's replica = the owner's operands, so the owner's
-  bits);
+  into a send slot; a halo exchange -- ONE all-gather per colour of only the members some other
+  rank keeps a replica of (the boundary: ``exported``; each rank's run of a colour is ordered
+  boundary members first, so they are the head of the slot) --; ``nngp_gibbs_w_apply`` replays the
+  draws of the other ranks' members in V (dw from this rank's replica = the owner's operands, so
+  the owner's bits);
 * sigma2, tau2, beta: the stats of the own rows, all-gathered and folded in rank order, so every
   rank draws the same scalars from the same host RNG stream.
 
@@ -23,7 +25,8 @@ The chain is the single-GPU chain: the same Philox normals (keyed by location an
 per-location arithmetic; only the summation order of the global sums (the log density of the
 proposal, the conjugate statistics) follows the ranks.  With one rank it is ``SeqNNGP``'s chain
 bit for bit (tests/test_gpu_gibbs_sharded.py).  Cost per iteration on top of the sharded work:
-one all-gather per colour (32 at m = 15) and the replay of the boundary members.
+one all-gather per colour (32 at m = 15) of the boundary members' w (``plan.exchange_bytes`` per
+rank and sweep, against ``plan.allgather_bytes`` for every member) and their replay.
 """
 from __future__ import annotations
 
@@ -47,14 +50,20 @@ class GibbsShardPlan:
     lo: int
     hi: int
     bounds: np.ndarray      # (world + 1,) shard boundaries
-    run: np.ndarray         # (n_colors, world + 1): members[run[c, r]:run[c, r + 1]] = rank r's members of colour c
-    maxc: np.ndarray        # (n_colors,) the largest per-rank run of each colour (the all-gather slot size)
+    run: np.ndarray         # (n_colors, world + 1): members_x[run[c, r]:run[c, r + 1]] = rank r's members of colour c
+    maxc: np.ndarray        # (n_colors,) the largest per-rank run of each colour (the send slot size)
     send_off: np.ndarray    # (n_colors + 1,) colour c's send slot: send[send_off[c]:send_off[c] + maxc[c]]
     recv_off: np.ndarray    # (n_colors + 1,) colour c's gathered block: recv[recv_off[c]:recv_off[c + 1]]
     halo: np.ndarray        # (n_h,) out-of-shard children of the own rows, ascending
     replica: np.ndarray     # (n_v,) V: own rows, halo and the parents of both, ascending
     apply_rows: np.ndarray  # (n_apply, 4) int32 (i, off[i], off[i + 1], src) of the foreign rows of V, by colour
     apply_off: np.ndarray   # (n_colors + 1,)
+    members_x: np.ndarray   # (n,) the members by colour; each (colour, rank) run: boundary members first, ascending
+    exported: np.ndarray    # (n,) bool: the row is in some other rank's replica set V (the boundary)
+    bcount: np.ndarray      # (n_colors, world) boundary members per (colour, rank): the head of each run
+    bmax: np.ndarray        # (n_colors,) the largest bcount of each colour: the all-gather size per rank
+    exchange_bytes: int     # bytes one rank receives per sweep (sum_c world * bmax[c] * 8)
+    allgather_bytes: int    # ... had every member been all-gathered (sum_c world * maxc[c] * 8)
 
 
 def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, rank: int) -> GibbsShardPlan:
@@ -80,7 +89,17 @@ def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, ra
     counts = np.diff(run, axis=1)
     maxc = counts.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
     send_off = np.concatenate([[0], np.cumsum(maxc)]).astype(np.int64)
-    recv_off = np.concatenate([[0], np.cumsum(maxc * world)]).astype(np.int64)
+    exported = gibbs_boundary(nbr, bounds)
+    # each (colour, rank) run ordered boundary members first (ascending), then the rest: the colour
+    # step's publish slot then starts with exactly the values the other ranks replay.  (Members of a
+    # colour are independent and their normals are keyed by location, so the order changes no bit.)
+    key = np.repeat(np.arange(n_colors * world, dtype=np.int64), counts.ravel())  # (colour, rank) run of a slot
+    xo = np.lexsort((members, ~exported[members], key))
+    members_x = members[xo]
+    cs = np.concatenate([[0], np.cumsum(exported[members_x], dtype=np.int64)])
+    bcount = cs[run[:, 1:]] - cs[run[:, :-1]]
+    bmax = bcount.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
+    recv_off = np.concatenate([[0], np.cumsum(bmax * world)]).astype(np.int64)
     # halo: children of the own rows outside the shard; V: own rows, halo, parents of both
     ch = rev_j[off[lo]:off[hi]].astype(np.int64)
     halo = np.unique(ch[(ch < lo) | (ch >= hi)])
@@ -88,17 +107,42 @@ def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, ra
     par = par[(par >= 0) & (par < n)]
     replica = np.unique(np.concatenate([np.arange(lo, hi), halo, par]))
     foreign = replica[(replica < lo) | (replica >= hi)]
+    if not np.all(exported[foreign]):
+        raise AssertionError("a foreign replica row is not on its owner's boundary")
     pos = np.empty(n, dtype=np.int64)
-    pos[members] = np.arange(n)
+    pos[members_x] = np.arange(n)
     cf = colors[foreign]
     owner = np.searchsorted(bounds, foreign, side="right") - 1
-    k = pos[foreign] - run[cf, owner]
-    src = recv_off[cf] + owner * maxc[cf] + k
+    k = pos[foreign] - run[cf, owner]  # rank among the owner's boundary members of the colour
+    src = recv_off[cf] + owner * bmax[cf] + k
     order = np.argsort(cf, kind="stable")
     apply_rows = np.stack([foreign, off[foreign], off[foreign + 1], src], axis=1)[order].astype(np.int32)
     apply_off = np.concatenate([[0], np.cumsum(np.bincount(cf, minlength=n_colors))]).astype(np.int64)
     return GibbsShardPlan(world, rank, lo, hi, bounds, run, maxc, send_off, recv_off, halo, replica,
-                          np.ascontiguousarray(apply_rows), apply_off)
+                          np.ascontiguousarray(apply_rows), apply_off, members_x.astype(np.int32), exported, bcount,
+                          bmax, int(8 * world * bmax.sum()), int(8 * world * maxc.sum()))
+
+
+def gibbs_boundary(nbr, bounds) -> np.ndarray:
+    """exported[i]: row i is in the replica set V(r) = own(r) + H(r) + parents of both of some rank r
+    other than its owner (H(r): the out-of-shard children of own(r)).  i is in V(r), r != owner(i),
+    exactly when i has a parent owned by r (i in H(r)), or i is a parent of a row j that r owns or that
+    has a parent owned by r (i in parents(own(r) + H(r))).  With T(j) = {owner(j)} + owners of j's
+    parents: exported[i] = T(i) != {owner(i)} or T(j) != {owner(i)} for some child j of i -- one pass over
+    the parent lists (nbr, -1 padded), identical on every rank."""
+    nbr = np.asarray(nbr)
+    n = nbr.shape[0]
+    own = np.repeat(np.arange(len(bounds) - 1, dtype=np.int32), np.diff(bounds)).astype(np.int32)
+    valid = (nbr >= 0) & (nbr < n)
+    on = np.where(valid, own[np.where(valid, nbr, 0)], -1)
+    tmin = np.minimum(own, np.where(valid, on, np.iinfo(np.int32).max).min(axis=1)) if nbr.shape[1] else own
+    tmax = np.maximum(own, on.max(axis=1)) if nbr.shape[1] else own
+    exported = (tmin != own) | (tmax != own)
+    jj, ss = np.nonzero(valid)
+    pi = nbr[jj, ss]
+    hit = (tmin[jj] != own[pi]) | (tmax[jj] != own[pi])
+    exported[pi[hit]] = True
+    return exported
 
 
 class ColourExchange:
@@ -114,15 +158,19 @@ class ColourExchange:
         self.n_collectives = 0
 
     def send_slot(self, c: int) -> torch.Tensor:
+        """Colour c's publish slot (maxc[c] values; the head, bmax[c], goes out)."""
         a = int(self.plan.send_off[c])
         return self.send[a:a + int(self.plan.maxc[c])]
 
     def exchange(self, c: int) -> None:
+        """The halo exchange of colour c: every rank's boundary members' new w (the head of its slot,
+        bmax[c] values) all-gathered, (world, bmax[c]) rank-major; nothing when no rank has one."""
         p = self.plan
-        if not self.active or p.maxc[c] == 0:
+        if not self.active or p.bmax[c] == 0:
             return
-        dist.all_gather_into_tensor(self.recv[int(p.recv_off[c]):int(p.recv_off[c + 1])], self.send_slot(c),
-                                    group=self.group)
+        a = int(p.send_off[c])
+        dist.all_gather_into_tensor(self.recv[int(p.recv_off[c]):int(p.recv_off[c + 1])],
+                                    self.send[a:a + int(p.bmax[c])], group=self.group)
         self.n_collectives += 1
 
 
@@ -154,7 +202,8 @@ class ShardedSeqNNGP(SeqNNGP):
                                          self.colors, self.members.cpu().numpy(), self.color_off, self.world,
                                          self.rank)
         self.lo, self.hi = p.lo, p.hi
-        self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
+        # the colour runs in the plan's order (boundary members first: the head of each publish slot)
+        self._member_rows = _lib.gibbs_member_rows(torch.from_numpy(p.members_x).to(dev), self.off)
         self._apply_rows = torch.from_numpy(p.apply_rows).to(dev)
         self._xchg = ColourExchange(p, dev, group, active=self.collective)
         # halo sweep: the halo rows' own points appended to the coordinate table (row n + t = halo[t]),
@@ -265,7 +314,7 @@ class ShardedSeqNNGP(SeqNNGP):
             self._graphs[key] = gr
         gr.replay()
         self._xchg.n_collectives += self._coll_per_range.setdefault((c0, c1), int(
-            sum(1 for c in range(c0, c1) if self.plan.maxc[c] > 0)) if self._xchg.active else 0)
+            sum(1 for c in range(c0, c1) if self.plan.bmax[c] > 0)) if self._xchg.active else 0)
 
     def _colour_loop(self, c0, c1, graph):
         L, p, x = self._L, self.plan, self._xchg
@@ -358,4 +407,4 @@ class ShardedSeqNNGP(SeqNNGP):
         return self
 
 
-__all__ = ["ShardedSeqNNGP", "GibbsShardPlan", "gibbs_shard_plan", "ColourExchange", "ops"]
+__all__ = ["ShardedSeqNNGP", "GibbsShardPlan", "gibbs_shard_plan", "gibbs_boundary", "ColourExchange", "ops"]

@@ -96,8 +96,8 @@ def _single_sweep(P):
 def _rank_colour(P, plan, c, w, r, send):
     a, b = plan.run[c, plan.rank], plan.run[c, plan.rank + 1]
     so = plan.send_off[c]
-    for k, g in enumerate(range(a, b)):
-        send[so + k] = _colour_member(P, P["members"][g], w, r)
+    for k, g in enumerate(range(a, b)):  # the plan's run order: boundary members first
+        send[so + k] = _colour_member(P, plan.members_x[g], w, r)
 
 
 def _rank_apply(P, plan, c, w, r, recv):
@@ -121,8 +121,8 @@ def test_sharded_sweep_equals_single_bitwise(world, storage):
     for c in range(len(P["color_off"]) - 1):
         for k in range(world):
             _rank_colour(P, plans[k], c, W[k], R[k], sends[k])
-        mc, ro = plans[0].maxc[c], plans[0].recv_off[c]
-        for k in range(world):  # the all-gather: rank-major blocks of maxc[c]
+        mc, ro = plans[0].bmax[c], plans[0].recv_off[c]
+        for k in range(world):  # the halo all-gather: the head (bmax[c]) of each rank's slot, rank-major
             recv[ro + k * mc: ro + (k + 1) * mc] = sends[k][plans[0].send_off[c]: plans[0].send_off[c] + mc]
         for k in range(world):
             _rank_apply(P, plans[k], c, W[k], R[k], recv)
@@ -139,6 +139,17 @@ def test_sharded_sweep_equals_single_bitwise(world, storage):
         assert sum(p.apply_rows.shape[0] for p in plans) > 0
         if storage == "sorted":  # spatial shards: the halo is a small part of the shard
             assert all(p.halo.size < p.hi - p.lo for p in plans)
+            # the halo exchange moves the boundary only
+            assert plans[0].exchange_bytes < plans[0].allgather_bytes
+    # every rank's plan agrees on the boundary and the runs' order; the boundary is exactly the union of
+    # the foreign parts of the replica sets
+    union = np.zeros(P["n"], dtype=bool)
+    for p in plans:
+        assert np.array_equal(p.exported, plans[0].exported) and np.array_equal(p.members_x, plans[0].members_x)
+        f = p.replica[(p.replica < p.lo) | (p.replica >= p.hi)]
+        union[f] = True
+    assert np.array_equal(union, plans[0].exported)
+    assert np.array_equal(np.sort(plans[0].members_x), np.sort(P["members"]))
 
 
 def test_plan_sources_point_at_owners():
@@ -147,8 +158,8 @@ def test_plan_sources_point_at_owners():
     plans = [gibbs_shard_plan(P["nbr"], P["off"], P["rev_j"], P["colors"], P["members"], P["color_off"], world, k)
              for k in range(world)]
     pos = np.empty(P["n"], dtype=np.int64)
-    pos[P["members"]] = np.arange(P["n"])
     p0 = plans[0]
+    pos[p0.members_x] = np.arange(P["n"])
     for p in plans:
         for c in range(len(P["color_off"]) - 1):
             rows = p.apply_rows[p.apply_off[c]:p.apply_off[c + 1]]
@@ -156,9 +167,10 @@ def test_plan_sources_point_at_owners():
                 assert P["colors"][i] == c and not (p.lo <= i < p.hi)
                 assert (e0, e1) == (P["off"][i], P["off"][i + 1])
                 blk = src - p0.recv_off[c]
-                owner, k = divmod(int(blk), int(p0.maxc[c]))
+                owner, k = divmod(int(blk), int(p0.bmax[c]))
                 assert plans[owner].lo <= i < plans[owner].hi
-                assert pos[i] == p0.run[c, owner] + k
+                assert pos[i] == p0.run[c, owner] + k and k < p0.bcount[c, owner]
+                assert p0.exported[i]
 
 
 def _free_port():
