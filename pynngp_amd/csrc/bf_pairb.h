@@ -187,7 +187,14 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
          : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_lk(M, KIND) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
         ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3 : 2))))
 
-// Threads per block (one tile of kPairbThreads / 2 locations per block).  256 measured fastest:
+// waves per SIMD the kernel for (m, kind) is built for (NNGP_PAIRB_ATTR's minimum): blocks per CU
+constexpr int pairb_waves_per_simd(int m, int kind) {
+    return (m <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(m, kind)) ? 3
+           : (m <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_lk(m, kind) && m < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2
+                                                                                                     : 1;
+}
+
+// Threads per block (one tile of up to kPairbThreads / 2 locations per block).  256 measured fastest:
 // 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
 // config 3 and +5 % / +1 % at config 2 (same-box A/B).
 #ifndef NNGP_PAIRB_THREADS
@@ -195,7 +202,34 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 #endif
 constexpr int kPairbThreads = NNGP_PAIRB_THREADS;
 constexpr int kPairbWaves = kPairbThreads / 64;
-constexpr int kPairbTile = kPairbThreads / 2;  // locations per tile
+constexpr int kPairbTile = kPairbThreads / 2;  // locations per tile (at most)
+constexpr int kDeviceCUs = 256;                 // MI355X (gfx950): 8 XCDs x 32 CUs
+
+// Tiling of n_rows locations (round 4).  A SIMD running one wave alone issues it ~1.2x slower than
+// each of two paired waves (dependency latency; tools/ubench/valu_mix), so a last round
+// of blocks that fills the device only partly (config 2: 782 tiles of 128 on 512 two-wave block
+// slots -- 1.53 rounds) costs a lone-wave round.  The tiles are therefore made a whole number of
+// rounds of the device's block slots (256 CUs x blocks per CU), each tile holding q or q + 1 rows
+// (config 2: 1,024 tiles of 97-98 rows; config 3: 8,192 of 122-123), as long as every wave of a tile
+// keeps a live row (q > 96); else the plain 128-row tiling.
+struct PairbTiling {
+    int64_t tiles, q, rem;  // tiles; tile t holds q + (t < rem) rows starting at t q + min(t, rem)
+};
+inline PairbTiling pairb_tiling(int64_t n_rows, int m, int kind) {
+    const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
+    if (T == 0) return {0, 0, 0};
+    const int64_t C = (int64_t)kDeviceCUs * pairb_waves_per_simd(m, kind);
+    const int64_t Tb = (T + C - 1) / C * C;
+    const int64_t t = (Tb > T && n_rows / Tb > 3 * 32) ? Tb : T;
+    return {t, n_rows / t, n_rows % t};
+}
+// the most tiles any (m, kind) uses for n_rows (workspace sizing): T + C - 1 with C <= 3 x 256, and
+// balanced tilings keep more than 96 rows per tile
+inline int64_t pairb_tiles_bound(int64_t n_rows) {
+    const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
+    const int64_t b = T + 3 * kDeviceCUs - 1 < n_rows / 97 ? T + 3 * kDeviceCUs - 1 : n_rows / 97;
+    return b > T ? b : T;
+}
 
 // Tile record fold: wave butterflies (fixed order), then the 4 waves in order by thread 0.
 // lm: product of the lanes' F mantissas (each in [0.5, 1); 128 of them stay above 2^-128),
@@ -262,7 +296,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 const double* __restrict__ qvalues, double* __restrict__ Bout,
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim,
-                                                const double* __restrict__ cblk) {
+                                                const double* __restrict__ cblk, int64_t tq, int64_t trem,
+                                                int64_t* __restrict__ hdr) {
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
@@ -299,6 +334,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
     __shared__ double sh[1][kPairbWaves][5];
     const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = gridDim.x;  // the tile count, for the record fold
     const int q = (int)(threadIdx.x & 1);
     const bool q1 = q == 1;
     const bool lead0 = !q1;
@@ -306,8 +342,9 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     uint32_t mask1 = q1 ? 0xffffffffu : 0u;
     asm volatile("" : "+v"(mask1));  // opaque to the optimizer (see pr_pick)
     {
-        const int64_t r = tile * kPairbTile + (threadIdx.x >> 1);
-        const bool live = r < n_rows;
+        const int64_t lr = threadIdx.x >> 1;  // the tile's local row (pairb_tiling)
+        const int64_t r = tile * tq + (tile < trem ? tile : trem) + lr;
+        const bool live = lr < tq + (tile < trem ? 1 : 0);
         const int64_t rl = live ? r : n_rows - 1;
         // branch-free (a branch here makes the compiler drain every outstanding load, the
         // early exp-table fetch included, at the join): without an order, read nbr's word
@@ -773,25 +810,28 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     }
 }
 
-inline int64_t bf_pairb_tiles(int64_t n_rows) { return (n_rows + kPairbTile - 1) / kPairbTile; }
-
-// workspace: tile records (32 B each), tile exponent sums (4 B each)
+// workspace: a 256-B header (int64 tile count, written by the sweep and read by the fold), the tile
+// records (32 B each) and the tile exponent sums (4 B each), sized for pairb_tiles_bound(n_rows)
 inline size_t pairb_align(size_t b) { return (b + 255) & ~(size_t)255; }
+constexpr size_t kPairbHeader = 256;
 inline size_t bf_pairb_workspace_bytes(int64_t n_rows) {
-    const int64_t t = bf_pairb_tiles(n_rows);
-    return t > 0 ? pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) : 0;
+    const int64_t t = pairb_tiles_bound(n_rows);
+    return t > 0 ? kPairbHeader + pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) : 0;
 }
+inline int64_t* pairb_hdr(void* ws) { return (int64_t*)ws; }
+inline double4* pairb_rec(void* ws) { return (double4*)((char*)ws + kPairbHeader); }
 inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
-    return (int32_t*)((char*)ws + pairb_align((size_t)bf_pairb_tiles(n_rows) * 32));
+    return (int32_t*)((char*)ws + kPairbHeader + pairb_align((size_t)pairb_tiles_bound(n_rows) * 32));
 }
 
 template <int M, int KIND, int D>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
-    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)bf_pairb_tiles(a.n_rows)), dim3(kPairbThreads), lds, s, a.coords,
+    const PairbTiling tl = pairb_tiling(a.n_rows, M, KIND);
+    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)tl.tiles), dim3(kPairbThreads), lds, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
-                       a.qcoords, a.qvalues, a.B, a.F, a.R, (double4*)a.bpart, pairb_lexp(a.bpart, a.n_rows), a.dim,
-                       a.cblk);
+                       a.qcoords, a.qvalues, a.B, a.F, a.R, pairb_rec(a.bpart), pairb_lexp(a.bpart, a.n_rows), a.dim,
+                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart));
 }
 
 // m = 25..32: one instantiation per m for every kind and dimension (runtime kind NNGP_KIND_GENERIC,

@@ -229,10 +229,12 @@ __device__ __forceinline__ void mant_norm(double& m, double& e) {
 }
 
 __global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restrict__ rec,
-                                                          const int32_t* __restrict__ lexp, int64_t n_tiles,
+                                                          const int32_t* __restrict__ lexp,
+                                                          const int64_t* __restrict__ hdr,
                                                           double* __restrict__ partials) {
     __shared__ double sh[16][5];
     const int t = threadIdx.x;
+    const int64_t n_tiles = hdr[0];  // the sweep's tile count (pairb_tiling; written by its block 0)
     double a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;  // a: mantissa product, e: exponent sum
     // 8 records per thread in flight per round: 8,192 records (N ~ 10^6) in one memory round trip.
     // A product of 8 mantissas in [1/2, 1) stays above 2^-8: one renormalisation per round.
@@ -292,8 +294,8 @@ __global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restr
 }
 
 hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, hipStream_t s) {
-    hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(1024), 0, s, (const double4*)ws, pairb_lexp(ws, n_rows),
-                       bf_pairb_tiles(n_rows), partials);
+    hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(1024), 0, s, (const double4*)pairb_rec(ws),
+                       pairb_lexp(ws, n_rows), (const int64_t*)pairb_hdr(ws), partials);
     return hipGetLastError();
 }
 
@@ -357,7 +359,7 @@ static bool launch_lane_m(const BfArgs& a, const CovParams& P, hipStream_t s) {
 int64_t bf_record_count(int64_t n_rows, int algo, int m) {
     if (n_rows == 0) return 0;
     if (algo == kAlgoLane) return bf_lane_blocks(n_rows);
-    if (algo == kAlgoPairB) return bf_pairb_tiles(n_rows);
+    if (algo == kAlgoPairB) return pairb_tiles_bound(n_rows);
     if (algo == kAlgoQuad) return bf_group_blocks(n_rows, 4);
     return bf_wave_blocks(n_rows);
 }

@@ -48,11 +48,16 @@ def test_version_and_loglik_helper(lib):
 def test_workspace_sizes(lib):
     # (n_rows, m, kind, dim, algo): the blocked pair kernel keeps one 32-B record and one 4-B exponent
     # per 128-location tile, the lane kernel a record per 256 rows
+    # (a 256-B header with the tile count; records for the most tiles a balanced tiling uses: the plain
+    # 128-row tiles plus up to one round of 3 x 256 block slots, at more than 96 rows per tile)
     al = lambda b: (b + 255) // 256 * 256  # noqa: E731
     tiles = (1_000_000 + 127) // 128
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 0) == al(32 * tiles) + al(4 * tiles)
+    bound = max(tiles, min(tiles + 767, 1_000_000 // 97))
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 15, 0, 2, 0) == 256 + al(32 * bound) + al(4 * bound)
     assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 0, 2, 0) >= 4 * 8 * (1_000_000 // 256)
-    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 3, 2, 0) == al(32 * tiles) + al(4 * tiles)
+    assert lib.nngp_bf_sweep_workspace_bytes(1_000_000, 8, 3, 2, 0) == 256 + al(32 * bound) + al(4 * bound)
+    small = lib.nngp_bf_sweep_workspace_bytes(1000, 15, 0, 2, 0)  # bound max(8, min(8 + 767, 1000 // 97))
+    assert small == 256 + al(32 * 10) + al(4 * 10)
     assert lib.nngp_bf_sweep_workspace_bytes(-1, 15, 0, 2, 0) == 0
     assert lib.nngp_bf_sweep_workspace_bytes(0, 15, 0, 2, 0) == 0
     assert lib.nngp_bf_sweep_workspace_bytes(10, 40, 0, 3, 0) > 0
