@@ -64,6 +64,7 @@ int main(int argc, char** argv) {
     CHECK_HIP(hipMalloc((void**)&d_p, sizeof(double) * 4));
     CHECK_HIP(hipMalloc(&ws_knn, knn_bytes));
     CHECK_HIP(hipMalloc(&ws_bf, bf_bytes > 0 ? bf_bytes : 256));
+    CHECK_HIP(hipMemset(ws_bf, 0, 256)); /* the sweep workspace's header starts at zero (nngp.h) */
     CHECK_HIP(hipMemcpy(d_xy, xy, sizeof(double) * 2 * n, hipMemcpyHostToDevice));
     CHECK_HIP(hipMemcpy(d_v, v, sizeof(double) * n, hipMemcpyHostToDevice));
 

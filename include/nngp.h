@@ -147,7 +147,10 @@ int nngp_knn_query(const double *ref, int64_t n_ref, int32_t dim, const double *
  * partials: 4 doubles, or NULL to defer the final fold: the per-block records stay in
  * the workspace and nngp_bf_finalize (same n_rows, m, kind, dim, algo) folds them later,
  * e.g. on another stream while the next sweep (with another workspace) runs.
- * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo) bytes, 256-B aligned.
+ * workspace: nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo) bytes, 256-B aligned, its first
+ * 256 bytes zeroed once before the first sweep that uses it (the pair kernel's header: its tile count
+ * and the ticket of the fold a small sweep does in its last block, which every sweep leaves at zero;
+ * the same holds for nngp_bf_cross and nngp_bf_sweep_blocks workspaces).
  * kind, sigma2 > 0, phi > 0, tau2 >= 0: the covariance (the reference's `cov`); nu: the smoothness
  * of NNGP_COV_MATERN (0 < nu <= 50), ignored by the other kinds.
  * ------------------------------------------------------------------------- */

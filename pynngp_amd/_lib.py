@@ -215,8 +215,11 @@ def _stream(dev: torch.device):
 
 
 def _workspace(nbytes: int, dev: torch.device) -> torch.Tensor:
-    # torch's caching allocator returns >= 512-byte aligned blocks
-    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+    # torch's caching allocator returns >= 512-byte aligned blocks; the first 256 bytes (the pair kernel's
+    # header: tile count and the fused fold's ticket) start at zero, as include/nngp.h requires
+    ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+    ws[:256].zero_()
+    return ws
 
 
 def _as_coords(coords: torch.Tensor) -> torch.Tensor:

@@ -215,9 +215,13 @@ constexpr int kDeviceCUs = 256;                 // MI355X (gfx950): 8 XCDs x 32 
 struct PairbTiling {
     int64_t tiles, q, rem;  // tiles; tile t holds q + (t < rem) rows starting at t q + min(t, rem)
 };
+#ifndef NNGP_PAIRB_BALANCE  // 0: plain 128-row tiles (A/B builds)
+#define NNGP_PAIRB_BALANCE 1
+#endif
 inline PairbTiling pairb_tiling(int64_t n_rows, int m, int kind) {
     const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
     if (T == 0) return {0, 0, 0};
+    if (!NNGP_PAIRB_BALANCE) return {T, n_rows / T, n_rows % T};
     const int64_t C = (int64_t)kDeviceCUs * pairb_waves_per_simd(m, kind);
     const int64_t Tb = (T + C - 1) / C * C;
     const int64_t t = (Tb > T && n_rows / Tb > 3 * 32) ? Tb : T;
@@ -274,6 +278,125 @@ __device__ __forceinline__ void pairb_tile_fold(double (*sh)[kPairbWaves][5], in
     lexp[tile] = (int32_t)le + __builtin_amdgcn_frexp_exp(lm);
 }
 
+// ---- the fixed-order fold of the tile records (the separate finalize kernel and the sweep's fused
+// last-block fold run this same code with kPairbThreads threads, so their bits agree).
+// rec[t] = (mantissa product m_t in [1/2, 1), sum r^2/F, bad-pivot row, bad-index row), lexp[t] =
+// exponent sum e_t.  sum log F = log(prod_t m_t) + (sum_t e_t) ln 2: the mantissas are multiplied
+// (renormalised by frexp after every product, exponents summed exactly as integers) and ONE log is
+// taken at the end -- a log per record made the single-block fold 10 us at 7,813 records.
+// Row reduction (16 lanes) by four DPP steps -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror -- after which every lane of a row holds the row's result (each step combines a lane
+// with one partner, a op b == b op a, so all 16 lanes agree bit for bit); the four row results are
+// then read from lanes 0, 16, 32, 48 and combined in that order.
+template <int OP>  // 0: sum, 1: product, 2: min
+__device__ __forceinline__ double fold_op(double a, double b) {
+    return OP == 0 ? a + b : OP == 1 ? a * b : fmin(a, b);
+}
+template <int OP>
+__device__ __forceinline__ double wave_fold_dpp(double v) {
+    v = fold_op<OP>(v, dpp_f64<0xB1>(v));
+    v = fold_op<OP>(v, dpp_f64<0x4E>(v));
+    v = fold_op<OP>(v, dpp_f64<0x141>(v));
+    v = fold_op<OP>(v, dpp_f64<0x140>(v));
+    const long long u = __double_as_longlong(v);
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        r[k] = __hiloint2double(__builtin_amdgcn_readlane((int)(u >> 32), 16 * k),
+                                __builtin_amdgcn_readlane((int)(u & 0xffffffffll), 16 * k));
+    return fold_op<OP>(fold_op<OP>(r[0], r[1]), fold_op<OP>(r[2], r[3]));
+}
+
+// m in [1/2, 1) and its exponent moved into e (exact: e holds integers far below 2^53)
+__device__ __forceinline__ void mant_norm(double& m, double& e) {
+    e += (double)__builtin_amdgcn_frexp_exp(m);
+    m = __builtin_amdgcn_frexp_mant(m);
+}
+
+// COHERENT: the records were written by other blocks of the running kernel (the fused fold): read at
+// agent scope (past this XCD's non-coherent L2)
+template <bool COHERENT>
+__device__ __forceinline__ double4 pairb_rec_load(const double4* rec, int64_t k) {
+    if constexpr (COHERENT) {
+        const double* p = (const double*)(rec + k);
+        return make_double4(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    } else {
+        return rec[k];
+    }
+}
+template <bool COHERENT>
+__device__ __forceinline__ int32_t pairb_lexp_load(const int32_t* lexp, int64_t k) {
+    if constexpr (COHERENT) return __hip_atomic_load(lexp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return lexp[k];
+}
+
+template <bool COHERENT = false>
+__device__ __forceinline__ void pairb_fold_records(const double4* __restrict__ rec, const int32_t* __restrict__ lexp,
+                                                   int64_t n_tiles, double* __restrict__ partials,
+                                                   double (*sh)[5]) {
+    constexpr int NT = kPairbThreads;
+    const int t = threadIdx.x;
+    double a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;  // a: mantissa product, e: exponent sum
+    // 8 records per thread in flight per round; a product of 8 mantissas in [1/2, 1) stays above 2^-8:
+    // one renormalisation per round
+    for (int64_t k0 = t; k0 < n_tiles; k0 += 8 * NT) {
+        double4 r[8];
+        int32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = k0 + (int64_t)u * NT;
+            r[u] = k < n_tiles ? pairb_rec_load<COHERENT>(rec, k) : make_double4(1.0, 0.0, INFINITY, INFINITY);
+            x[u] = k < n_tiles ? pairb_lexp_load<COHERENT>(lexp, k) : 0;
+        }
+        double pm = 1.0;
+        int32_t pe = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            pm *= r[u].x;
+            pe += x[u];
+            b += r[u].y;
+            c = fmin(c, r[u].z);
+            d = fmin(d, r[u].w);
+        }
+        a *= pm;
+        e += (double)pe;
+        mant_norm(a, e);
+    }
+    // one wave: 64 mantissas in [1/2, 1) multiply to no less than 2^-64
+    a = wave_fold_dpp<1>(a);
+    e = wave_fold_dpp<0>(e);
+    mant_norm(a, e);
+    b = wave_fold_dpp<0>(b);
+    c = wave_fold_dpp<2>(c);
+    d = wave_fold_dpp<2>(d);
+    if ((t & 63) == 0) {
+        sh[t >> 6][0] = a;
+        sh[t >> 6][1] = e;
+        sh[t >> 6][2] = b;
+        sh[t >> 6][3] = c;
+        sh[t >> 6][4] = d;
+    }
+    __syncthreads();
+    if (t == 0) {  // the wave results in wave order
+        a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) {
+            a *= sh[w][0];
+            e += sh[w][1];
+            b += sh[w][2];
+            c = fmin(c, sh[w][3]);
+            d = fmin(d, sh[w][4]);
+        }
+        partials[0] = fma(e, 0.6931471805599453, log(a));
+        partials[1] = b;
+        partials[2] = c == INFINITY ? -1.0 : c;
+        partials[3] = d == INFINITY ? -1.0 : d;
+    }
+}
+
 // 1/x to ~1 ulp for a positive normal x: v_rcp_f64 (~2^-26) and one second-order correction
 // y (1 + e + e^2), e = 1 - x y (3 ops; the e^3 term is below 2^-78; two Newton steps are 4)
 __device__ __forceinline__ double pr_rcp(double x) {
@@ -297,7 +420,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim,
                                                 const double* __restrict__ cblk, int64_t tq, int64_t trem,
-                                                int64_t* __restrict__ hdr) {
+                                                int64_t* __restrict__ hdr, double* __restrict__ fused) {
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
@@ -806,11 +929,55 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                          lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)i : INFINITY,
                          (live && bad_index) ? (double)i : INFINITY, sh, 0, rec, lexp, tile);
         __syncthreads();
-        if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
+        if (fused == nullptr) {
+            if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
+            return;
+        }
+        // fused fold (small sweeps, NNGP_PAIRB_FUSED_FOLD_MAX_ROWS): the record goes out at agent scope,
+        // a ticket counts the finished tiles, and the last tile's block folds every record (the same
+        // pairb_fold_records as the separate finalize kernel) -- one launch per sweep instead of two.
+        // The ticket (the workspace header's second word) is zero before the first sweep and reset by
+        // the last block.
+        __shared__ int last;
+        if (threadIdx.x == 0) {
+            double lm = 1.0, le = 0.0, qq = 0.0, bp = INFINITY, bi = INFINITY;
+#pragma unroll
+            for (int k = 0; k < kPairbWaves; ++k) {
+                lm *= sh[0][k][0];
+                le += sh[0][k][1];
+                qq += sh[0][k][2];
+                bp = fmin(bp, sh[0][k][3]);
+                bi = fmin(bi, sh[0][k][4]);
+            }
+            double* rp = (double*)(rec + tile);
+            __hip_atomic_store(rp, __builtin_amdgcn_frexp_mant(lm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(rp + 1, qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(rp + 2, bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(rp + 3, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(lexp + tile, (int32_t)le + __builtin_amdgcn_frexp_exp(lm), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            // release: the record's stores complete (vmcnt counts stores on gfx9) before the ticket
+            __builtin_amdgcn_s_waitcnt(0);
+            unsigned int* ticket = (unsigned int*)(hdr + 1);
+            const unsigned int old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = old == gridDim.x - 1;
+            if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (last) {
+            __shared__ double fsh[kPairbWaves][5];
+            pairb_fold_records<true>(rec, lexp, (int64_t)gridDim.x, fused, fsh);
+        }
     }
 }
 
-// workspace: a 256-B header (int64 tile count, written by the sweep and read by the fold), the tile
+// Fused record fold (one launch per sweep) up to this many rows; 0: always the separate fold kernel.
+#ifndef NNGP_PAIRB_FUSED_FOLD_MAX_ROWS
+#define NNGP_PAIRB_FUSED_FOLD_MAX_ROWS 0
+#endif
+
+// workspace: a 256-B header (int64 tile count, written by the sweep and read by the fold; uint32
+// ticket of the fused fold, zero between sweeps), the tile
 // records (32 B each) and the tile exponent sums (4 B each), sized for pairb_tiles_bound(n_rows)
 inline size_t pairb_align(size_t b) { return (b + 255) & ~(size_t)255; }
 constexpr size_t kPairbHeader = 256;
@@ -819,6 +986,10 @@ inline size_t bf_pairb_workspace_bytes(int64_t n_rows) {
     return t > 0 ? kPairbHeader + pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) : 0;
 }
 inline int64_t* pairb_hdr(void* ws) { return (int64_t*)ws; }
+// the sweep folds its own records when the caller wants the partials now and the sweep is small
+inline bool pairb_fuse_fold(const BfArgs& a) {
+    return a.partials != nullptr && a.n_rows > 0 && a.n_rows <= (int64_t)NNGP_PAIRB_FUSED_FOLD_MAX_ROWS;
+}
 inline double4* pairb_rec(void* ws) { return (double4*)((char*)ws + kPairbHeader); }
 inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
     return (int32_t*)((char*)ws + kPairbHeader + pairb_align((size_t)pairb_tiles_bound(n_rows) * 32));
@@ -831,7 +1002,7 @@ static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s
     hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)tl.tiles), dim3(kPairbThreads), lds, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
                        a.qcoords, a.qvalues, a.B, a.F, a.R, pairb_rec(a.bpart), pairb_lexp(a.bpart, a.n_rows), a.dim,
-                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart));
+                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart), pairb_fuse_fold(a) ? a.partials : nullptr);
 }
 
 // m = 25..32: one instantiation per m for every kind and dimension (runtime kind NNGP_KIND_GENERIC,

@@ -193,108 +193,18 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
     }
 }
 
-// fixed-order fold of bf_pairb's tile records: rec[t] = (mantissa product m_t in [1/2, 1),
-// sum r^2/F, bad-pivot row, bad-index row), lexp[t] = exponent sum e_t.  sum log F =
-// log(prod_t m_t) + (sum_t e_t) ln 2: the mantissas are multiplied (renormalised by frexp
-// after every product, exponents summed exactly as integers) and ONE log is taken at the
-// end -- a log per record made the single-block fold 10 us at 7,813 records.
-// Row reduction (16 lanes) by four DPP steps -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
-// row_mirror -- after which every lane of a row holds the row's result (each step combines
-// a lane with one partner, a op b == b op a, so all 16 lanes agree bit for bit); the four
-// row results are then read from lanes 0, 16, 32, 48 and combined in that order.  DPP
-// moves take a few cycles where a ds_bpermute butterfly step waits on the LDS pipe.
-template <int OP>  // 0: sum, 1: product, 2: min
-__device__ __forceinline__ double fold_op(double a, double b) {
-    return OP == 0 ? a + b : OP == 1 ? a * b : fmin(a, b);
-}
-template <int OP>
-__device__ __forceinline__ double wave_fold_dpp(double v) {
-    v = fold_op<OP>(v, dpp_f64<0xB1>(v));
-    v = fold_op<OP>(v, dpp_f64<0x4E>(v));
-    v = fold_op<OP>(v, dpp_f64<0x141>(v));
-    v = fold_op<OP>(v, dpp_f64<0x140>(v));
-    const long long u = __double_as_longlong(v);
-    double r[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        r[k] = __hiloint2double(__builtin_amdgcn_readlane((int)(u >> 32), 16 * k),
-                                __builtin_amdgcn_readlane((int)(u & 0xffffffffll), 16 * k));
-    return fold_op<OP>(fold_op<OP>(r[0], r[1]), fold_op<OP>(r[2], r[3]));
-}
-
-// m in [1/2, 1) and its exponent moved into e (exact: e holds integers far below 2^53)
-__device__ __forceinline__ void mant_norm(double& m, double& e) {
-    e += (double)__builtin_amdgcn_frexp_exp(m);
-    m = __builtin_amdgcn_frexp_mant(m);
-}
-
-__global__ __launch_bounds__(1024) void bf_finalize_pairb(const double4* __restrict__ rec,
-                                                          const int32_t* __restrict__ lexp,
-                                                          const int64_t* __restrict__ hdr,
-                                                          double* __restrict__ partials) {
-    __shared__ double sh[16][5];
-    const int t = threadIdx.x;
-    const int64_t n_tiles = hdr[0];  // the sweep's tile count (pairb_tiling; written by its block 0)
-    double a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;  // a: mantissa product, e: exponent sum
-    // 8 records per thread in flight per round: 8,192 records (N ~ 10^6) in one memory round trip.
-    // A product of 8 mantissas in [1/2, 1) stays above 2^-8: one renormalisation per round.
-    for (int64_t k0 = t; k0 < n_tiles; k0 += 8 * 1024) {
-        double4 r[8];
-        int32_t x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t k = k0 + (int64_t)u * 1024;
-            r[u] = k < n_tiles ? rec[k] : make_double4(1.0, 0.0, INFINITY, INFINITY);
-            x[u] = k < n_tiles ? lexp[k] : 0;
-        }
-        double pm = 1.0;
-        int32_t pe = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            pm *= r[u].x;
-            pe += x[u];
-            b += r[u].y;
-            c = fmin(c, r[u].z);
-            d = fmin(d, r[u].w);
-        }
-        a *= pm;
-        e += (double)pe;
-        mant_norm(a, e);
-    }
-    // one wave: 64 mantissas in [1/2, 1) multiply to no less than 2^-64
-    a = wave_fold_dpp<1>(a);
-    e = wave_fold_dpp<0>(e);
-    mant_norm(a, e);
-    b = wave_fold_dpp<0>(b);
-    c = wave_fold_dpp<2>(c);
-    d = wave_fold_dpp<2>(d);
-    if ((t & 63) == 0) {
-        sh[t >> 6][0] = a;
-        sh[t >> 6][1] = e;
-        sh[t >> 6][2] = b;
-        sh[t >> 6][3] = c;
-        sh[t >> 6][4] = d;
-    }
-    __syncthreads();
-    if (t == 0) {  // the 16 wave results in wave order
-        a = 1.0, e = 0.0, b = 0.0, c = INFINITY, d = INFINITY;
-#pragma unroll
-        for (int w = 0; w < 16; ++w) {
-            a *= sh[w][0];
-            e += sh[w][1];
-            b += sh[w][2];
-            c = fmin(c, sh[w][3]);
-            d = fmin(d, sh[w][4]);
-        }
-        partials[0] = fma(e, 0.6931471805599453, log(a));
-        partials[1] = b;
-        partials[2] = c == INFINITY ? -1.0 : c;
-        partials[3] = d == INFINITY ? -1.0 : d;
-    }
+// the separate fold of bf_pairb's tile records (pairb_fold_records, bf_pairb.h): one block of the same
+// kPairbThreads threads as the sweep's fused fold, so both give the same bits
+__global__ __launch_bounds__(kPairbThreads) void bf_finalize_pairb(const double4* __restrict__ rec,
+                                                                   const int32_t* __restrict__ lexp,
+                                                                   const int64_t* __restrict__ hdr,
+                                                                   double* __restrict__ partials) {
+    __shared__ double sh[kPairbWaves][5];
+    pairb_fold_records(rec, lexp, hdr[0], partials, sh);
 }
 
 hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, hipStream_t s) {
-    hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(1024), 0, s, (const double4*)pairb_rec(ws),
+    hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(kPairbThreads), 0, s, (const double4*)pairb_rec(ws),
                        pairb_lexp(ws, n_rows), (const int64_t*)pairb_hdr(ws), partials);
     return hipGetLastError();
 }
@@ -396,7 +306,7 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         ok = bf_pairb_launch(b, Pu, s);
         if (!ok) return hipErrorInvalidValue;
         hipError_t e = hipGetLastError();
-        if (e != hipSuccess || a.partials == nullptr) return e;
+        if (e != hipSuccess || a.partials == nullptr || pairb_fuse_fold(a)) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoQuad) {
         ok = bf_group_launch(a, P, 4, s);

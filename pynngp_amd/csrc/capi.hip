@@ -240,7 +240,7 @@ int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* o
     if (!(group ? nngp::bf_group_blocks_launch(args, s) : nngp::bf_pairb_blocks_launch(args, s)))
         return fail(NNGP_EUNSUP, "no covariance-block kernel for m=%d", m);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess)
+    if (e == hipSuccess && !(!group && nngp::pairb_fuse_fold(args)))
         e = group ? nngp::bf_finalize_launch((const double*)workspace, nngp::bf_group_blocks(n_rows, 4), partials, s)
                   : nngp::bf_finalize_pairb_launch(workspace, n_rows, partials, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep_blocks launch");

@@ -1,32 +1,65 @@
 // Per-launch table of the Matern-nu correlation for the fused pair kernel (nngp_math.h, "Matern-nu by
-// table"): one block per octave of t = (phi d)^2; its 4 bins x 14 Chebyshev nodes evaluate rho with the
-// direct Temme / continued-fraction evaluation (nngp_matern_rho) at full lane use, then one thread per bin
-// turns the node values into the bin's monomial coefficients (nngp_matern_bin_fit, the same code as the
-// host check tests/host/matern_table_check.cpp).  Stream-ordered before the sweep that reads it.
+// table"), stream-ordered before the sweep that reads it.
 #include "nngp_internal.h"
 #include "nngp_math.h"
 
 namespace nngp {
 
+// coefficients of f^k in the shifted Chebyshev polynomial T_j(2 f - 1) (exact integers; rows j, columns k)
+__constant__ double kShiftedCheb[NNGP_MT_NC][NNGP_MT_NC] = {
+    {1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 2.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -8.0, 8.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 18.0, -48.0, 32.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -32.0, 160.0, -256.0, 128.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 50.0, -400.0, 1120.0, -1280.0, 512.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -72.0, 840.0, -3584.0, 6912.0, -6144.0, 2048.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 98.0, -1568.0, 9408.0, -26880.0, 39424.0, -28672.0, 8192.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -128.0, 2688.0, -21504.0, 84480.0, -180224.0, 212992.0, -131072.0, 32768.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+    {-1.0, 162.0, -4320.0, 44352.0, -228096.0, 658944.0, -1118208.0, 1105920.0, -589824.0, 131072.0, 0.0, 0.0, 0.0, 0.0},
+    {1.0, -200.0, 6600.0, -84480.0, 549120.0, -2050048.0, 4659200.0, -6553600.0, 5570560.0, -2621440.0, 524288.0, 0.0, 0.0, 0.0},
+    {-1.0, 242.0, -9680.0, 151008.0, -1208064.0, 5637632.0, -16400384.0, 30638080.0, -36765696.0, 27394048.0, -11534336.0, 2097152.0, 0.0, 0.0},
+    {1.0, -288.0, 13728.0, -256256.0, 2471040.0, -14057472.0, 50692096.0, -120324096.0, 190513152.0, -199229440.0, 132120576.0, -50331648.0, 8388608.0, 0.0},
+    {-1.0, 338.0, -18928.0, 416416.0, -4759040.0, 32361472.0, -141213696.0, 412778496.0, -825556992.0, 1133117440.0, -1049624576.0, 627048448.0, -218103808.0, 33554432.0},
+};
+
+// One block per octave of t: its NNGP_MT_K bins x NNGP_MT_NC nodes evaluate rho with the direct evaluation
+// (nngp_matern_rho; the Temme / continued-fraction loops are the kernel's critical path), then the fit of
+// nngp_matern_bin_fit in parallel -- one thread per (bin, Chebyshev coefficient) for the transform of the
+// deviations from the middle node's value, one per (bin, power of f) for the monomial coefficients --
+// with the same sums in the same order as the serial host version.
 __global__ __launch_bounds__(64) void matern_table_kernel(const CovParams P, double* __restrict__ tab) {
     static_assert(NNGP_MT_K * NNGP_MT_NC <= 64, "one node per thread");
     __shared__ double rho[NNGP_MT_K][NNGP_MT_NC];
+    __shared__ double cheb[NNGP_MT_K][NNGP_MT_NC];
     __shared__ double costab[NNGP_MT_NC * NNGP_MT_NC];
     const int o = blockIdx.x;
     const int tid = threadIdx.x;
+    const int jb = tid / NNGP_MT_NC, k = tid % NNGP_MT_NC;
+    const bool work = tid < NNGP_MT_K * NNGP_MT_NC;
+    const int b = o * NNGP_MT_K + jb;
+    if (o == 0 || o >= P.mt_noct - 1) {  // rho = 1 below the table, 0 above
+        if (work) tab[(int64_t)b * NNGP_MT_NC + k] = (o == 0 && k == 0) ? 1.0 : 0.0;
+        return;
+    }
     for (int i = tid; i < NNGP_MT_NC * NNGP_MT_NC; i += 64)
         costab[i] = cos(3.141592653589793 * (i / NNGP_MT_NC) * ((i % NNGP_MT_NC) + 0.5) / NNGP_MT_NC);
-    if (o > 0 && o < P.mt_noct - 1 && tid < NNGP_MT_K * NNGP_MT_NC) {
-        const int jb = tid / NNGP_MT_NC, k = tid % NNGP_MT_NC;
-        rho[jb][k] = nngp_matern_rho(P, sqrt(nngp_matern_bin_t(P, o * NNGP_MT_K + jb, nngp_matern_node(k))));
+    if (work) rho[jb][k] = nngp_matern_rho(P, sqrt(nngp_matern_bin_t(P, b, nngp_matern_node(k))));
+    __syncthreads();
+    if (work) {  // Chebyshev coefficient c_k of bin jb (k plays j's role here)
+        const double vref = rho[jb][NNGP_MT_NC / 2];
+        double c = 0.0;
+#pragma unroll
+        for (int i = 0; i < NNGP_MT_NC; ++i) c = fma(rho[jb][i] - vref, costab[k * NNGP_MT_NC + i], c);
+        cheb[jb][k] = c * ((k == 0 ? 1.0 : 2.0) / NNGP_MT_NC);
     }
     __syncthreads();
-    if (tid < NNGP_MT_K) {
-        double coef[NNGP_MT_NC];
-        const int b = o * NNGP_MT_K + tid;
-        nngp_matern_bin_fit(P, b, rho[tid], costab, coef);
+    if (work) {  // coefficient of f^k: sum_j c_j [f^k] T_j(2 f - 1), j ascending (then the middle value)
+        double a = 0.0;
 #pragma unroll
-        for (int k = 0; k < NNGP_MT_NC; ++k) tab[(int64_t)b * NNGP_MT_NC + k] = coef[k];
+        for (int j = 0; j < NNGP_MT_NC; ++j) a = fma(cheb[jb][j], kShiftedCheb[j][k], a);
+        if (k == 0) a += rho[jb][NNGP_MT_NC / 2];
+        tab[(int64_t)b * NNGP_MT_NC + k] = a;
     }
 }
 

@@ -58,8 +58,12 @@ T* ptr(const c10::optional<at::Tensor>& t) {
     return t.has_value() ? (T*)t->data_ptr() : nullptr;
 }
 
+// a sweep workspace's first 256 bytes (the pair kernel's header: tile count, fused-fold ticket) start at
+// zero (include/nngp.h); the rest is scratch
 at::Tensor workspace(int64_t bytes, const at::Tensor& like) {
-    return at::empty({bytes > 256 ? bytes : 256}, like.options().dtype(at::kByte));
+    auto ws = at::empty({bytes > 256 ? bytes : 256}, like.options().dtype(at::kByte));
+    ws.narrow(0, 0, 256).zero_();
+    return ws;
 }
 
 // ---------------------------------------------------------------- neighbour sets

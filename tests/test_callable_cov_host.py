@@ -17,8 +17,6 @@ def _aniso(s2, A):
     def cov(a, b):
         lib = torch if isinstance(a, torch.Tensor) else np
         t = a[..., :, None, :] - b[..., None, :, :]
-        # the quadratic form elementwise: torch's fp64 matmul on the GPU differed from numpy's by 5e-10
-        # relative here (measured), which the evaluation probe rightly refuses as not the same function
         q = A[0, 0] * t[..., 0] ** 2 + 2.0 * A[0, 1] * t[..., 0] * t[..., 1] + A[1, 1] * t[..., 1] ** 2
         return s2 * lib.exp(-lib.sqrt(q))
 

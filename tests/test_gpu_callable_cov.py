@@ -26,11 +26,12 @@ def _aniso(s2, A, tau2=0.0):
     def cov(a, b):
         lib = torch if isinstance(a, torch.Tensor) else np
         t = a[..., :, None, :] - b[..., None, :, :]
-        # the quadratic form elementwise: torch's fp64 matmul on the GPU differed from numpy's by 5e-10
-        # relative here (measured), which the evaluation probe rightly refuses as not the same function
         q = A[0, 0] * t[..., 0] ** 2 + 2.0 * A[0, 1] * t[..., 0] * t[..., 1] + A[1, 1] * t[..., 1] ** 2
         c = s2 * lib.exp(-lib.sqrt(q))
-        return c + tau2 * (q == 0) if tau2 else c
+        # (a bool tensor times a Python float is float32 in torch: cast, or the nugget is rounded to fp32 --
+        # which the evaluation probe caught, 5e-10 relative against the numpy plug-in, refusing the torch mode)
+        z = (q == 0).to(c.dtype) if lib is torch else (q == 0)
+        return c + tau2 * z if tau2 else c
 
     return cov
 
