@@ -66,10 +66,15 @@ class GibbsShardPlan:
     allgather_bytes: int    # ... had every member been all-gathered (sum_c world * maxc[c] * 8)
 
 
-def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, rank: int) -> GibbsShardPlan:
+def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, rank: int,
+                     exchange: str = "halo") -> GibbsShardPlan:
     """Plan rank ``rank`` of ``world`` for the DAG in storage order (host numpy arrays: nbr (n, m),
     reverse CSR off / rev_j, colours, members grouped by colour ascending inside a colour, colour
-    offsets).  Every rank computes the same runs, slot sizes and sources."""
+    offsets).  Every rank computes the same runs, slot sizes and sources.  ``exchange="halo"`` moves
+    the boundary members only; ``"all"`` every member (round 3's all-gather: the A/B reference, and at
+    one rank the only way to put a collective in the colour loop)."""
+    if exchange not in ("halo", "all"):
+        raise ValueError("exchange must be 'halo' or 'all'")
     nbr = np.asarray(nbr)
     off = np.asarray(off, dtype=np.int64)
     rev_j = np.asarray(rev_j)
@@ -89,7 +94,7 @@ def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, ra
     counts = np.diff(run, axis=1)
     maxc = counts.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
     send_off = np.concatenate([[0], np.cumsum(maxc)]).astype(np.int64)
-    exported = gibbs_boundary(nbr, bounds)
+    exported = gibbs_boundary(nbr, bounds) if exchange == "halo" else np.ones(nbr.shape[0], dtype=bool)
     # each (colour, rank) run ordered boundary members first (ascending), then the rest: the colour
     # step's publish slot then starts with exactly the values the other ranks replay.  (Members of a
     # colour are independent and their normals are keyed by location, so the order changes no bit.)
@@ -183,11 +188,13 @@ class ShardedSeqNNGP(SeqNNGP):
     without one, a single rank).  ``collective`` forces the exchanges through the group even at
     one rank (the path a one-GPU box tests).  ``graphs`` (default: on over RCCL) replays the
     colour loop from captured HIP graphs.  Results (``w_nodes`` / ``w_s`` / ``w_t``,
-    ``sample``) are gathered over the ranks and identical on every rank.
+    ``sample``) are gathered over the ranks and identical on every rank.  ``exchange``: "halo" (the
+    boundary members per colour, default) or "all" (every member, round 3's all-gather).
     """
 
     def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
-                 collective: Optional[bool] = None, graphs: Optional[bool] = None, **kwargs):
+                 collective: Optional[bool] = None, graphs: Optional[bool] = None, exchange: str = "halo",
+                 **kwargs):
         super().__init__(*args, **kwargs)
         inited = dist.is_available() and dist.is_initialized()
         self.rank = int(rank if rank is not None else (dist.get_rank(group) if inited else 0))
@@ -200,7 +207,7 @@ class ShardedSeqNNGP(SeqNNGP):
         n, m = self.n, self.m
         self.plan = p = gibbs_shard_plan(self.nbr.cpu().numpy(), self.off.cpu().numpy(), self.rev_j.cpu().numpy(),
                                          self.colors, self.members.cpu().numpy(), self.color_off, self.world,
-                                         self.rank)
+                                         self.rank, exchange=exchange)
         self.lo, self.hi = p.lo, p.hi
         # the colour runs in the plan's order (boundary members first: the head of each publish slot)
         self._member_rows = _lib.gibbs_member_rows(torch.from_numpy(p.members_x).to(dev), self.off)

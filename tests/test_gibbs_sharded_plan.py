@@ -211,3 +211,16 @@ def test_gloo_colour_exchange_world2():
         n_col = ncoll if n_col is None else n_col
         assert ncoll == n_col > 0
     assert out[0][2] + out[1][2] == 500
+
+
+def test_plan_exchange_all_is_every_member():
+    """exchange="all" (round 3's all-gather, the A/B reference): every row is exported, the gathered
+    block is the whole slot, and the runs keep the colour order."""
+    P = _problem(n=300, m=5, seed=9)
+    p = gibbs_shard_plan(P["nbr"], P["off"], P["rev_j"], P["colors"], P["members"], P["color_off"], 3, 1,
+                         exchange="all")
+    assert p.exported.all() and np.array_equal(p.bmax, p.maxc) and p.exchange_bytes == p.allgather_bytes
+    assert np.array_equal(p.members_x, P["members"])
+    with pytest.raises(ValueError):
+        gibbs_shard_plan(P["nbr"], P["off"], P["rev_j"], P["colors"], P["members"], P["color_off"], 3, 1,
+                         exchange="some")

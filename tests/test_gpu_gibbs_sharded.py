@@ -32,14 +32,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(world, backend, out):
+def _run(world, backend, out, exchange="halo"):
     port = _port()
     procs = []
     for rank in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK="0",
                    WORLD_SIZE=str(world))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gibbs_sharded_child.py"), backend,
-                                       out, str(ITERS)], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                       out, str(ITERS), exchange], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                       text=True))
     outs = []
     for p in procs:
@@ -72,11 +72,18 @@ def single(dev):
     return dict(w_sweep=w_sweep, w_final=g.w_nodes.cpu().numpy(), y_un=g.y_unobserved.cpu().numpy(), **res)
 
 
-def test_one_rank_rccl_equals_single_chain(single, tmp_path):
-    got = _run(1, "nccl", str(tmp_path / "r1.npz"))
+@pytest.mark.parametrize("exchange", ["all", "halo"])
+def test_one_rank_rccl_equals_single_chain(single, tmp_path, exchange):
+    """One rank over RCCL: with exchange="all" every colour's all-gather runs (captured in the HIP graphs
+    of the colour loop); with the halo exchange a single rank has no boundary, so no colour collective."""
+    got = _run(1, "nccl", str(tmp_path / "r1.npz"), exchange)
     meta = json.loads(str(got["meta"]))
-    assert meta["world"] == 1 and meta["n_collectives"] > 0
-    assert meta["graphs"] >= 1  # the colour loop replayed from captured HIP graphs (RCCL inside)
+    assert meta["world"] == 1
+    if exchange == "all":
+        assert meta["n_collectives"] > 0 and meta["exchange_bytes"] == meta["allgather_bytes"] > 0
+    else:
+        assert meta["n_collectives"] == 0 and meta["exchange_bytes"] == 0
+    assert meta["graphs"] >= 1  # the colour loop replayed from captured HIP graphs
     assert np.array_equal(got["w_sweep"], single["w_sweep"])
     for k in ("beta", "sigma2", "tau2", "phi"):
         assert np.array_equal(got[k], single[k]), k
@@ -84,11 +91,13 @@ def test_one_rank_rccl_equals_single_chain(single, tmp_path):
     assert np.array_equal(got["y_un"], single["y_un"])
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ranks_on_one_gpu_gloo(single, tmp_path, world):
-    got = _run(world, "gloo", str(tmp_path / f"r{world}.npz"))
+@pytest.mark.parametrize("world,exchange", [(2, "halo"), (3, "halo"), (2, "all")])
+def test_ranks_on_one_gpu_gloo(single, tmp_path, world, exchange):
+    got = _run(world, "gloo", str(tmp_path / f"r{world}.npz"), exchange)
     meta = json.loads(str(got["meta"]))
     assert meta["world"] == world and meta["halo"] > 0 and meta["apply"] > 0
+    if exchange == "halo":  # the boundary only
+        assert 0 < meta["exchange_bytes"] < meta["allgather_bytes"]
     assert np.array_equal(got["w_sweep"], single["w_sweep"])  # one sweep: bit for bit
     for k in ("sigma2", "tau2", "phi"):
         np.testing.assert_allclose(got[k], single[k], rtol=1e-9, atol=0)

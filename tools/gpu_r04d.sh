@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 out=gpurun_out/r04d
 mkdir -p $out
-timeout -k 10 900 python -u -m pytest -v --durations=20 --timeout 300 --timeout-method thread -m gpu tests > $out/pytest_gpu.txt 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gibbs_sharded.py > $out/pytest_sharded.txt 2>&1 || exit 1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $out/bench_driver.json 2> $out/bench_driver.err || exit 1
 timeout -k 10 600 bash tools/ab_clock.sh r04d_c3 "base||" "nobal|NNGP_LIB=ab/nobal/libnngp_hip.so|" "ff|NNGP_LIB=ab/ff/libnngp_hip.so|" > $out/ab_c3.txt 2>&1 || exit 1
