@@ -182,3 +182,22 @@ def test_matern_elementwise_and_custom_matern(lib, dev, c_oracle):
     assert np.max(np.abs(F1 - F2) / F2) <= 1e-10
     ll1, ll2 = c_oracle.loglik_from_partials(p1.cpu().numpy(), 20000), c_oracle.loglik_from_partials(p2.cpu().numpy(), 20000)
     assert abs(ll1 - ll2) <= 1e-12 * abs(ll2)
+
+
+def test_isotropic_gpu_only_fn_predict_m0_and_onesample(lib, dev):
+    """An IsotropicCovariance built on the GPU-only Matern correlation (_lib.matern): C(0) is evaluated on
+    the device (the m = 0 prediction variance is C(0) + tau2), and oneSample -- whose phi proposals need a
+    fused kind -- refuses it with a TypeError instead of failing inside the sampler."""
+    from pynngp_amd import NNGP, IsotropicCovariance
+
+    rng = np.random.default_rng(5)
+    t = rng.uniform(size=(300, 2))
+    y = rng.standard_normal(300)
+    cv = IsotropicCovariance(lambda d: 1.3 * lib.matern(9.0 * d, 1.2), tau2=0.1)
+    assert abs(cv.sigma2 - 1.3) <= 1e-15
+    g0 = NNGP(t, y, None, "S=T", 0, cv)
+    mean, var = g0.predict(values=y, query=rng.uniform(size=(20, 2)))
+    assert np.all(mean == 0.0) and np.allclose(var, 1.4, rtol=1e-15, atol=0)
+    g = NNGP(t, y, None, "S=T", 8, cv)
+    with pytest.raises(TypeError, match="built-in covariance"):
+        g.oneSample()

@@ -200,6 +200,18 @@ def test_checkpoint_resume_bit_identical(dev, tmp_path, with_ref):
         SeqNNGP(t2, y, **kw).restore(tmp_path / "ck.npz")
     with pytest.raises(ValueError, match="phi_tuning"):
         SeqNNGP(t, y, **{**kw, "phi_tuning": 0.3}).restore(tmp_path / "ck.npz")
+    # a checkpoint from before the data fingerprint (pynngp_amd < 0.2) still restores, with a warning
+    import json
+
+    with np.load(tmp_path / "ck.npz", allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    meta = json.loads(str(arrs["meta"]))
+    del meta["fingerprint"]
+    arrs["meta"] = np.array(json.dumps(meta))
+    np.savez(tmp_path / "ck_old.npz", **arrs)
+    with pytest.warns(UserWarning, match="predates the data fingerprint"):
+        c = SeqNNGP(t, y, **kw).restore(tmp_path / "ck_old.npz")
+    assert c.iteration == 6
 
 
 def test_reference_set_rejects_repeated_points(dev):

@@ -45,3 +45,28 @@ def test_fake_kernels_trace_shapes():
     assert tuple(nb.shape) == (64, 6) and nb.dtype == torch.int32
     assert tuple(B.shape) == (64, 6) and tuple(F.shape) == (64,) and tuple(p.shape) == (4,)
     assert tuple(o.shape) == (64,) and tuple(s.shape) == (64, 6)
+
+
+def test_bf_sweep_blocks_checks_lengths_before_any_device_call():
+    """nngp_bf_sweep_blocks takes raw pointers: the binding checks every length first (values (n_points,),
+    qvalues (n_locs,), order int32 (rows,)), so a short array can never reach the kernel."""
+    import pytest as _pytest
+    import torch as _torch
+
+    from pynngp_amd import _lib
+
+    m, rows, n = 4, 10, 12
+    cov = _torch.zeros((m + 1) * (m + 2) // 2, rows, dtype=_torch.float64)
+    nbr = _torch.zeros(rows, m, dtype=_torch.int32)
+    bad = [dict(values=_torch.zeros(n - 1, dtype=_torch.float64)),
+           dict(qvalues=_torch.zeros(n + 1, dtype=_torch.float64)),
+           dict(order=_torch.zeros(rows, dtype=_torch.int64)),
+           dict(order=_torch.zeros(rows - 1, dtype=_torch.int32))]
+    for kw in bad:
+        with _pytest.raises(ValueError):
+            _lib.bf_sweep_blocks(cov, nbr, n, **kw)
+    with _pytest.raises(ValueError):
+        _lib.bf_sweep_blocks(cov[:-1], nbr, n)
+    # well-formed CPU tensors reach the device check (no CPU path)
+    with _pytest.raises(_lib.NNGPExtensionError):
+        _lib.bf_sweep_blocks(cov, nbr, n, values=_torch.zeros(n, dtype=_torch.float64))
