@@ -205,18 +205,19 @@ constexpr int kPairbWaves = kPairbThreads / 64;
 constexpr int kPairbTile = kPairbThreads / 2;  // locations per tile (at most)
 constexpr int kDeviceCUs = 256;                 // MI355X (gfx950): 8 XCDs x 32 CUs
 
-// Tiling of n_rows locations (round 4).  A SIMD running one wave alone issues it ~1.2x slower than
-// each of two paired waves (dependency latency; tools/ubench/valu_mix), so a last round
-// of blocks that fills the device only partly (config 2: 782 tiles of 128 on 512 two-wave block
-// slots -- 1.53 rounds) costs a lone-wave round.  The tiles are therefore made a whole number of
-// rounds of the device's block slots (256 CUs x blocks per CU), each tile holding q or q + 1 rows
-// (config 2: 1,024 tiles of 97-98 rows; config 3: 8,192 of 122-123), as long as every wave of a tile
-// keeps a live row (q > 96); else the plain 128-row tiling.
+// Tiling of n_rows locations: q or q + 1 rows per tile (the sweep writes the tile count into the
+// workspace header, where the record fold reads it).  NNGP_PAIRB_BALANCE (round 4, measured and not
+// kept): make the tiles a whole number of rounds of the device's block slots (256 CUs x blocks per
+// CU), each holding q or q + 1 rows as long as every wave keeps a live row (q > 96) -- meant to avoid
+// a last, partly filled round of lone waves (config 2: 782 tiles on 512 two-wave slots, 1.53 rounds).
+// Same-box A/B (profiles/r04d): config 3 186.3 vs 178.8 us (+4 %: 32,768 instead of 31,252 waves, each
+// with the full instruction count), config 2 29.2 vs 28.1 us -- the partly filled round costs less
+// than the extra waves.  Default: the plain tiling (ceil(n / 128) tiles).
 struct PairbTiling {
     int64_t tiles, q, rem;  // tiles; tile t holds q + (t < rem) rows starting at t q + min(t, rem)
 };
-#ifndef NNGP_PAIRB_BALANCE  // 0: plain 128-row tiles (A/B builds)
-#define NNGP_PAIRB_BALANCE 1
+#ifndef NNGP_PAIRB_BALANCE  // 1: balanced rounds (measured slower, above)
+#define NNGP_PAIRB_BALANCE 0
 #endif
 inline PairbTiling pairb_tiling(int64_t n_rows, int m, int kind) {
     const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
@@ -972,6 +973,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 }
 
 // Fused record fold (one launch per sweep) up to this many rows; 0: always the separate fold kernel.
+// Measured and not kept (round 4, profiles/r04d): the record at agent scope, the drain and the ticket
+// in every block cost more than the separate 4-us fold launch -- config 2 34.0 vs 29.2 us per sweep.
 #ifndef NNGP_PAIRB_FUSED_FOLD_MAX_ROWS
 #define NNGP_PAIRB_FUSED_FOLD_MAX_ROWS 0
 #endif
