@@ -151,7 +151,9 @@ def colour_roofline(prof):
         return None
     bw = prof["bytes_per_launch"] / (prof["avg_ns"] * 1e-9)
     out = {"kernel": prof["kernel"], "avg_us": prof["avg_ns"] / 1e3, "traffic": prof["bytes_per_launch"],
-           "hbm_GBps": bw / 1e9, "hbm_frac": bw / HBM_PEAK, "source": prof["source"]}
+           "hbm_GBps": bw / 1e9, "hbm_frac": bw / HBM_PEAK, "source": prof["source"],
+           "traffic_note": "FETCH_SIZE x2 is MI355X_MICROARCH.md's calibration for 16-B-per-lane streaming reads; "
+                           "this kernel's reads are 8-B gathers (uncalibrated), so the figure is an upper bound"}
     for k in ("valu_per_wave", "valu_active_cycles_per_instr", "simd_valu_busy"):
         if k in prof:
             out[k] = prof[k]
