@@ -352,7 +352,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                             f"N={n} per chain, m={m}, exponential, "
                             f"{args.steps} timed iterations after {args.warmup} warm-up",
                 "n_per_gpu": args.n, "m": m, "kind": "exponential", "chains": n_chains, "chains_per_gpu": cpg,
-                "parallelism": (f"one chain over {world} GPU(s): storage-row shards, one all-gather per colour"
+                "parallelism": (f"one chain over {world} GPU(s): storage-row shards, one halo all-gather (the "
+                                "boundary members) per colour"
                                 if single else f"replicas x{world * cpg} ({cpg} independent chain(s) per GPU"
                                 + ("" if cpg == 1 else ", each on its own stream") + ")"),
             },
