@@ -1,5 +1,8 @@
-"""Time the caller-covariance path (IsotropicCovariance: nngp_joint_dist -> fn -> nngp_bf_sweep_blocks)
-against the fused kernels at N = 1e6, m = 15 (Z-order visiting order), HIP events; one JSON line."""
+"""Time the caller-covariance paths against the fused kernels at N = 1e6, m = 15 (Z-order visiting order),
+HIP events; one JSON line: IsotropicCovariance (nngp_joint_dist -> fn -> nngp_bf_sweep_blocks) and, round 4,
+CallableCovariance (a reference-style cov(a, b) -- here an anisotropic exponential in torch, batched on the
+GPU -- on every joint block's coordinate rows -> nngp_bf_sweep_blocks), the fused Matern-nu kind (the pair
+kernel's table) and the m = 28 blocks path (four-lane kernel)."""
 import json
 import os
 import sys
@@ -8,7 +11,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from pynngp_amd import Covariance, IsotropicCovariance, _lib  # noqa: E402
+from pynngp_amd import CallableCovariance, Covariance, IsotropicCovariance, _lib  # noqa: E402
 
 dev = torch.device("cuda", 0)
 rng = np.random.default_rng(0)
@@ -53,6 +56,30 @@ def custom_matern():
 
 out["custom_matern_total_ms"] = timed(custom_matern, reps=5)
 out["matern_eval_ms"] = timed(lambda: _lib.matern(dist, 1.3), reps=5)
+A = (400.0, 150.0, 100.0)
+
+
+def aniso(a, b):  # a reference-style plug-in: cross-covariance of two row sets, broadcasting over leading dims
+    t = a[..., :, None, :] - b[..., None, :, :]
+    q = A[0] * t[..., 0] ** 2 + 2.0 * A[1] * t[..., 0] * t[..., 1] + A[2] * t[..., 1] ** 2
+    return 1.4 * torch.exp(-torch.sqrt(q))
+
+
+cc = CallableCovariance(aniso, tau2=0.05)
+cblk = cc.blocks(c, srt, 0, order=order)
+out["callable_mode"] = cc.mode
+out["callable_blocks_ms"] = timed(lambda: cc.blocks(c, srt, 0, order=order), reps=5)
+out["callable_sweep_ms"] = timed(lambda: _lib.bf_sweep_blocks(cblk, srt, n, 0, values=v, qvalues=v, order=order))
+del cblk
+nb28 = _lib.knn_prior(c, 28)
+o28, s28 = _lib.row_order(c, 0, n, nb28)
+d28 = _lib.joint_dist(c, s28, 0, order=o28)
+b28 = cov.blocks(d28, 28)
+del d28
+out["blocks_sweep_m28_ms"] = timed(lambda: _lib.bf_sweep_blocks(b28, s28, n, 0, values=v, qvalues=v, order=o28), reps=5)
+out["fused_exponential_m28_ms"] = timed(lambda: _lib.bf_sweep(c, s28, 0, "exponential", 1.0, 30.0, 0.0, values=v,
+                                                              order=o28), reps=5)
+del b28
 _, _, p1 = _lib.bf_sweep_blocks(blocks, srt, n, 0, values=v, qvalues=v, order=order)
 _, _, p2 = _lib.bf_sweep(c, srt, 0, "exponential", 1.0, 30.0, 0.0, values=v, order=order)
 out["loglik_blocks"] = float(-0.5 * (n * np.log(2 * np.pi) + p1[0].item() + p1[1].item()))
