@@ -70,17 +70,15 @@ int32_t nngp_resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim,
 #define NNGP_MAX_M 63
 #define NNGP_MAX_DIM 3
 
-/* Library version string, e.g. "pynngp_amd 0.3.0 gfx950". */
+/* Library version string, e.g. "pynngp_amd 0.2.0 gfx950". */
 const char *nngp_version(void);
 
 /* ABI revision of this header (NNGP_ABI_VERSION), for a caller built against an older one to
  * refuse a library whose signatures moved.  Revision 2 (library 0.2.0) changed, relative to 1
  * (0.1.0): nngp_bf_finalize takes workspace_bytes as its 2nd argument; nngp_gibbs_w_sweep reads
  * (n, 4) member rows (nngp_gibbs_member_rows) and lost its `off` argument; nngp_bf_sweep /
- * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32.  Revision 3
- * (library 0.3.0) adds the member-record Gibbs entry points (nngp_gibbs_prepare_members,
- * nngp_gibbs_member_draws, nngp_gibbs_w_sweep_members); no existing signature changed. */
-#define NNGP_ABI_VERSION 3
+ * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32. */
+#define NNGP_ABI_VERSION 2
 int32_t nngp_abi_version(void);
 
 /* Message for the last error returned on the calling thread. */
@@ -291,17 +289,6 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  * nngp_gibbs_normals: z[i] = the Philox4x32-10 normal the sweep would draw for
  *   (seed, location i, sweep), for all n locations in one parallel pass; passing it
  *   as nngp_gibbs_w_sweep's z gives the bit-identical chain with shorter colour steps.
- *
- * Member records (the one-GPU chain's colour steps): a colour's members are ~1/n_colours of
- * the nodes, so their node-order operands P_i, 1/F_i, yres_i, z_i were one cache line each.
- * mrec (device double (n_members, 4), 32-B aligned, in member_rows order) holds them per member:
- * nngp_gibbs_prepare_members: nngp_gibbs_prepare's reverse-entry pass into `prep`, then
- *   mrec[g][0] = P_i, mrec[g][1] = 1/F_i for i = member_rows[g][0] (the same arithmetic and
- *   summation order as nngp_gibbs_prepare's P and 1/F, which it does not write).
- * nngp_gibbs_member_draws: once per iteration (after yres changes): mrec[g][2] = yres_i,
- *   mrec[g][3] = the Philox normal of (seed, location i, sweep) -- nngp_gibbs_normals's value.
- * nngp_gibbs_w_sweep_members: nngp_gibbs_w_sweep reading P, 1/F, yres and z from mrec: the
- *   bit-identical chain.
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,
  *   out[2 + c] = sum_i h_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p));
  *   h_i = noise_w[i], or 1 when noise_w is NULL.
@@ -342,14 +329,6 @@ int nngp_gibbs_w_sweep(const int32_t *member_rows, const int32_t *color_off_host
                        double *w, double *r, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
                        void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
-int nngp_gibbs_prepare_members(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
-                               const int32_t *rev_k, const int32_t *member_rows, int64_t n, int32_t m, void *prep,
-                               size_t prep_bytes, double *mrec, void *stream);
-int nngp_gibbs_member_draws(const int32_t *member_rows, int64_t n_members, const double *yres, uint64_t seed,
-                            uint64_t sweep, double *mrec, void *stream);
-int nngp_gibbs_w_sweep_members(const int32_t *member_rows, const int32_t *color_off_host, int32_t n_colors,
-                               const void *prep, int64_t n, int32_t m, double sigma2, double tau2, const double *mrec,
-                               const double *noise_w, double *w, double *r, const int32_t *rev_j, void *stream);
 int nngp_gibbs_prepare_range(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
                              const int32_t *rev_k, int64_t n, int32_t m, int64_t row0, int64_t row1, void *prep,
                              size_t prep_bytes, void *stream);

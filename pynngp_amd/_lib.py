@@ -55,9 +55,6 @@ SYMBOLS = (
     "nngp_gibbs_w_apply",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
-    "nngp_gibbs_prepare_members",
-    "nngp_gibbs_member_draws",
-    "nngp_gibbs_w_sweep_members",
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4, "matern": 5}
@@ -65,7 +62,7 @@ MATERN_NU_MAX = 50.0
 ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
-ABI_VERSION = 3  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
+ABI_VERSION = 2  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
 BLOCKS_MAX_M = 32  # nngp_bf_sweep_blocks: 1 <= m <= 32
 
 
@@ -161,12 +158,6 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_stats_workspace_bytes.restype = SZ
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
-    lib.nngp_gibbs_prepare_members.argtypes = [P, P, P, P, P, P, I64, I32, P, SZ, P, P]
-    lib.nngp_gibbs_prepare_members.restype = ctypes.c_int
-    lib.nngp_gibbs_member_draws.argtypes = [P, I64, P, U64, U64, P, P]
-    lib.nngp_gibbs_member_draws.restype = ctypes.c_int
-    lib.nngp_gibbs_w_sweep_members.argtypes = [P, P, I32, P, I64, I32, D, D, P, P, P, P, P, P]
-    lib.nngp_gibbs_w_sweep_members.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_check_partials.argtypes = [P, P, P]
     lib.nngp_check_partials.restype = ctypes.c_int
@@ -743,72 +734,6 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
                                      _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
-
-
-def _check_member_rows(member_rows: torch.Tensor) -> int:
-    if member_rows.dtype != torch.int32 or member_rows.dim() != 2 or member_rows.shape[1] != 4 \
-            or not member_rows.is_contiguous():
-        raise ValueError("member_rows must be a contiguous int32 (k, 4) tensor from gibbs_member_rows")
-    return member_rows.shape[0]
-
-
-def _check_mrec(mrec: torch.Tensor, k: int) -> None:
-    if mrec.dtype != torch.float64 or tuple(mrec.shape) != (k, 4) or not mrec.is_contiguous() \
-            or mrec.data_ptr() % 32:
-        raise ValueError(f"mrec must be a contiguous, 32-byte aligned float64 ({k}, 4) tensor")
-
-
-def gibbs_prepare_members(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor,
-                          rev_k: torch.Tensor, member_rows: torch.Tensor, mrec: torch.Tensor,
-                          prep: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """:func:`gibbs_prepare`'s reverse-entry pass into ``prep``, with P_i and 1/F_i written into the
-    member records ``mrec`` (float64 (n, 4), member_rows order; columns 0, 1) instead of node order
-    (nngp_gibbs_prepare_members); returns ``prep``."""
-    dev = _require_gpu(B, Ft, off, rev_j, rev_k, member_rows, mrec, prep)
-    n, m = B.shape
-    if _check_member_rows(member_rows) != n:
-        raise ValueError(f"member_rows must list all {n} locations")
-    _check_mrec(mrec, n)
-    lib = load()
-    need = lib.nngp_gibbs_prep_bytes(n, m)
-    if prep is None or prep.numel() < need:
-        prep = _workspace(need, dev)
-    _check(lib.nngp_gibbs_prepare_members(_ptr(B), _ptr(Ft), _ptr(off), _ptr(rev_j), _ptr(rev_k), _ptr(member_rows),
-                                          n, m, _ptr(prep), prep.numel(), _ptr(mrec), _stream(dev)),
-           "nngp_gibbs_prepare_members")
-    return prep
-
-
-def gibbs_member_draws(member_rows: torch.Tensor, yres: torch.Tensor, seed: int, sweep: int,
-                       mrec: torch.Tensor) -> None:
-    """Columns 2, 3 of the member records: yres_i and the sweep's Philox normal of location i
-    (nngp_gibbs_member_draws), once per iteration after yres changes."""
-    dev = _require_gpu(member_rows, yres, mrec)
-    k = _check_member_rows(member_rows)
-    _check_mrec(mrec, k)
-    if yres.dtype != torch.float64 or yres.dim() != 1 or not yres.is_contiguous():
-        raise ValueError("yres must be a contiguous float64 (n,) tensor")
-    _check(load().nngp_gibbs_member_draws(_ptr(member_rows), k, _ptr(yres), int(seed) & (2 ** 64 - 1), int(sweep),
-                                          _ptr(mrec), _stream(dev)), "nngp_gibbs_member_draws")
-
-
-def gibbs_w_sweep_members(member_rows: torch.Tensor, color_off_host, prep: torch.Tensor, m: int, sigma2: float,
-                          tau2: float, mrec: torch.Tensor, w: torch.Tensor, r: torch.Tensor, rev_j: torch.Tensor,
-                          noise_w: Optional[torch.Tensor] = None) -> None:
-    """:func:`gibbs_w_sweep` reading P, 1/F, yres and z from the member records (nngp_gibbs_w_sweep_members):
-    the bit-identical chain with one coalesced load per member for those four operands."""
-    import numpy as np
-
-    dev = _require_gpu(member_rows, prep, mrec, w, r, rev_j, noise_w)
-    _check_noise_w(noise_w, w.shape[0])
-    k = _check_member_rows(member_rows)
-    _check_mrec(mrec, k)
-    co = np.ascontiguousarray(color_off_host, dtype=np.int32)
-    if len(co) < 1 or co[-1] > k:
-        raise ValueError("colour offsets exceed the member rows")
-    _check(load().nngp_gibbs_w_sweep_members(_ptr(member_rows), co.ctypes.data, len(co) - 1, _ptr(prep), w.shape[0],
-                                             int(m), float(sigma2), float(tau2), _ptr(mrec), _ptr(noise_w), _ptr(w),
-                                             _ptr(r), _ptr(rev_j), _stream(dev)), "nngp_gibbs_w_sweep_members")
 
 
 def gibbs_normals(z: torch.Tensor, seed: int, sweep: int) -> torch.Tensor:

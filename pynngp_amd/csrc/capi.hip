@@ -59,7 +59,7 @@ int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_coun
 
 extern "C" {
 
-const char* nngp_version(void) { return "pynngp_amd 0.3.0 gfx950"; }
+const char* nngp_version(void) { return "pynngp_amd 0.2.0 gfx950"; }
 
 int32_t nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 
@@ -426,54 +426,6 @@ int nngp_gibbs_w_sweep(const int32_t* member_rows, const int32_t* color_off_host
     hipError_t e = nngp::gibbs_w_sweep_launch(member_rows, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres,
                                               noise_w, w, r, rev_j, z, seed, sweep, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
-    return NNGP_OK;
-}
-
-int nngp_gibbs_prepare_members(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
-                               const int32_t* rev_k, const int32_t* member_rows, int64_t n, int32_t m, void* prep,
-                               size_t prep_bytes, double* mrec, void* stream) {
-    if (Ft == nullptr || off == nullptr || prep == nullptr || (n > 0 && (member_rows == nullptr || mrec == nullptr)) ||
-        (m > 0 && (B == nullptr || rev_j == nullptr || rev_k == nullptr)))
-        return fail(NNGP_EINVAL, "null pointer argument");
-    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n or m");
-    if (((uintptr_t)prep & 255) != 0) return fail(NNGP_EINVAL, "prep must be 256-byte aligned");
-    if (((uintptr_t)member_rows & 15) != 0 || ((uintptr_t)mrec & 31) != 0)
-        return fail(NNGP_EINVAL, "member_rows must be 16-byte and mrec 32-byte aligned");
-    if (prep_bytes < nngp::gibbs_prep_bytes(n, m))
-        return fail(NNGP_EINVAL, "prep too small: %zu < %zu bytes", prep_bytes, nngp::gibbs_prep_bytes(n, m));
-    hipError_t e = nngp::gibbs_prepare_members_launch(B, Ft, off, rev_j, rev_k, member_rows, n, m, prep, mrec,
-                                                      (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e, "gibbs_prepare_members launch");
-    return NNGP_OK;
-}
-
-int nngp_gibbs_member_draws(const int32_t* member_rows, int64_t n_members, const double* yres, uint64_t seed,
-                            uint64_t sweep, double* mrec, void* stream) {
-    if (n_members < 0) return fail(NNGP_EINVAL, "bad n_members");
-    if (n_members == 0) return NNGP_OK;
-    if (member_rows == nullptr || yres == nullptr || mrec == nullptr) return fail(NNGP_EINVAL, "null pointer argument");
-    if (((uintptr_t)member_rows & 15) != 0 || ((uintptr_t)mrec & 31) != 0)
-        return fail(NNGP_EINVAL, "member_rows must be 16-byte and mrec 32-byte aligned");
-    hipError_t e = nngp::gibbs_member_draws_launch(member_rows, n_members, yres, seed, sweep, mrec, (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e, "gibbs_member_draws launch");
-    return NNGP_OK;
-}
-
-int nngp_gibbs_w_sweep_members(const int32_t* member_rows, const int32_t* color_off_host, int32_t n_colors,
-                               const void* prep, int64_t n, int32_t m, double sigma2, double tau2, const double* mrec,
-                               const double* noise_w, double* w, double* r, const int32_t* rev_j, void* stream) {
-    if (member_rows == nullptr || color_off_host == nullptr || prep == nullptr || mrec == nullptr || w == nullptr ||
-        r == nullptr || (m > 0 && rev_j == nullptr))
-        return fail(NNGP_EINVAL, "null pointer argument");
-    if (((uintptr_t)member_rows & 15) != 0 || ((uintptr_t)mrec & 31) != 0)
-        return fail(NNGP_EINVAL, "member_rows must be 16-byte and mrec 32-byte aligned");
-    if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
-    if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
-    if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
-        return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
-    hipError_t e = nngp::gibbs_w_sweep_members_launch(member_rows, n_colors, color_off_host, prep, n, m, sigma2, tau2,
-                                                      mrec, noise_w, w, r, rev_j, (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep_members launch");
     return NNGP_OK;
 }
 

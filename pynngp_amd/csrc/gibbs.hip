@@ -462,36 +462,22 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
                                                      const int32_t* __restrict__ rev_j,
                                                      const double* __restrict__ z, uint64_t seed, uint64_t sweep,
                                                      double* __restrict__ w_out, const double* __restrict__ var,
-                                                     int64_t m_cap, const double4* __restrict__ mrec) {
+                                                     int64_t m_cap) {
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
     const bool live = g < n_members;
-    const int64_t gc = live ? g : n_members - 1;
-    const int4 mr = member_rows[gc];
+    const int4 mr = member_rows[live ? g : n_members - 1];
     const int64_t i = mr.x;
     const int32_t e0 = mr.y, e1 = live ? mr.z : mr.y;
     // every load that depends only on the member row is issued at once, branch-free: the
     // member's own operands and its first child's reverse entry in one memory round trip, then
     // the child's r_j in a second (a guarded load per operand made the compiler wait for each
     // before issuing the next).  r_i is safe to read early: no other member of the colour is a
-    // parent of i, so nothing else writes it during the step.  With member records (mrec, kernel
-    // argument: wave-uniform) P_i, 1/F_i, yres_i and z_i come in one coalesced 32-B load.
-    const double wi = w[i], ri = r[i];
-    double iF, Pi, yi, zl;
-    if (mrec != nullptr) {
-        const double4 q = mrec[gc];
-        Pi = q.x;
-        iF = q.y;
-        yi = q.z;
-        zl = q.w;
-    } else {
-        iF = invF[i];
-        Pi = P[i];
-        yi = yres[i];
-        zl = z != nullptr ? z[i] : 0.0;
-    }
+    // parent of i, so nothing else writes it during the step.
+    const double wi = w[i], ri = r[i], iF = invF[i], Pi = P[i], yi = yres[i];
     const double hi = noise_w != nullptr ? noise_w[i] : 1.0;
+    const double zl = z != nullptr ? z[i] : 0.0;
     if (var != nullptr) {  // (sigma2, tau2) from device memory: a graph-captured step replays with new values
         is2 = 1.0 / var[0];
         it2 = 1.0 / var[1];
@@ -538,7 +524,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
     const double it2i = noise_w != nullptr ? it2 * hi : it2;  // 1 / (tau2 / h_i)
     const double prec = fma(iF + Pi, is2, it2i);
     const double lin = fma(yi, it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
-    const double zi = (z != nullptr || mrec != nullptr) ? zl : philox_normal(seed, (uint64_t)i, sweep);
+    const double zi = z != nullptr ? zl : philox_normal(seed, (uint64_t)i, sweep);
     const double sd = nngp_rsqrt(prec);
     const double wn = fma(zi, sd, lin / prec);
     const double dw = wn - wi;
@@ -567,84 +553,7 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
         const int64_t threads = (b - a) * kGroup;
         hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                            (const int4*)member_rows + a, b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2,
-                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr, n * (int64_t)m,
-                           (const double4*)nullptr);
-    }
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- member records (one-GPU chain)
-// A colour's members are ~1/n_colours of the nodes, scattered over the storage order, so each of
-// a member's own node-order operands (P_i, 1/F_i, yres_i, z_i) is a cache line of its own -- at
-// N = 1e6 they were most of the colour kernel's fetched bytes (profiles/r04e: 45 MB fetched per
-// 32k-member step).  The member records hold them in MEMBER order (colour by colour, as the
-// colour kernel walks them), one double4 (P, 1/F, yres, z) per member: P and 1/F written when a phi
-// is accepted (gibbs_member_prepare, the rows pass's own arithmetic and summation order), yres and
-// z once per iteration (gibbs_member_draws, the same Philox stream as philox_normals_kernel).  Same
-// values, same bits as the node-order arrays; only w_i, r_i (and the children's r_j) stay gathers.
-__global__ __launch_bounds__(256) void gibbs_member_prepare(const int4* __restrict__ member_rows, int64_t n_members,
-                                                            const double* __restrict__ Brev,
-                                                            const double* __restrict__ Grev,
-                                                            const double* __restrict__ Ft, double4* __restrict__ mrec) {
-    const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int64_t g = t / kRowLanes;
-    const int l = (int)(t % kRowLanes);
-    const bool live = g < n_members;
-    const int4 mr = member_rows[live ? g : n_members - 1];
-    const int32_t e0 = mr.y, e1 = live ? mr.z : e0;
-    double acc = 0.0;
-    for (int32_t e = e0 + l; e < e1; e += kRowLanes) acc = fma(Brev[e], Grev[e], acc);
-#pragma unroll
-    for (int o = kRowLanes / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    if (live && l == 0) *(double2*)(mrec + g) = make_double2(acc, 1.0 / Ft[mr.x]);
-}
-
-__global__ __launch_bounds__(256) void gibbs_member_draws(const int4* __restrict__ member_rows, int64_t n_members,
-                                                          const double* __restrict__ yres, uint64_t seed,
-                                                          uint64_t sweep, double4* __restrict__ mrec) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_members) return;
-    const int64_t i = member_rows[g].x;
-    const double y = yres[i];
-    *((double2*)(mrec + g) + 1) = make_double2(y, philox_normal(seed, (uint64_t)i, sweep));
-}
-
-hipError_t gibbs_prepare_members_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
-                                        const int32_t* rev_k, const int32_t* member_rows, int64_t n, int m, void* prep,
-                                        double* mrec, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const GibbsPrep g = prep_layout(prep, n, m);
-    const int64_t ne = n * (int64_t)m;
-    if (ne > 0)
-        hipLaunchKernelGGL(gibbs_prepare_entries, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, B, Ft, rev_j,
-                           rev_k, off, (int64_t)0, n, m, g.Brev, g.Grev);
-    hipLaunchKernelGGL(gibbs_member_prepare, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s,
-                       (const int4*)member_rows, n, g.Brev, g.Grev, Ft, (double4*)mrec);
-    return hipGetLastError();
-}
-
-hipError_t gibbs_member_draws_launch(const int32_t* member_rows, int64_t n_members, const double* yres, uint64_t seed,
-                                     uint64_t sweep, double* mrec, hipStream_t s) {
-    if (n_members <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gibbs_member_draws, dim3((unsigned)((n_members + 255) / 256)), dim3(256), 0, s,
-                       (const int4*)member_rows, n_members, yres, seed, sweep, (double4*)mrec);
-    return hipGetLastError();
-}
-
-hipError_t gibbs_w_sweep_members_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
-                                        const void* prep, int64_t n, int m, double sigma2, double tau2,
-                                        const double* mrec, const double* noise_w, double* w, double* r,
-                                        const int32_t* rev_j, hipStream_t s) {
-    const GibbsPrep g = prep_layout((void*)prep, n, m);
-    for (int c = 0; c < n_colors; ++c) {
-        const int64_t a = color_off_host[c], b = color_off_host[c + 1];
-        if (b <= a) continue;
-        const int64_t threads = (b - a) * kGroup;
-        hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                           (const int4*)member_rows + a, b - a, g.Brev, g.Grev, (const double*)nullptr,
-                           (const double*)nullptr, 1.0 / tau2, 1.0 / sigma2, (const double*)nullptr, noise_w, w, r,
-                           rev_j, (const double*)nullptr, (uint64_t)0, (uint64_t)0, (double*)nullptr,
-                           (const double*)nullptr, n * (int64_t)m, (const double4*)mrec + a);
+                           yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr, n * (int64_t)m);
     }
     return hipGetLastError();
 }
@@ -658,7 +567,7 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
     const int64_t threads = n_members * kGroup;
     hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                        (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
-                       noise_w, w, r, rev_j, z, seed, sweep, w_out, var, n * (int64_t)m, (const double4*)nullptr);
+                       noise_w, w, r, rev_j, z, seed, sweep, w_out, var, n * (int64_t)m);
     return hipGetLastError();
 }
 

@@ -179,15 +179,6 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
                                 const void* prep, int64_t n, int m, double sigma2, double tau2,
                                 const double* yres, const double* noise_w, double* w, double* r,
                                 const int32_t* rev_j, const double* z, uint64_t seed, uint64_t sweep, hipStream_t s);
-hipError_t gibbs_prepare_members_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,
-                                        const int32_t* rev_k, const int32_t* member_rows, int64_t n, int m, void* prep,
-                                        double* mrec, hipStream_t s);
-hipError_t gibbs_member_draws_launch(const int32_t* member_rows, int64_t n_members, const double* yres, uint64_t seed,
-                                     uint64_t sweep, double* mrec, hipStream_t s);
-hipError_t gibbs_w_sweep_members_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
-                                        const void* prep, int64_t n, int m, double sigma2, double tau2,
-                                        const double* mrec, const double* noise_w, double* w, double* r,
-                                        const int32_t* rev_j, hipStream_t s);
 size_t gibbs_stats_workspace_bytes(int64_t n, int p);
 hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
                               const double* X, int p, const double* w, const double* noise_w, double* out,

@@ -93,10 +93,6 @@ class SeqNNGP:
     nngp.py:45-47: the uniform 5-NN mean of the observed responses at every node).
     """
 
-    # the colour steps read P_i, 1/F_i, yres_i and z_i from member records (colour-ordered, one
-    # coalesced load per member; nngp_gibbs_w_sweep_members) -- the sharded chain keeps node order
-    _member_records = True
-
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
                  seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
@@ -295,19 +291,13 @@ class SeqNNGP:
         self.B, self.Ft, self.r = z(n, self.m), z(n), z(n)
         self._B2, self._Ft2, self._r2 = z(n, self.m), z(n), z(n)
         self._part = z(4)
-        self._z = None if self._member_records else z(n)  # node-order normals (the member records hold them otherwise)
+        self._z = z(n)
         self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
         ops.load()  # the sweep goes through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
         self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
         self._stats_buf = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
-        self._prep = None
-        if self._member_records:
-            # (location, reverse-entry range) per colour-ordered member, and the member records:
-            # P_i, 1/F_i, yres_i, z_i per member in the same order (nngp_gibbs_prepare_members)
-            self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
-            self._mrec = z(n, 4)
-        SeqNNGP._prepare(self)
+        self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k)
         ph = self._part.cpu().numpy()
         self._check(ph)
         self.sum_logF, self.quad = float(ph[0]), float(ph[1])
@@ -378,20 +368,8 @@ class SeqNNGP:
         return self._part.cpu().numpy()
 
     def _prepare(self):
-        """Fold the accepted B / F for the colour steps (the sharded chain: its own rows only); the
-        one-GPU chain writes P and 1/F into the member records."""
-        if self._member_records:
-            self._prep = _lib.gibbs_prepare_members(self.B, self.Ft, self.off, self.rev_j, self.rev_k,
-                                                    self._member_rows, self._mrec, prep=self._prep)
-        else:
-            self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
-
-    def _draw_normals(self):
-        """The iteration's Philox normals (and, with member records, yres) for the colour steps."""
-        if self._member_records:
-            _lib.gibbs_member_draws(self._member_rows, self.yres, self.seed, self.iteration, self._mrec)
-        else:
-            _lib.gibbs_normals(self._z, self.seed, self.iteration)
+        """Fold the accepted B / F for the colour steps (the sharded chain: its own rows only)."""
+        self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
 
     def _stats(self):
         """[sum r^2/F, sum h (yres - w)^2, X'H(y - w)] on the host (the sharded chain: folded over ranks)."""
@@ -406,17 +384,12 @@ class SeqNNGP:
         return t
 
     def _sweep_colours(self, c0, c1):
-        if c1 <= c0:
-            return
-        if self._member_records:
-            _lib.gibbs_w_sweep_members(self._member_rows, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2,
-                                       self.tau2, self._mrec, self.w, self.r, self.rev_j, noise_w=self.noise_w)
-            return
-        if getattr(self, "_member_rows", None) is None:  # (location, reverse-entry range) per member, once
-            self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
-        _lib.gibbs_w_sweep(self.members, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2, self.tau2,
-                           self.yres, self.w, self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z,
-                           noise_w=self.noise_w, member_rows=self._member_rows)
+        if c1 > c0:
+            if getattr(self, "_member_rows", None) is None:  # (location, reverse-entry range) per member, once
+                self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
+            _lib.gibbs_w_sweep(self.members, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2, self.tau2,
+                               self.yres, self.w, self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z,
+                               noise_w=self.noise_w, member_rows=self._member_rows)
 
     def update_wt(self):
         """w_t | w_S, y_t for the data locations outside S (nngp.py:99): the leaves of the DAG,
@@ -452,7 +425,7 @@ class SeqNNGP:
         a, b = self.priors.sigma2_ig
         self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
         # w | rest (colour steps, in place on w and r; the sweep's normals in one parallel pass)
-        self._draw_normals()
+        _lib.gibbs_normals(self._z, self.seed, self.iteration)
         self.update_wt()
         self.update_ws()
         st = self._stats()
@@ -564,7 +537,7 @@ class SeqNNGP:
         self._check(self._part.cpu().numpy())
         self.r = r
         self.sum_logF, self.quad = meta["sum_logF"], meta["quad"]
-        SeqNNGP._prepare(self)
+        self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k, prep=self._prep)
         self.yres = self._residual_y(self.beta)
         return self
 

@@ -192,8 +192,6 @@ class ShardedSeqNNGP(SeqNNGP):
     boundary members per colour, default) or "all" (every member, round 3's all-gather).
     """
 
-    _member_records = False  # the colour runs and the replay read the node-order prep (nngp_gibbs_w_color)
-
     def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
                  collective: Optional[bool] = None, graphs: Optional[bool] = None, exchange: str = "halo",
                  **kwargs):

@@ -40,7 +40,7 @@ def main():
     g = ShardedSeqNNGP(t, y, X, device=dev, exchange=exchange, **KW)
     assert g.collective and g.world == world and g.rank == rank
     # one w sweep at the initial hyperparameters (Philox normals of sweep 0)
-    g._draw_normals()  # the Philox normals of sweep 0 (iteration 0)
+    _lib.gibbs_normals(g._z, g.seed, 0)
     g.update_wt()
     g.update_ws()
     w_sweep = g.w_nodes.cpu().numpy()

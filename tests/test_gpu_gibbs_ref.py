@@ -17,18 +17,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _model_order(smp):
-    """The sampler's storage-order state mapped back to model (node) order; z = the iteration's Philox
-    normals (what _draw_normals puts in the member records), per node."""
-    from pynngp_amd import _lib
-
+    """The sampler's storage-order state mapped back to model (node) order."""
     pos, perm = smp.pos, smp.perm
-    z = _lib.gibbs_normals(torch.empty(smp.n, dtype=torch.float64, device=smp.device), smp.seed, smp.iteration)
     nb = smp.nbr[pos].long()
     nbr = torch.where(nb >= 0, perm[nb.clamp(min=0)], -1).cpu().numpy().astype(np.int32)
     h = smp.noise_w[pos].cpu().numpy() if smp.noise_w is not None else np.ones(smp.n)
     return dict(nbr=nbr, B=smp.B[pos].cpu().numpy(), F=smp.Ft[pos].cpu().numpy(), h=h,
                 yres=smp.yres[pos].cpu().numpy(), colors=smp.colors[pos.cpu().numpy()],
-                z=z[pos].cpu().numpy(), w=smp.w_nodes.cpu().numpy(), r=smp.r[pos].cpu().numpy())
+                z=smp._z[pos].cpu().numpy(), w=smp.w_nodes.cpu().numpy(), r=smp.r[pos].cpu().numpy())
 
 
 def _data(rng, n_s, n_new, n_in, n_nan):
@@ -64,7 +60,7 @@ def test_reference_set_structure_and_sweep_vs_dense(dev, c_oracle):
     smp.set_w(ws=rng.standard_normal(300), wt=rng.standard_normal(460))
     from pynngp_amd import _lib
 
-    smp._draw_normals()
+    _lib.gibbs_normals(smp._z, smp.seed, smp.iteration)
     mo = _model_order(smp)
     P, b, _, _ = G.dag_posterior(mo["nbr"], mo["B"], mo["F"], smp.sigma2, smp.tau2, mo["h"], mo["yres"])
     order = np.where(mo["colors"] == smp.n_colors_ref, 0, mo["colors"] + 1)
@@ -97,7 +93,7 @@ def test_reference_set_stationary_law(dev):
     W, Y = [], []
     n_it = 20000
     for k in range(n_it):
-        smp._draw_normals()
+        _lib.gibbs_normals(smp._z, smp.seed, smp.iteration)
         smp.update_wt()
         smp.update_ws()
         smp.update_y_unobserved()

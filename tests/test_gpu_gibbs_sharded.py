@@ -64,7 +64,7 @@ def single(dev):
 
     t, y, X = C.problem()
     g = SeqNNGP(t, y, X, device=dev, **C.KW)
-    g._draw_normals()  # the Philox normals of sweep 0 (iteration 0)
+    _lib.gibbs_normals(g._z, g.seed, 0)
     g.update_wt()
     g.update_ws()
     w_sweep = g.w_nodes.cpu().numpy()

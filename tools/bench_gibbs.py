@@ -29,8 +29,6 @@ ap.add_argument("--single-chain", action="store_true")
 ap.add_argument("--force-group", action="store_true")
 ap.add_argument("--backend", default="nccl")
 ap.add_argument("--graphs", type=int, default=None, help="single chain: 1/0 forces the HIP-graph colour loop on/off")
-ap.add_argument("--node-order", action="store_true",
-                help="one-GPU chain without member records (node-order P, 1/F, yres, z: the A/B baseline)")
 args = ap.parse_args()
 # several GPUs (torchrun): independent chains, one per GPU ("replicas only")
 world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,12 +58,7 @@ if args.single_chain:
     g = ShardedSeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev,
                        graphs=None if args.graphs is None else bool(args.graphs))
 else:
-    cls = SeqNNGP
-    if args.node_order:
-        class NodeOrder(SeqNNGP):
-            _member_records = False
-        cls = NodeOrder
-    g = cls(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
+    g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
 torch.cuda.synchronize()
 setup_s = time.perf_counter() - t0
 for _ in range(args.warmup):
@@ -93,7 +86,7 @@ if rank == 0:
     chains = 1 if args.single_chain else world
     what = "ONE chain sharded over the GPUs" if args.single_chain else "one chain per GPU"
     print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, {what}", **extra,
-                      "member_records": bool(getattr(g, "_member_records", False)), "chains": chains, "chain_iters_per_s": chains * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
+                      "chains": chains, "chain_iters_per_s": chains * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
                   "locations_per_s": args.n * args.iters / el, "setup_s": setup_s, "n_colors": int(g.n_colors),
                   "phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "accept": g.n_accept / max(1, g.iteration)}))
 if grouped:
