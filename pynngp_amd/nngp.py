@@ -182,20 +182,17 @@ class CallableCovariance:
     ``_lib.bf_sweep_blocks``'s layout (lower triangle, entry-major) and factorised on the GPU
     (``nngp_bf_sweep_blocks``: B, F, residuals and the log-likelihood partials; 1 <= m <= 32).
     Evaluation, chosen once per object by probing ``fn`` on a few rows against one call per row:
-      * ``"torch_pairs"``: ``fn`` broadcasts over leading batch dimensions of torch tensors on the GPU
-        -- one call per chunk with the lower triangle's point pairs, a (rows, E, 1, d) and b (rows, E,
-        1, d), E = (m+1)(m+2)/2: only the entries the factorisation reads ((m+2)/(2(m+1)) of the square,
-        0.53 at m = 15), already in the kernel's entry-major order;
-      * ``"torch"``: the same with the whole square, X of shape (rows, m+1, d) as fn(X, X);
-      * ``"numpy_pairs"`` / ``"numpy"``: the same with numpy arrays (host evaluation of the user's
-        function, one call per chunk; the blocks then go to the GPU);
+      * ``"torch"``: ``fn`` broadcasts over a leading batch dimension of torch tensors on the GPU --
+        one call per chunk of rows with X of shape (rows, m+1, d), on the device;
+      * ``"numpy"``: the same with numpy arrays (host evaluation of the user's function, one call
+        per chunk; the blocks then go to the GPU);
       * ``"loop"``: one call per location with the (m+1, d) numpy rows the reference passes.
     ``batch`` forces a mode.  The covariance values are the caller's code; everything after them
     (the factorisation, B, F, the log-likelihood) runs on the GPU, with no CPU path.
     ``tau2`` is an optional nugget added to the diagonal (0: ``fn``'s own values are C)."""
 
     kind = "custom"
-    MODES = ("torch_pairs", "torch", "numpy_pairs", "numpy", "loop", "loop_torch")
+    MODES = ("torch", "numpy", "loop", "loop_torch")
 
     def __init__(self, fn: Callable, tau2: float = 0.0, batch: Optional[str] = None, chunk_bytes: int = 1 << 28):
         if not callable(fn):
@@ -211,38 +208,8 @@ class CallableCovariance:
         return self.fn(a, b)
 
     # -- evaluation modes --------------------------------------------------------
-    @staticmethod
-    def _tri(k: int, dev):
-        """Lower-triangle entry e = a (a+1)/2 + b of a k x k block: (a, b) index vectors."""
-        a = torch.arange(k, device=dev)
-        return torch.repeat_interleave(a, a + 1), torch.cat([torch.arange(j + 1, device=dev) for j in range(k)])
-
-    def _eval_pairs(self, X: torch.Tensor, mode: str) -> torch.Tensor:
-        """fn on the lower triangle's point pairs of every joint block: (r, E) in entry order."""
-        ta, tb = self._tri(X.shape[1], X.device)
-        A, B = X[:, ta, None, :], X[:, tb, None, :]  # (r, E, 1, d)
-        if mode == "torch_pairs":
-            C = self.fn(A, B)
-            if not isinstance(C, torch.Tensor):
-                raise TypeError("not a torch tensor")
-            C = C.to(device=X.device, dtype=torch.float64)
-        else:
-            C = torch.from_numpy(np.ascontiguousarray(np.asarray(self.fn(A.cpu().numpy(), B.cpu().numpy()),
-                                                                 dtype=np.float64))).to(X.device)
-        if tuple(C.shape) != (X.shape[0], ta.numel(), 1, 1):
-            raise ValueError(f"cov(a, b) returned {tuple(C.shape)} for {X.shape[0]} x {ta.numel()} point pairs")
-        return C.reshape(X.shape[0], ta.numel())
-
     def _eval(self, X: torch.Tensor, mode: str) -> torch.Tensor:
         """fn's joint blocks (r, k, k) on X's device for X (r, k, d)."""
-        if mode.endswith("_pairs"):  # the lower triangle, mirrored (probe comparisons)
-            k = X.shape[1]
-            ta, tb = self._tri(k, X.device)
-            C = X.new_zeros((X.shape[0], k, k))
-            v = self._eval_pairs(X, mode)
-            C[:, ta, tb] = v
-            C[:, tb, ta] = v
-            return C
         if mode == "torch":
             C = self.fn(X, X)
             if not isinstance(C, torch.Tensor):
@@ -278,20 +245,12 @@ class CallableCovariance:
         if ref.shape != (X.shape[0], k, k) or not np.all(np.isfinite(ref)):
             raise ValueError(f"cov(a, b) must return a finite ({k}, {k}) matrix for two ({k}, d) row sets")
         scale = float(np.max(np.abs(ref))) if ref.size else 1.0
-        ta, tb = (t.cpu().numpy() for t in self._tri(k, X.device))
-        for bm in ("torch_pairs", "torch", "numpy_pairs", "numpy"):
+        for bm in ("torch", "numpy"):
             try:
                 C = self._eval(X, bm)
             except Exception:  # noqa: BLE001
                 continue
-            if tuple(C.shape) != ref.shape:
-                continue
-            Ch = C.cpu().numpy()
-            if bm.endswith("_pairs"):  # the factorisation reads the lower triangle only
-                Ch, R = Ch[:, ta, tb], ref[:, ta, tb]
-            else:
-                R = ref
-            if np.allclose(Ch, R, rtol=1e-13, atol=1e-15 * scale):
+            if tuple(C.shape) == ref.shape and np.allclose(C.cpu().numpy(), ref, rtol=1e-13, atol=1e-15 * scale):
                 self.mode = bm
                 return bm
         self.mode = ref_mode
@@ -309,21 +268,18 @@ class CallableCovariance:
         out = torch.empty((ne, rows), dtype=torch.float64, device=dev)
         if rows == 0:
             return out
-        ta, tb = self._tri(m + 1, dev)  # entry e = a (a+1)/2 + b: rows a, then b = 0..a
+        a = torch.arange(m + 1, device=dev)
+        ta = torch.repeat_interleave(a, a + 1)  # entry e = a (a+1)/2 + b: rows a, then b = 0..a
+        tb = torch.cat([torch.arange(int(k) + 1, device=dev) for k in range(m + 1)])
+        per_row = (m + 1) * (m + 1) * 8 * 3 + (m + 1) * coords.shape[1] * 8
+        chunk = max(1, min(rows, self.chunk_bytes // per_row))
         mode = self.resolve_mode(joint_points(coords, nbr[:min(rows, 4)], i0, qcoords, None if order is None else
                                               order[:min(rows, 4)]))
-        d = coords.shape[1]
-        # bytes per row of a chunk: the user's intermediates (~3 per entry) and the inputs
-        per_row = ne * 8 * (3 + 2 * d) if mode.endswith("_pairs") else (m + 1) * (m + 1) * 8 * 3 + (m + 1) * d * 8
-        chunk = max(1, min(rows, self.chunk_bytes // per_row))
         if mode.startswith("loop"):
             chunk = min(chunk, 4096)
         for r0 in range(0, rows, chunk):
             r1 = min(rows, r0 + chunk)
             X = joint_points(coords, nbr[r0:r1], i0, qcoords, None if order is None else order[r0:r1])
-            if mode.endswith("_pairs"):
-                out[:, r0:r1] = self._eval_pairs(X, mode).t()
-                continue
             C = self._eval(X, mode)
             if tuple(C.shape) != (r1 - r0, m + 1, m + 1):
                 raise ValueError(f"cov(a, b) returned {tuple(C.shape)} for {r1 - r0} joint blocks of {m + 1} rows")

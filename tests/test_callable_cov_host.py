@@ -87,7 +87,7 @@ def test_joint_points_and_blocks_layout():
     cov = _aniso(1.1, [[20.0, 3.0], [3.0, 9.0]])
     cc = CallableCovariance(cov, tau2=0.25)
     blk = cc.blocks(x, nbr)
-    assert cc.mode == "torch_pairs"  # broadcasts over two leading dims: the lower triangle's pairs only
+    assert cc.mode == "torch"
     assert blk.shape == (21, 50)
     t = 17
     C = cov(X[t].numpy(), X[t].numpy()) + 0.25 * np.eye(6)
@@ -96,7 +96,7 @@ def test_joint_points_and_blocks_layout():
             assert blk[a * (a + 1) // 2 + b, t].item() == pytest.approx(C[a, b], rel=1e-14, abs=1e-300)
 
 
-@pytest.mark.parametrize("which,mode", [("aniso", "torch_pairs"), ("loop", "loop")])
+@pytest.mark.parametrize("which,mode", [("aniso", "torch"), ("loop", "loop")])
 def test_mode_probe(which, mode):
     from pynngp_amd.nngp import CallableCovariance, joint_points
 
@@ -127,11 +127,9 @@ def test_numpy_batched_mode_and_forced_mode():
     nbr = torch.from_numpy(O.knn_prior(x.numpy(), 3))
     cc = CallableCovariance(np_only)
     b1 = cc.blocks(x, nbr)
-    assert cc.mode == "numpy_pairs"
+    assert cc.mode == "numpy"
     b2 = CallableCovariance(np_only, batch="loop").blocks(x, nbr)
     np.testing.assert_allclose(b1.numpy(), b2.numpy(), rtol=1e-15, atol=0)
-    b3 = CallableCovariance(np_only, batch="numpy").blocks(x, nbr)  # the whole square
-    np.testing.assert_allclose(b1.numpy(), b3.numpy(), rtol=1e-15, atol=0)
     with pytest.raises(ValueError):
         CallableCovariance(np_only, batch="gpu")
     with pytest.raises(TypeError):
@@ -148,20 +146,3 @@ def test_bad_plugin_raises():
     with pytest.raises(ValueError, match="finite"):
         CallableCovariance(lambda a, b: np.full((np.asarray(a).shape[-2], np.asarray(b).shape[-2]), np.nan)).blocks(
             x, nbr)
-
-
-def test_pairs_mode_equals_square_mode():
-    """The pairwise evaluation (lower triangle only) gives the square evaluation's entries."""
-    from pynngp_amd.nngp import CallableCovariance
-
-    rng = np.random.default_rng(9)
-    x = torch.from_numpy(rng.uniform(size=(300, 2)))
-    nbr = torch.from_numpy(O.knn_prior(x.numpy(), 12))
-    fn = _aniso(1.4, [[40.0, -10.0], [-10.0, 25.0]])
-    bp = CallableCovariance(fn, tau2=0.1).blocks(x, nbr)
-    bs = CallableCovariance(fn, tau2=0.1, batch="torch").blocks(x, nbr)
-    np.testing.assert_allclose(bp.numpy(), bs.numpy(), rtol=1e-15, atol=0)
-    # a plug-in that only takes 2-D row sets cannot take the pairs: the probe falls back
-    cc = CallableCovariance(_loop_only(1.0, 5.0))
-    cc.blocks(x, nbr[:10])
-    assert cc.mode == "loop"

@@ -88,7 +88,7 @@ def test_callable_sweep_vs_oracle(dev, form, m):
     v = torch.from_numpy(y).to(dev)
     nb = _lib.knn_prior(c, m)
     B, F, p = _sweep_any(cc, c, nb, 0, values=v, qvalues=v)
-    assert cc.mode == {"torch": "torch_pairs", "numpy": "numpy_pairs", "loop": "loop"}[form]
+    assert cc.mode == form
     assert p[2].item() == -1 and p[3].item() == -1
     Bo, Fo, po = O.bf_sweep_callable(x, nb.cpu().numpy(), _aniso(1.4, A1, 0.05), y)
     _check(B, F, p, Bo, Fo, po, n)
@@ -201,21 +201,3 @@ def test_isotropic_and_callable_agree_at_m28(dev):
     np.testing.assert_allclose(F1.cpu().numpy(), F2.cpu().numpy(), rtol=1e-10)
     assert torch.all((B1 - B2).abs() <= 1e-9 * (1 + B2.abs()))
     assert abs(p1[1].item() - p2[1].item()) <= 1e-11 * abs(p2[1].item())
-
-
-@pytest.mark.parametrize("mode", ["torch", "numpy"])
-def test_square_modes_equal_pairs(dev, mode):
-    """The whole-square evaluation (forced) factors to the same bits as the pairwise one."""
-    from pynngp_amd import CallableCovariance, _lib
-    from pynngp_amd.nngp import _sweep_any
-
-    rng = np.random.default_rng(21)
-    x = rng.uniform(size=(3000, 2))
-    y = rng.standard_normal(3000)
-    c, v = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
-    nb = _lib.knn_prior(c, 15)
-    f = _aniso(1.2, A1, 0.05) if mode == "torch" else _np_only(1.2, A1, 0.05)
-    B1, F1, p1 = _sweep_any(CallableCovariance(f), c, nb, 0, values=v, qvalues=v)
-    B2, F2, p2 = _sweep_any(CallableCovariance(f, batch=mode), c, nb, 0, values=v, qvalues=v)
-    np.testing.assert_allclose(F1.cpu().numpy(), F2.cpu().numpy(), rtol=1e-14)
-    assert torch.all((B1 - B2).abs() <= 1e-12 * (1 + B2.abs()))

@@ -70,11 +70,7 @@ cblk = cc.blocks(c, srt, 0, order=order)
 out["callable_mode"] = cc.mode
 out["callable_blocks_ms"] = timed(lambda: cc.blocks(c, srt, 0, order=order), reps=5)
 out["callable_sweep_ms"] = timed(lambda: _lib.bf_sweep_blocks(cblk, srt, n, 0, values=v, qvalues=v, order=order))
-sq = CallableCovariance(aniso, tau2=0.05, batch="torch")  # the whole (m+1)^2 square per block (round 4's first form)
-sblk = sq.blocks(c, srt, 0, order=order)
-out["callable_square_blocks_ms"] = timed(lambda: sq.blocks(c, srt, 0, order=order), reps=5)
-out["callable_pairs_vs_square_max_abs"] = float((sblk - cblk).abs().max())
-del cblk, sblk
+del cblk
 nb28 = _lib.knn_prior(c, 28)
 o28, s28 = _lib.row_order(c, 0, n, nb28)
 d28 = _lib.joint_dist(c, s28, 0, order=o28)
