@@ -453,6 +453,13 @@ hipError_t gibbs_member_rows_launch(const int32_t* members, int64_t n, const int
 // children.  Race-free within a colour (moral-graph colouring: no two members share a
 // child, and no member is another's child).
 
+// INLINE_Z: the normals are drawn inside the step (z == nullptr: Philox rounds, log and cos on the
+// critical path); otherwise read from z.  Two instantiations because a kernel's VGPR allocation is
+// static: the inline-Philox code held the z-given kernel -- the one every sampler runs -- at 70 VGPRs,
+// 7 waves per SIMD; without it 46 VGPRs, the 8-wave cap (round 4, profiles/r04l: 0.8022 -> 0.7885 ms per
+// Gibbs iteration at N = 1e6, median of 4 interleaved runs; the 8-wave cap binds, so asking the compiler
+// for more waves per SIMD changes nothing).
+template <bool INLINE_Z>
 __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ member_rows, int64_t n_members,
                                                      const double* __restrict__ Brev, const double* __restrict__ Grev,
                                                      const double* __restrict__ P, const double* __restrict__ invF,
@@ -524,7 +531,8 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
     const double it2i = noise_w != nullptr ? it2 * hi : it2;  // 1 / (tau2 / h_i)
     const double prec = fma(iF + Pi, is2, it2i);
     const double lin = fma(yi, it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
-    const double zi = z != nullptr ? zl : philox_normal(seed, (uint64_t)i, sweep);
+    double zi = zl;
+    if constexpr (INLINE_Z) zi = philox_normal(seed, (uint64_t)i, sweep);
     const double sd = nngp_rsqrt(prec);
     const double wn = fma(zi, sd, lin / prec);
     const double dw = wn - wi;
@@ -551,7 +559,8 @@ hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const 
         const int64_t a = color_off_host[c], b = color_off_host[c + 1];
         if (b <= a) continue;
         const int64_t threads = (b - a) * kGroup;
-        hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+        hipLaunchKernelGGL(z != nullptr ? gibbs_w_color<false> : gibbs_w_color<true>,
+                           dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                            (const int4*)member_rows + a, b - a, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2,
                            yres, noise_w, w, r, rev_j, z, seed, sweep, nullptr, nullptr, n * (int64_t)m);
     }
@@ -565,7 +574,8 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
     if (n_members <= 0) return hipSuccess;
     const GibbsPrep g = prep_layout((void*)prep, n, m);
     const int64_t threads = n_members * kGroup;
-    hipLaunchKernelGGL(gibbs_w_color, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(z != nullptr ? gibbs_w_color<false> : gibbs_w_color<true>,
+                       dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                        (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
                        noise_w, w, r, rev_j, z, seed, sweep, w_out, var, n * (int64_t)m);
     return hipGetLastError();
