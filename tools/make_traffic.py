@@ -10,6 +10,7 @@ and writes
     instruction and SIMD VALU busy);
   * profiles/traffic.json: one entry per preset kernel, which bench.py copies into the bench line's
     roofline.traffic and roofline_valu.
+Presets the tag did not measure keep their entries in profiles/traffic.json.
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024): on gfx950 FETCH_SIZE counts half the
 bytes of 16-B-per-lane streaming reads, WRITE_SIZE counts 16-B stores exactly
 (/opt/skills/guides/MI355X_MICROARCH.md, HBM / rocprofv3).  busy = sum over waves of VALU-active
@@ -34,7 +35,7 @@ PRESETS = {
     4: ({"n_per_gpu": 10_000_000, "m": 20, "kind": "exponential", "layout": "storage", "write_BF": True},
         [("sweep", "void nngp::bf_pairb<20, 0, 2>")]),
     5: ({"preset": 5, "n_per_gpu": 1_000_000, "m": 15, "kind": "exponential"},
-        [("sweep", "void nngp::bf_pairb<15, 0, 2>"), ("colour", "nngp::gibbs_w_color")]),
+        [("sweep", "void nngp::bf_pairb<15, 0, 2>"), ("colour", "void nngp::gibbs_w_color<false>")]),
 }
 BYTES_PER_LOC = {3: 36 * 15 + 32, 2: 36 * 15 + 32, 4: 36 * 20 + 32, 5: 36 * 15 + 32 + 8}
 ROWS = {3: 1e6, 2: 1e5, 4: 1e7, 5: 1e6}
@@ -62,7 +63,16 @@ def main():
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     doc = json.load(open(tpath)) if os.path.exists(tpath) else {"entries": []}
     doc["_doc"] = __doc__.split("\n\n")[0].strip() + " -- see tools/make_traffic.py for the definitions."
-    keep = []  # every entry is regenerated from this tag
+
+    def preset_of(e):
+        for q, (key, _) in PRESETS.items():
+            if all(e.get(k) == v for k, v in key.items()):
+                return q
+        return None
+
+    ran = [p for p in PRESETS if os.path.isdir(os.path.join(base, f"c{p}"))]
+    # the presets this tag measured are regenerated; the others keep their committed entries
+    keep = [e for e in doc.get("entries", []) if preset_of(e) not in ran]
     summary, lines = {}, [f"# Roofline provenance `{tag}` (tools/gpu_provenance.sh + tools/make_traffic.py)", ""]
     for p, (key, kernels) in PRESETS.items():
         d = os.path.join(base, f"c{p}")
