@@ -510,6 +510,15 @@ NNGP_FN double nngp_exp_unit(const CovParams& P, const double* tab, double u) {
     const double f = fma(P.nphi256, u, -k);               // |f| <= 1/2
     const int32_t ki = nngp_lo_dword(t);
     const double Tadj = tab[ki & (NNGP_EXP_TAB_N - 1)];   // 2^(j/256), high dword - (j << 12)
+    // the polynomial before the table value is first used: the LDS read (bank-conflicted random
+    // lookups) gets the polynomial's latency to land in (round 4, profiles/r04u: -0.8 %, same bits).
+    // The coefficients as literals (not CovParams fields): the persistent kernels re-materialise
+    // them instead of pinning 8 more SGPRs for the whole tile loop
+    constexpr double Q[4] = NNGP_EXP2_Q;
+    double q = fma(Q[3], f, Q[2]);
+    q = fma(q, f, Q[1]);
+    q = fma(q, f, Q[0]);
+    const double fq = f * q;
 #ifdef NNGP_MATH_HOST
     uint64_t bits;
     memcpy(&bits, &Tadj, 8);
@@ -521,13 +530,7 @@ NNGP_FN double nngp_exp_unit(const CovParams& P, const double* tab, double u) {
     const int32_t hi = (int32_t)(tb >> 32) + (int32_t)((uint32_t)ki << 12);
     const double Ts = __hiloint2double(hi, (int32_t)(tb & 0xffffffffll));  // 2^(j/256) 2^n
 #endif
-    // the coefficients as literals (not CovParams fields): the persistent kernels re-materialise
-    // them instead of pinning 8 more SGPRs for the whole tile loop
-    constexpr double Q[4] = NNGP_EXP2_Q;
-    double q = fma(Q[3], f, Q[2]);
-    q = fma(q, f, Q[1]);
-    q = fma(q, f, Q[0]);
-    return fma(Ts, f * q, Ts);
+    return fma(Ts, fq, Ts);
 }
 
 // unit-variance covariance of kind KIND at squared distance d2 (tab: nngp_exp_table_load_unit)
