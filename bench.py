@@ -428,6 +428,9 @@ def main():
     ap.add_argument("--single-chain", action="store_true",
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")
+    ap.add_argument("--plan", default="auto", choices=["auto", "on", "off"],
+                    help="tile pair plans (shared covariances evaluated once per tile; built with the neighbour "
+                         "sets, outside the timed region): auto = wherever they serve the sweep")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()
@@ -481,7 +484,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     sweep = ShardedLogLik(c, args.m, rank, world, algo=args.algo, spatial_order=not args.no_order,
-                          layout=args.layout, api=args.sweep_api, collective=distributed)
+                          layout=args.layout, api=args.sweep_api, collective=distributed,
+                          plan={"auto": None, "on": True, "off": False}[args.plan])
     if args.layout == "storage":
         # the synthetic field lives in the engine's storage order (an MCMC state would);
         # same iid N(0,1) values, assigned to locations in storage order
@@ -570,6 +574,10 @@ def main():
                 "row_order": "index" if args.no_order else "z-order",
                 "layout": args.layout,
                 "write_BF": want_bf,
+                "pair_plan": ({"tiles_planned": sweep._plan_ctypes.n_planned,
+                               "tiles_direct": sweep._plan_ctypes.n_direct, "build_s": sweep.plan_build_s,
+                               "bytes": int(sweep._plan[0].numel())}
+                              if sweep._plan_for(args.kind) is not None else None),
                 "sweep_api": "torch.ops.nngp.bf_sweep_out" if args.sweep_api == "ops" else "ctypes",
                 "global_batch": n_total,
                 "parallelism": f"dp{world} (contiguous Z-order location shards; the (4,) partials of every "

@@ -70,15 +70,17 @@ int32_t nngp_resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim,
 #define NNGP_MAX_M 63
 #define NNGP_MAX_DIM 3
 
-/* Library version string, e.g. "pynngp_amd 0.2.0 gfx950". */
+/* Library version string, e.g. "pynngp_amd 0.3.0 gfx950". */
 const char *nngp_version(void);
 
 /* ABI revision of this header (NNGP_ABI_VERSION), for a caller built against an older one to
  * refuse a library whose signatures moved.  Revision 2 (library 0.2.0) changed, relative to 1
  * (0.1.0): nngp_bf_finalize takes workspace_bytes as its 2nd argument; nngp_gibbs_w_sweep reads
  * (n, 4) member rows (nngp_gibbs_member_rows) and lost its `off` argument; nngp_bf_sweep /
- * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32. */
-#define NNGP_ABI_VERSION 2
+ * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32.  Revision 3
+ * (library 0.3.0) adds the tile pair plans (nngp_pair_plan_*, nngp_bf_sweep_plan); nothing
+ * earlier moved. */
+#define NNGP_ABI_VERSION 3
 int32_t nngp_abi_version(void);
 
 /* Message for the last error returned on the calling thread. */
@@ -165,6 +167,39 @@ int nngp_bf_sweep(const double *coords, int64_t n_points, int32_t dim, const int
  * sweep needed, so a mismatched call fails with NNGP_EINVAL instead of reading past it. */
 int nngp_bf_finalize(const void *workspace, size_t workspace_bytes, int64_t n_rows, int32_t m, int32_t kind,
                      int32_t dim, int32_t algo, double *partials, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Tile pair plans: the same sweep with every covariance a tile shares evaluated once.
+ * The pair kernel (NNGP_ALGO_PAIRB) sweeps tiles of ~128 consecutive rows; in a spatial visiting
+ * order neighbouring locations share most of their neighbours, so only ~36 % of a tile's joint-block
+ * entries are distinct point pairs (N = 1e6, m = 15).  A plan -- built once per (nbr, order, i0,
+ * n_points), like the neighbour sets -- lists per tile its distinct points and pairs and, per
+ * location, where each of its entries lives; nngp_bf_sweep_plan then evaluates each pair once into
+ * LDS and factors every location's block from there.  Same reference methods as nngp_bf_sweep
+ * (_CNs / _Ccross / _Cs / _Bsi / _Fsi, nngp.py:73-96); its B, F, R are bit-identical to
+ * nngp_bf_sweep's with NNGP_ALGO_PAIRB on the same arguments, and so are its partials (tiles whose
+ * points or pairs exceed the LDS budget are swept by the unplanned kernel into the same records).
+ * nngp_pair_plan_supported: 1 when plans serve (m, kind, dim): 2 <= m <= 18, kinds 0..4, dim 1..3.
+ * nngp_pair_plan_bytes: the plan buffer's size (0: unsupported m).
+ * nngp_pair_plan_build: builds the plan for the sweep's nbr / order / i0 / n_points (device
+ * pointers as nngp_bf_sweep; 256-B aligned plan) on `stream`, then SYNCHRONISES the stream (a setup
+ * call, the one exception to the no-synchronisation rule above) to fill the host array
+ * info[NNGP_PLAN_INFO_LEN]: tiles swept through the plan, tiles swept directly, then the geometry the
+ * plan was built for (n_rows, m, dim, i0, n_points) and a tag.  The plan stays valid while nbr and
+ * order are unchanged (the caller's responsibility, as for any cached factorisation).
+ * nngp_bf_sweep_plan: nngp_bf_sweep's arguments (algo PAIRB implied; kinds 0..4, no nu) plus the
+ * plan and its info; n_rows, m, dim, i0 and n_points must be those in info (checked).
+ * ------------------------------------------------------------------------- */
+#define NNGP_PLAN_INFO_LEN 8
+int nngp_pair_plan_supported(int32_t m, int32_t kind, int32_t dim);
+size_t nngp_pair_plan_bytes(int64_t n_rows, int32_t m, int32_t dim);
+int nngp_pair_plan_build(const int32_t *nbr, const int32_t *order, int64_t n_rows, int32_t m, int64_t i0,
+                         int64_t n_points, int32_t dim, void *plan, size_t plan_bytes, int64_t *info, void *stream);
+int nngp_bf_sweep_plan(const double *coords, int64_t n_points, int32_t dim, const int32_t *nbr, const int32_t *order,
+                       int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
+                       const double *values, double *B, double *F, double *R, double *partials, void *workspace,
+                       size_t workspace_bytes, const void *plan, size_t plan_bytes, const int64_t *info,
+                       void *stream);
 
 /* ---------------------------------------------------------------------------
  * B/F of query locations t against a reference set S (prediction / kriging at

@@ -11,7 +11,7 @@ from .sweep import ShardedLogLik, shard_range, combine_partials  # noqa: F401
 from .gibbs import SeqNNGP, Priors  # noqa: F401
 from .gibbs_sharded import ShardedSeqNNGP  # noqa: F401
 
-__version__ = "0.2.0"
+__version__ = "0.3.0"
 
 
 def load_ops():

@@ -55,6 +55,10 @@ SYMBOLS = (
     "nngp_gibbs_w_apply",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
+    "nngp_pair_plan_supported",
+    "nngp_pair_plan_bytes",
+    "nngp_pair_plan_build",
+    "nngp_bf_sweep_plan",
 )
 
 KIND_CODES = {"exponential": 0, "matern32": 1, "matern52": 2, "gaussian": 3, "spherical": 4, "matern": 5}
@@ -62,7 +66,8 @@ MATERN_NU_MAX = 50.0
 ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
-ABI_VERSION = 2  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
+ABI_VERSION = 3  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
+PLAN_INFO_LEN = 8  # NNGP_PLAN_INFO_LEN
 BLOCKS_MAX_M = 32  # nngp_bf_sweep_blocks: 1 <= m <= 32
 
 
@@ -159,6 +164,15 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
+    lib.nngp_pair_plan_supported.argtypes = [I32, I32, I32]
+    lib.nngp_pair_plan_supported.restype = ctypes.c_int
+    lib.nngp_pair_plan_bytes.argtypes = [I64, I32, I32]
+    lib.nngp_pair_plan_bytes.restype = SZ
+    lib.nngp_pair_plan_build.argtypes = [P, P, I64, I32, I64, I64, I32, P, SZ, P, P]
+    lib.nngp_pair_plan_build.restype = ctypes.c_int
+    lib.nngp_bf_sweep_plan.argtypes = [P, I64, I32, P, P, I64, I32, I64, I32, D, D, D, P, P, P, P, P, P, SZ, P, SZ, P,
+                                       P]
+    lib.nngp_bf_sweep_plan.restype = ctypes.c_int
     lib.nngp_check_partials.argtypes = [P, P, P]
     lib.nngp_check_partials.restype = ctypes.c_int
     lib.nngp_loglik_from_partials.argtypes = [P, I64]
@@ -319,15 +333,67 @@ def _check_kind(kind: str, nu: Optional[float]) -> float:
     return -1.0
 
 
+class PairPlan:
+    """A tile pair plan (``nngp_pair_plan_build``, include/nngp.h): the distinct covariance pairs of
+    every sweep tile and each location's map into them, for one (nbr, order, i0, n_points).  Passed to
+    :func:`bf_sweep` (``plan=``), it evaluates each shared covariance once per tile; B / F / R and the
+    partials are bit-identical to the unplanned pair kernel's.  The plan is stale once nbr or order
+    change (rebuild it, as the neighbour sets themselves)."""
+
+    def __init__(self, buf: torch.Tensor, info, nbr: torch.Tensor, order: Optional[torch.Tensor]):
+        self.buf = buf
+        self.info = (ctypes.c_int64 * PLAN_INFO_LEN)(*info)
+        self.n_planned, self.n_direct = int(info[0]), int(info[1])
+        self.n_rows, self.m, self.dim, self.i0, self.n_points = (int(v) for v in info[2:7])
+        self._nbr_ptr, self._order_ptr = nbr.data_ptr(), (order.data_ptr() if order is not None else 0)
+
+    def matches(self, nbr: torch.Tensor, order: Optional[torch.Tensor], i0: int, n_points: int, dim: int) -> bool:
+        """True when this plan was built for these (same storage) nbr / order and geometry."""
+        return (nbr.data_ptr() == self._nbr_ptr and (order.data_ptr() if order is not None else 0) == self._order_ptr
+                and tuple(nbr.shape) == (self.n_rows, self.m) and i0 == self.i0 and n_points == self.n_points
+                and dim == self.dim)
+
+
+def pair_plan_supported(m: int, kind: str, dim: int) -> bool:
+    """Whether tile pair plans serve (m, kind, dim) (2 <= m <= 18, kinds exponential .. spherical, dim 1..3)."""
+    return kind in KIND_CODES and bool(load().nngp_pair_plan_supported(int(m), KIND_CODES[kind], int(dim)))
+
+
+def pair_plan(nbr: torch.Tensor, n_points: int, dim: int, i0: int = 0,
+              order: Optional[torch.Tensor] = None) -> PairPlan:
+    """Build the tile pair plan of a sweep over ``nbr`` (int32 (rows, m) on the GPU; rows are locations
+    ``i0 + (order[t] if order else t)`` of an ``n_points``-point field of dimension ``dim``).  A setup
+    call: it synchronises torch's current stream once (the plan's tile counts come back to the host)."""
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError(f"nbr must be int32 (rows, m), got {nbr.dtype} {tuple(nbr.shape)}")
+    nbr = nbr.contiguous()
+    dev = _require_gpu(nbr, order)
+    rows, m = nbr.shape
+    if order is not None and (order.dtype != torch.int32 or order.shape != (rows,)):
+        raise ValueError("order must be int32 (rows,)")
+    lib = load()
+    nbytes = lib.nngp_pair_plan_bytes(rows, m, dim)
+    if nbytes == 0:
+        raise NNGPExtensionError(f"no pair plans for m={m}, dim={dim} (2 <= m <= 18, dim 1..3)")
+    buf = _workspace(nbytes, dev)
+    info = (ctypes.c_int64 * PLAN_INFO_LEN)()
+    _check(lib.nngp_pair_plan_build(_ptr(nbr), _ptr(order), rows, m, int(i0), int(n_points), int(dim), _ptr(buf),
+                                    buf.numel(), info, _stream(dev)), "nngp_pair_plan_build")
+    return PairPlan(buf, list(info), nbr, order)
+
+
 def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2: float, phi: float,
              tau2: float = 0.0, values: Optional[torch.Tensor] = None, want_bf: bool = True,
              algo: str = "auto", B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
              partials: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
              order: Optional[torch.Tensor] = None,
              R: Optional[torch.Tensor] = None,
-             defer: bool = False, nu: Optional[float] = None
+             defer: bool = False, nu: Optional[float] = None, plan: Optional[PairPlan] = None
              ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """Fused B/F + log-likelihood sweep over rows ``i0 .. i0 + len(nbr)``.
+
+    ``plan``: a :func:`pair_plan` of this nbr / order / i0 (the pair kernel with every shared
+    covariance evaluated once per tile; kinds exponential .. spherical, algo ``auto`` / ``pairb``).
 
     ``nu``: the smoothness of the ``matern`` kind (0 < nu <= 50; required there, ignored otherwise).
 
@@ -377,6 +443,17 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
     _check_out(R, "R", (rows,), dev)
     if workspace.device != dev or not workspace.is_contiguous():
         raise ValueError("workspace must be a contiguous tensor on the sweep's device")
+    if plan is not None:
+        if algo not in ("auto", "pairb"):
+            raise ValueError(f"a pair plan runs the pair kernel, not algo {algo!r}")
+        if not isinstance(plan, PairPlan) or plan.buf.device != dev:
+            raise ValueError("plan must be a PairPlan on the sweep's device")
+        _check(lib.nngp_bf_sweep_plan(_ptr(coords), coords.shape[0], d, _ptr(nbr), _ptr(order), rows, m, i0,
+                                      KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B),
+                                      _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace), workspace.numel(),
+                                      _ptr(plan.buf), plan.buf.numel(), plan.info, _stream(dev)),
+               "nngp_bf_sweep_plan")
+        return B, F, partials
     _check(lib.nngp_bf_sweep(_ptr(coords), coords.shape[0], d, _ptr(nbr), _ptr(order), rows, m, i0, KIND_CODES[kind],
                              float(sigma2), float(phi), float(tau2), nu, _ptr(values), _ptr(B), _ptr(F), _ptr(R),
                              _ptr(partials), _ptr(workspace), workspace.numel(), a, _stream(dev)),

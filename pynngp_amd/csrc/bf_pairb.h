@@ -48,6 +48,7 @@
 #include "bf_group.h"
 #include "nngp_internal.h"
 #include "nngp_math.h"
+#include "pair_plan.h"
 
 namespace nngp {
 
@@ -412,7 +413,17 @@ __device__ __forceinline__ double pr_rcp(double x) {
 // cblk[(a (a + 1) / 2 + b) * n_rows + t] (entry-major: one load instruction reads 32 consecutive
 // rows).  Slots with an invalid neighbour index are decoupled exactly (0 off the diagonal, 1 on it)
 // whatever the caller's values there; sigma2 = 1 (the blocks are the covariances themselves).
-template <int M, int KIND, int D>
+// Tile pair plans (pair_plan.h): PL = true reads the tile's distinct covariance pairs and its entry map from
+// the plan instead of gathering coordinates per location; tiles != null lists the tiles (regions) this
+// launch sweeps (the planned and the direct launches of a planned sweep), n_tiles = all regions.
+struct PairPlanArgs {
+    const uint8_t* slots = nullptr;   // region slots (pair_plan.h), region r at slots + r * slot_bytes
+    const int32_t* tiles = nullptr;   // logical block -> region, or null (block b sweeps tile b)
+    int64_t slot_bytes = 0;
+    int64_t n_tiles = 0;              // regions of the whole sweep (the record fold's count)
+};
+
+template <int M, int KIND, int D, bool PL = false>
 __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const double* __restrict__ coords, int64_t n_points,
                                                 const int32_t* __restrict__ nbr, const int32_t* __restrict__ order,
                                                 int64_t n_rows, int64_t i0, const CovParams Pc, double sigma2,
@@ -421,7 +432,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim,
                                                 const double* __restrict__ cblk, int64_t tq, int64_t trem,
-                                                int64_t* __restrict__ hdr, double* __restrict__ fused) {
+                                                int64_t* __restrict__ hdr, double* __restrict__ fused,
+                                                const PairPlanArgs pp) {
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
@@ -432,6 +444,18 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
     constexpr bool LEFT = pairb_lk(M, KIND);
+    static_assert(!PL || (!CM && !MT && !LEFT && D >= 1 && M >= kPlanMinM && M <= kPlanMaxM),
+                  "pair plans: the right-looking fused kinds, 1 <= D <= 3");
+    // the planned kernel's LDS: the tile's points (coordinates, values) and its distinct covariances
+    constexpr int PCS = plan_cs(D >= 1 ? D : 1);
+    constexpr int PE = PL ? plan_ecap(M, D >= 1 ? D : 1) + 1 : 1;  // covariance slots (slot 0: exact zero)
+    constexpr int PU = PL ? kPlanUMax : 1;
+    constexpr int KE = (PE - 1 + kPairbThreads - 1) / kPairbThreads;  // pair words per thread (max)
+    // points first (LDS address 0: a pair word's byte offsets are their addresses), then the covariances
+    // (sized for every lane of the last pair group: lanes past nE store into slots no entry reads)
+    __shared__ double ucrd[PU * PCS];
+    __shared__ double uval[PU];
+    __shared__ double ptab[PL ? KE * kPairbThreads + 1 : 1];
     constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
     constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
                           (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
@@ -457,8 +481,9 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     }
 
     __shared__ double sh[1][kPairbWaves][5];
-    const int64_t tile = xcd_logical_block(blockIdx.x, gridDim.x);
-    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = gridDim.x;  // the tile count, for the record fold
+    const int64_t ltile = xcd_logical_block(blockIdx.x, gridDim.x);
+    const int64_t tile = pp.tiles != nullptr ? (int64_t)__builtin_amdgcn_readfirstlane(pp.tiles[ltile]) : ltile;
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[0] = pp.tiles != nullptr ? pp.n_tiles : gridDim.x;  // for the record fold
     const int q = (int)(threadIdx.x & 1);
     const bool q1 = q == 1;
     const bool lead0 = !q1;
@@ -481,7 +506,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
             const int a = 2 * s + q;
-            jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
+            jn[s] = PL ? -1 : nbr[rl * M + (a < M ? a : M - 1)];
         }
         double o[NP][DA], z[NP];
         // one unsigned compare per slot (a negative index is out of range as a huge unsigned);
@@ -501,19 +526,21 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const double* pc = self ? qcoords + i * ds : (in_range ? coords + (int64_t)j * ds : far_point<DA>(a));
             const double* pv = self ? (qvalues != nullptr ? qvalues + i : kZeroValue)
                                     : ((values != nullptr && in_range) ? values + j : kZeroValue);
-            if constexpr (CM) {
+            if constexpr (CM || PL) {
             } else if constexpr (D == 0) {
                 load_point_rt(pc, dim, o[s]);
             } else {
                 load_point<D>(pc, o[s]);
             }
-            if constexpr (!LEFT) z[s] = *pv;  // (the left-looking kernel gathers the values late)
+            if constexpr (!LEFT && !PL) z[s] = *pv;  // (the left-looking kernel gathers the values late)
         }
         if constexpr (ZLDS) {
 #pragma unroll
             for (int s = 0; s < NP; ++s) zsh[s][threadIdx.x] = z[s];  // read back by this thread only
         }
         const bool bad_index = (int64_t)jmax >= n_points || jmin < -1;
+        const uint8_t* pslot = PL ? pp.slots + tile * pp.slot_bytes : nullptr;
+        double badi_plan = INFINITY;
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
@@ -522,7 +549,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const double4* g = (const double4*)cblk;
             for (int k = (int)threadIdx.x; k < n4; k += kPairbThreads) pairb_mtab[k] = g[k];
             __syncthreads();
-        } else if constexpr (!CM) {
+        } else if constexpr (!CM && !PL) {
 #pragma unroll
             for (int e = 0; e < kTabPer; ++e)
                 if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
@@ -533,6 +560,121 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         double R[NP][NP][2];
         bool bad = false;
         double Fu, res;
+        if constexpr (PL) {
+            // ---- the tile's plan (pair_plan.h): this lane's entry map and row indices first (their loads
+            // overlap the staging below), then the points, the distinct pairs, the joint block from LDS
+            constexpr int CHE = plan_map_chunks(M), CHL = plan_loc_chunks(M);
+            // (block-uniform: scalar loads and branches)
+            const int nU = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[0]);
+            const int nE = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[1]);
+            badi_plan = threadIdx.x == 0 ? ((const double*)pslot)[1] : INFINITY;  // the region's first bad location
+            // the slot through a buffer descriptor (uniform base, per-lane voffset, per-load soffset: no
+            // 64-bit address arithmetic per load)
+            const __amdgpu_buffer_rsrc_t srd =
+                __builtin_amdgcn_make_buffer_rsrc((void*)pslot, (short)0, (int)pp.slot_bytes, 0x00020000);
+            uint32_t mw[4 * (CHE + CHL)];
+#pragma unroll
+            for (int c = 0; c < CHE + CHL; ++c) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srd, kPlanMapOff + 16 * (int)threadIdx.x,
+                                                                      c * kPairbThreads * 16, 0);
+                mw[4 * c] = v.x;
+                mw[4 * c + 1] = v.y;
+                mw[4 * c + 2] = v.z;
+                mw[4 * c + 3] = v.w;
+            }
+            const int32_t* ul = (const int32_t*)(pslot + kPlanUOff);
+            for (int u = (int)threadIdx.x; u < nU; u += kPairbThreads) {
+                const int64_t g = ul[u];
+                double x[DA];
+                load_point<DA>(coords + g * ds, x);
+#pragma unroll
+                for (int k = 0; k < DA; ++k) ucrd[(u + 1) * PCS + k] = x[k];
+                uval[u + 1] = values != nullptr ? values[g] : 0.0;
+            }
+            const int nit = (nE + kPairbThreads - 1) / kPairbThreads;  // block-uniform
+            uint32_t pwd[KE];
+#pragma unroll
+            for (int it = 0; it < KE; ++it)  // (words past nE inside the slot's pair area: unused)
+                pwd[it] = it < nit ? __builtin_amdgcn_raw_buffer_load_b32(srd, kPlanPairOff + 4 * (int)threadIdx.x,
+                                                                          it * kPairbThreads * 4, 0)
+                                   : 0u;
+#pragma unroll
+            for (int e = 0; e < kTabPer; ++e)
+                if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
+                    etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
+            if (threadIdx.x == 0) {
+                ptab[0] = 0.0;
+                uval[0] = 0.0;
+#pragma unroll
+                for (int c = 0; c < PCS; ++c) ucrd[c] = 0.0;  // (read by a group's unused tail)
+            }
+            __syncthreads();
+            NNGP_PHASE(plan_pairs);
+            // each distinct pair once, block-cooperatively (the unplanned kernel's nngp_cov_unit on the same
+            // operands: (a - b)^2 == (b - a)^2 bit for bit)
+            // in groups of PG pairs per thread: all of a group's point reads are issued before its
+            // arithmetic, so the LDS latency overlaps (a group past nE reads slot 0 and stores nothing)
+            constexpr int PG = 4;
+#pragma unroll
+            for (int g = 0; g < (KE + PG - 1) / PG; ++g) {
+                if (PG * g < nit) {  // block-uniform
+                    double xa[PG][DA], xb[PG][DA];
+#pragma unroll
+                    for (int j = 0; j < PG; ++j) {
+                        const int it = PG * g + j;
+                        const uint32_t w = it < KE ? pwd[it < KE ? it : 0] : 0u;  // LDS byte offsets of both points
+                        const double* pa = (const double*)((const char*)ucrd + (w & 0xffffu));
+                        const double* pb = (const double*)((const char*)ucrd + (w >> 16));
+                        if constexpr (DA == 2) {
+                            const double2 va = *(const double2*)pa, vb = *(const double2*)pb;
+                            xa[j][0] = va.x;
+                            xa[j][1] = va.y;
+                            xb[j][0] = vb.x;
+                            xb[j][1] = vb.y;
+                        } else {
+#pragma unroll
+                            for (int c = 0; c < DA; ++c) {
+                                xa[j][c] = pa[c];
+                                xb[j][c] = pb[c];
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < PG; ++j) {
+                        const int it = PG * g + j;
+                        const int k = (int)threadIdx.x + it * kPairbThreads;
+                        if (it < KE)  // branch-free: lanes past nE store into slots past nE (no entry reads them)
+                            ptab[k + 1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(xa[j], xb[j]));
+                    }
+                }
+            }
+            __syncthreads();
+            NNGP_PHASE(plan_fill);
+            // the joint block in the unplanned kernel's register order (pair_plan.h plan_entry): entry e's
+            // LDS byte offset is u16 half e & 1 of map word e >> 1
+            auto rd = [&](int e) -> double {
+                const uint32_t off = (e & 1) ? (mw[e >> 1] >> 16) : (mw[e >> 1] & 0xffffu);
+                return *(const double*)((const char*)ptab + off);
+            };
+            int e = 0;
+#pragma unroll
+            for (int s = 0; s < NP; ++s) {
+#pragma unroll
+                for (int t = 0; t < s; ++t) {
+                    R[s][t][0] = rd(e++);
+                    R[s][t][1] = rd(e++);
+                }
+                R[s][s][0] = Pc.diag;
+                R[s][s][1] = rd(e++);
+            }
+#pragma unroll
+            for (int s = 0; s < NP; ++s) {
+                const int h = 4 * CHE + (s >> 1);
+                const uint32_t u = (s & 1) ? (mw[h] >> 16) : (mw[h] & 0xffffu);
+                z[s] = uval[u];
+            }
+        }
         if constexpr (CM) {
             // ---- covariances from the caller's blocks, own-parity-first order.  vm: bit a set when
             // joint row a holds a point (a valid neighbour slot, or a = M); this lane's rows, then the
@@ -573,7 +715,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         if constexpr (!LEFT) {
         NNGP_PHASE(covariances);
         // ---- unit-variance covariances in own-parity-first order
-        if constexpr (!CM) {
+        if constexpr (!CM && !PL) {
             double p[NP][DA];
 #pragma unroll
             for (int t = 0; t < NP; ++t)
@@ -928,7 +1070,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         // into the mantissa product as log(NaN) would; the flag is what callers check)
         pairb_tile_store(lead ? __builtin_amdgcn_frexp_mant(F) : 1.0, lead ? __builtin_amdgcn_frexp_exp(F) : 0,
                          lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)i : INFINITY,
-                         (live && bad_index) ? (double)i : INFINITY, sh, 0, rec, lexp, tile);
+                         PL ? badi_plan : ((live && bad_index) ? (double)i : INFINITY), sh, 0, rec, lexp, tile);
         __syncthreads();
         if (fused == nullptr) {
             if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
@@ -998,14 +1140,51 @@ inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
     return (int32_t*)((char*)ws + kPairbHeader + pairb_align((size_t)pairb_tiles_bound(n_rows) * 32));
 }
 
-template <int M, int KIND, int D>
-static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
+// a.tiles != null: sweep only the listed tiles (a planned sweep's direct regions, pair_plan.h), a.n_tiles
+// being the whole sweep's count; the records are then the caller's to fold (never fused)
+template <int M, int KIND, int D, bool PL = false>
+static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s, const PairPlanArgs* ppl = nullptr) {
     const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
     const PairbTiling tl = pairb_tiling(a.n_rows, M, KIND);
-    hipLaunchKernelGGL((bf_pairb<M, KIND, D>), dim3((unsigned)tl.tiles), dim3(kPairbThreads), lds, s, a.coords,
+    PairPlanArgs pp = ppl != nullptr ? *ppl : PairPlanArgs{};
+    if (!PL && a.tiles != nullptr) {
+        pp.tiles = a.tiles;
+        pp.n_tiles = a.n_tiles;
+    }
+    const int64_t nb = PL ? a.n_plan_blocks : (a.tiles != nullptr ? a.n_tile_list : tl.tiles);
+    if (nb == 0) return;
+    hipLaunchKernelGGL((bf_pairb<M, KIND, D, PL>), dim3((unsigned)nb), dim3(kPairbThreads), lds, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
                        a.qcoords, a.qvalues, a.B, a.F, a.R, pairb_rec(a.bpart), pairb_lexp(a.bpart, a.n_rows), a.dim,
-                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart), pairb_fuse_fold(a) ? a.partials : nullptr);
+                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart),
+                       pairb_fuse_fold(a) && pp.tiles == nullptr ? a.partials : nullptr, pp);
+}
+
+// the planned regions of a planned sweep (pair_plan.h; the direct ones go through bf_pairb_launch with
+// a.tiles = the direct list)
+template <int M, int KIND, int D>
+static void launch_pairb_planned_mkd(const BfArgs& a, const CovParams& Pc, const PlanLaunch& pl, hipStream_t s) {
+    PairPlanArgs pp;
+    pp.slots = pl.plan + kPlanGlobalHdr;
+    pp.slot_bytes = pl.slot_bytes;
+    pp.n_tiles = pl.n_regions;
+    pp.tiles = pl.planned;
+    BfArgs b = a;
+    b.n_plan_blocks = pl.n_planned;
+    launch_pairb_mkd<M, KIND, D, true>(b, Pc, s, &pp);
+}
+
+template <int M, int D>
+static bool launch_pairb_planned_if(const BfArgs& a, const CovParams& Pc, const PlanLaunch& pl, hipStream_t s) {
+    if (a.m != M || a.dim != D) return false;
+    switch (a.kind) {
+        case 0: launch_pairb_planned_mkd<M, 0, D>(a, Pc, pl, s); return true;
+        case 1: launch_pairb_planned_mkd<M, 1, D>(a, Pc, pl, s); return true;
+        case 2: launch_pairb_planned_mkd<M, 2, D>(a, Pc, pl, s); return true;
+        case 3: launch_pairb_planned_mkd<M, 3, D>(a, Pc, pl, s); return true;
+        case 4: launch_pairb_planned_mkd<M, 4, D>(a, Pc, pl, s); return true;
+        default: return false;
+    }
 }
 
 // m = 25..32: one instantiation per m for every kind and dimension (runtime kind NNGP_KIND_GENERIC,

@@ -321,4 +321,26 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
     return bf_finalize_launch(a.bpart, nb, a.partials, s);
 }
 
+// a planned sweep (pair_plan.h): the plan's regions through the planned kernel, the direct ones through
+// the unplanned kernel (same tiling, same records), then the fold
+hipError_t bf_launch_planned(const BfArgs& a, const PlanLaunch& pl, hipStream_t s) {
+    if (a.n_rows == 0)
+        return a.partials != nullptr ? bf_finalize_launch(a.bpart, 0, a.partials, s) : hipSuccess;
+    const CovParams Pu = nngp_cov_params_unit(a.kind, a.phi, a.tau2 / a.sigma2);
+    if (pl.n_planned > 0 && !bf_pairb_planned_launch(a, Pu, pl, s)) return hipErrorInvalidValue;
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (pl.n_direct > 0) {
+        BfArgs b = a;
+        b.tiles = pl.direct;
+        b.n_tiles = pl.n_regions;
+        b.n_tile_list = pl.n_direct;
+        if (!bf_pairb_launch(b, Pu, s)) return hipErrorInvalidValue;
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (a.partials == nullptr) return hipSuccess;
+    return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
+}
+
 }  // namespace nngp

@@ -59,7 +59,7 @@ int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_coun
 
 extern "C" {
 
-const char* nngp_version(void) { return "pynngp_amd 0.2.0 gfx950"; }
+const char* nngp_version(void) { return "pynngp_amd 0.3.0 gfx950"; }
 
 int32_t nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 
@@ -173,6 +173,89 @@ int nngp_bf_cross(const double* ref, int64_t n_ref, int32_t dim, const double* q
         return fail(NNGP_EINVAL, "query_values need ref_values");
     return bf_common(ref, n_ref, dim, query, n_query, nbr, order, n_rows, m, q0, kind, sigma2, phi, tau2, nu, ref_values,
                      query_values, B, F, R, partials, workspace, workspace_bytes, algo, stream);
+}
+
+int nngp_pair_plan_supported(int32_t m, int32_t kind, int32_t dim) {
+    return nngp::bf_pairb_planned_supported(m, kind, dim) ? 1 : 0;
+}
+
+size_t nngp_pair_plan_bytes(int64_t n_rows, int32_t m, int32_t dim) {
+    if (n_rows < 0 || n_rows > INT32_MAX || !nngp::bf_pairb_planned_supported(m, 0, dim)) return 0;
+    return (size_t)nngp::plan_total_bytes(n_rows, m);
+}
+
+int nngp_pair_plan_build(const int32_t* nbr, const int32_t* order, int64_t n_rows, int32_t m, int64_t i0,
+                         int64_t n_points, int32_t dim, void* plan, size_t plan_bytes, int64_t* info, void* stream) {
+    if (plan == nullptr || info == nullptr || (n_rows > 0 && nbr == nullptr))
+        return fail(NNGP_EINVAL, "plan, info (and nbr for n_rows > 0) must be non-null");
+    if (!nngp::bf_pairb_planned_supported(m, 0, dim))
+        return fail(NNGP_EUNSUP, "pair plans serve 2 <= m <= 18, dim 1..3 (m=%d, dim=%d)", m, dim);
+    if (n_rows < 0 || n_rows > INT32_MAX || i0 < 0 || n_points < 1 || i0 + n_rows > n_points || n_points > INT32_MAX)
+        return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld) (or n_rows / n_points >= 2^31)", (long long)i0,
+                    (long long)(i0 + n_rows), (long long)n_points);
+    if (((uintptr_t)plan & 255) != 0) return fail(NNGP_EINVAL, "plan must be 256-byte aligned");
+    const size_t need = (size_t)nngp::plan_total_bytes(n_rows, m);
+    if (plan_bytes < need) return fail(NNGP_EINVAL, "plan too small: %zu < %zu bytes", plan_bytes, need);
+    hipStream_t s = (hipStream_t)stream;
+    const nngp::PairbTiling tl = nngp::pairb_tiling(n_rows, m, 0);
+    if (tl.tiles != nngp::plan_regions(n_rows)) return fail(NNGP_EUNSUP, "plan regions differ from the pair tiling");
+    hipError_t e = nngp::pair_plan_build_launch(nbr, order, n_rows, m, dim, i0, n_points, tl.q, tl.rem,
+                                                nngp::plan_ecap(m, dim), plan, s);
+    if (e != hipSuccess) return hip_fail(e, "pair_plan build");
+    nngp::PlanHeader h;
+    e = hipMemcpyAsync(&h, plan, sizeof h, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "pair_plan counts");
+    info[0] = h.n_planned;
+    info[1] = h.n_direct;
+    info[2] = n_rows;
+    info[3] = m;
+    info[4] = dim;
+    info[5] = i0;
+    info[6] = n_points;
+    info[7] = nngp::kPlanMagic;
+    return NNGP_OK;
+}
+
+int nngp_bf_sweep_plan(const double* coords, int64_t n_points, int32_t dim, const int32_t* nbr, const int32_t* order,
+                       int64_t n_rows, int32_t m, int64_t i0, int32_t kind, double sigma2, double phi, double tau2,
+                       const double* values, double* B, double* F, double* R, double* partials, void* workspace,
+                       size_t workspace_bytes, const void* plan, size_t plan_bytes, const int64_t* info,
+                       void* stream) {
+    if (coords == nullptr || workspace == nullptr || plan == nullptr || info == nullptr)
+        return fail(NNGP_EINVAL, "coordinates, workspace, plan and info must be non-null");
+    if (info[7] != nngp::kPlanMagic || info[2] != n_rows || info[3] != m || info[4] != dim || info[5] != i0 ||
+        info[6] != n_points)
+        return fail(NNGP_EINVAL, "the plan was built for (n_rows %lld, m %lld, dim %lld, i0 %lld, n_points %lld), not "
+                                 "this sweep's (%lld, %d, %d, %lld, %lld)", (long long)info[2], (long long)info[3],
+                    (long long)info[4], (long long)info[5], (long long)info[6], (long long)n_rows, m, dim,
+                    (long long)i0, (long long)n_points);
+    if (!nngp::bf_pairb_planned_supported(m, kind, dim))
+        return fail(NNGP_EUNSUP, "planned sweeps serve kinds 0..4, 2 <= m <= 18, dim 1..3 (kind=%d)", kind);
+    if (plan_bytes < (size_t)nngp::plan_total_bytes(n_rows, m)) return fail(NNGP_EINVAL, "plan too small");
+    const int64_t nreg = nngp::plan_regions(n_rows);
+    if (info[0] < 0 || info[1] < 0 || info[0] + info[1] != nreg)
+        return fail(NNGP_EINVAL, "plan counts %lld + %lld != %lld tiles", (long long)info[0], (long long)info[1],
+                    (long long)nreg);
+    // the unplanned sweep's argument checks (same kernel family, same workspace)
+    if (m < 1 || (n_rows > 0 && nbr == nullptr)) return fail(NNGP_EINVAL, "nbr must be non-null");
+    if (!(sigma2 > 0.0) || !(phi > 0.0) || !(tau2 >= 0.0) || !isfinite(sigma2) || !isfinite(phi) || !isfinite(tau2))
+        return fail(NNGP_EINVAL, "theta must satisfy sigma2 > 0, phi > 0, tau2 >= 0 (finite)");
+    if (B != nullptr && F == nullptr) return fail(NNGP_EINVAL, "B given without F");
+    if (F != nullptr && B == nullptr && n_rows > 0) return fail(NNGP_EINVAL, "F given without B");
+    if (R != nullptr && values == nullptr) return fail(NNGP_EINVAL, "R (residuals) needs values");
+    if (((uintptr_t)workspace & 255) != 0) return fail(NNGP_EINVAL, "workspace must be 256-byte aligned");
+    const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, NNGP_ALGO_PAIRB);
+    if (workspace_bytes < need) return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
+    const uint8_t* p = (const uint8_t*)plan;
+    const int64_t sb = nngp::plan_slot_bytes(m);
+    const int32_t* planned = (const int32_t*)(p + nngp::kPlanGlobalHdr + nreg * sb);
+    nngp::PlanLaunch pl{p, nreg, info[0], info[1], sb, planned, planned + nreg};
+    nngp::BfArgs args{coords, n_points, nbr, n_rows, i0, m, kind, dim, sigma2, phi, tau2, 0.0, order, values, coords,
+                      values, B, F, R, partials, (double*)workspace};
+    hipError_t e = nngp::bf_launch_planned(args, pl, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "bf_sweep_plan launch");
+    return NNGP_OK;
 }
 
 int64_t nngp_joint_entries(int32_t m) { return m < 0 ? 0 : (int64_t)(m + 1) * (m + 2) / 2; }

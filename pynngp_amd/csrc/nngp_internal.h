@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "nngp_math.h"
+#include "pair_plan.h"
 
 namespace nngp {
 
@@ -98,6 +99,10 @@ struct BfArgs {
     double* partials;          // [4]
     double* bpart;             // 4 doubles per block: sum log F, sum r^2/F, first bad-pivot row, first bad-index row
     const double* cblk = nullptr;  // NNGP_KIND_BLOCKS: the joint blocks' covariances (bf_pairb.h), entry-major
+    // pair kernel, planned sweeps (pair_plan.h): sweep only the n_tile_list tiles listed in `tiles` (of
+    // n_tiles in all), or, for the planned launch, n_plan_blocks regions of the plan
+    const int32_t* tiles = nullptr;
+    int64_t n_tiles = 0, n_tile_list = 0, n_plan_blocks = 0;
 };
 
 int64_t bf_record_count(int64_t n_rows, int algo, int m);
@@ -111,6 +116,13 @@ bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
 bool bf_pairb_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS (bf_pairb.h)
+// tile pair plans (pair_plan.h, pair_plan.hip)
+bool bf_pairb_planned_supported(int m, int kind, int dim);
+bool bf_pairb_planned_launch(const BfArgs& a, const CovParams& P, const PlanLaunch& pl, hipStream_t s);
+hipError_t bf_launch_planned(const BfArgs& a, const PlanLaunch& pl, hipStream_t s);
+size_t pair_plan_build_lds(int m);
+hipError_t pair_plan_build_launch(const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int dim, int64_t i0,
+                                  int64_t n_points, int64_t tq, int64_t trem, int ecap, void* plan, hipStream_t s);
 bool bf_pairb_blocks_supported(int m);
 bool bf_group_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS at m = 25..32 (bf_group.h)
 bool bf_group_blocks_supported(int m);

@@ -115,7 +115,8 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
                   int64_t kind, double sigma2, double phi, double tau2, const c10::optional<at::Tensor>& values,
                   const c10::optional<at::Tensor>& B, const c10::optional<at::Tensor>& F,
                   const c10::optional<at::Tensor>& R, const at::Tensor& partials, const at::Tensor& ws,
-                  int64_t algo, double nu) {
+                  int64_t algo, double nu, const c10::optional<at::Tensor>& plan,
+                  const c10::optional<at::Tensor>& plan_info) {
     check_coords(coords, "coords");
     const at::OptionalDeviceGuard guard(coords.device());
     check_nbr(nbr, coords);
@@ -132,6 +133,22 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
     check_f64(partials, {4}, coords, "partials");
     TORCH_CHECK(ws.is_contiguous(), "workspace must be contiguous");
     check_same_device(coords, ws, "workspace");
+    if (plan.has_value()) {
+        // a tile pair plan (pair_plan op): the pair kernel with every shared covariance evaluated once per tile
+        TORCH_CHECK(plan_info.has_value() && plan_info->device().is_cpu() && plan_info->scalar_type() == at::kLong &&
+                        plan_info->numel() == NNGP_PLAN_INFO_LEN && plan_info->is_contiguous(),
+                    "plan_info must be the pair_plan op's CPU int64 (", NNGP_PLAN_INFO_LEN, ",) tensor");
+        TORCH_CHECK(plan->scalar_type() == at::kByte && plan->is_contiguous(), "plan must be a contiguous uint8 tensor");
+        check_same_device(coords, *plan, "plan");
+        TORCH_CHECK(algo == NNGP_ALGO_AUTO || algo == NNGP_ALGO_PAIRB, "a pair plan runs the pair kernel (algo ", algo, ")");
+        check_rc(nngp_bf_sweep_plan(coords.data_ptr<double>(), n, (int32_t)d, nbr.data_ptr<int32_t>(), ptr<int32_t>(order),
+                                    rows, (int32_t)m, i0, (int32_t)kind, sigma2, phi, tau2, ptr<double>(values),
+                                    ptr<double>(B), ptr<double>(F), ptr<double>(R), partials.data_ptr<double>(),
+                                    ws.data_ptr(), (size_t)ws.nbytes(), plan->data_ptr(), (size_t)plan->nbytes(),
+                                    plan_info->data_ptr<int64_t>(), stream(coords)),
+                 "nngp_bf_sweep_plan");
+        return;
+    }
     check_rc(nngp_bf_sweep(coords.data_ptr<double>(), n, (int32_t)d, nbr.data_ptr<int32_t>(), ptr<int32_t>(order), rows,
                            (int32_t)m, i0, (int32_t)kind, sigma2, phi, tau2, nu, ptr<double>(values), ptr<double>(B),
                            ptr<double>(F), ptr<double>(R), partials.data_ptr<double>(), ws.data_ptr(),
@@ -156,7 +173,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_sweep(const at::Tensor& coords
                                                                (int32_t)coords.size(1), (int32_t)algo), coords);
     bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values,
                  want_bf ? c10::optional<at::Tensor>(B) : c10::nullopt,
-                 want_bf ? c10::optional<at::Tensor>(F) : c10::nullopt, c10::nullopt, p, ws, algo, nu);
+                 want_bf ? c10::optional<at::Tensor>(F) : c10::nullopt, c10::nullopt, p, ws, algo, nu, c10::nullopt,
+                 c10::nullopt);
     return {B, F, p};
 }
 
@@ -186,6 +204,30 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
     // R = 0 - B_t v_N: the kriging mean is -R (zeros without reference values)
     at::Tensor mean = ref_values.has_value() ? R.neg() : at::zeros({rows}, f64);
     return {B, F, mean};
+}
+
+// the tile pair plan of a sweep over nbr (include/nngp.h nngp_pair_plan_build): (plan bytes on the GPU,
+// CPU int64 info).  A setup call: it synchronises the tensors' stream once.
+std::tuple<at::Tensor, at::Tensor> pair_plan(const at::Tensor& nbr, const c10::optional<at::Tensor>& order, int64_t i0,
+                                             int64_t n_points, int64_t dim) {
+    TORCH_CHECK(nbr.is_cuda(), "nbr must be a ROCm GPU tensor (there is no CPU fallback)");
+    const at::OptionalDeviceGuard guard(nbr.device());
+    check_nbr(nbr, nbr);
+    const int64_t rows = nbr.size(0), m = nbr.size(1);
+    if (order.has_value()) {
+        TORCH_CHECK(order->scalar_type() == at::kInt && order->sizes() == at::IntArrayRef{rows} && order->is_contiguous(),
+                    "order must be a contiguous int32 (rows,) tensor");
+        check_same_device(nbr, *order, "order");
+    }
+    const size_t bytes = nngp_pair_plan_bytes(rows, (int32_t)m, (int32_t)dim);
+    TORCH_CHECK(bytes > 0, "no pair plans for m=", m, ", dim=", dim, " (2 <= m <= 18, dim 1..3)");
+    auto plan = workspace((int64_t)bytes, nbr);
+    auto info = at::empty({NNGP_PLAN_INFO_LEN}, at::TensorOptions().dtype(at::kLong));
+    check_rc(nngp_pair_plan_build(nbr.data_ptr<int32_t>(), ptr<int32_t>(order), rows, (int32_t)m, i0, n_points,
+                                  (int32_t)dim, plan.data_ptr(), (size_t)plan.nbytes(), info.data_ptr<int64_t>(),
+                                  stream(nbr)),
+             "nngp_pair_plan_build");
+    return {plan, info};
 }
 
 std::tuple<at::Tensor, at::Tensor> row_order(const at::Tensor& coords, int64_t i0, int64_t rows,
@@ -236,7 +278,8 @@ TORCH_LIBRARY(nngp, m) {
           "bool want_bf, int algo, Tensor? order=None, float nu=-1.0) -> (Tensor, Tensor, Tensor)");
     m.def("bf_sweep_out(Tensor coords, Tensor nbr, Tensor? order, int i0, int kind, float sigma2, float phi, "
           "float tau2, Tensor? values, Tensor(a!)? B, Tensor(b!)? F, Tensor(c!)? R, Tensor(d!) partials, "
-          "Tensor(e!) workspace, int algo, float nu=-1.0) -> ()");
+          "Tensor(e!) workspace, int algo, float nu=-1.0, Tensor? plan=None, Tensor? plan_info=None) -> ()");
+    m.def("pair_plan(Tensor nbr, Tensor? order, int i0, int n_points, int dim) -> (Tensor, Tensor)");
     m.def("bf_cross(Tensor ref, Tensor query, Tensor nbr, int kind, float sigma2, float phi, float tau2, "
           "Tensor? ref_values, int algo, float nu=-1.0) -> (Tensor, Tensor, Tensor)");
     m.def("row_order(Tensor coords, int i0, int rows, Tensor? nbr) -> (Tensor, Tensor)");
@@ -251,5 +294,6 @@ TORCH_LIBRARY_IMPL(nngp, CUDA, m) {
     m.impl("bf_sweep_out", &bf_sweep_out);
     m.impl("bf_cross", &bf_cross);
     m.impl("row_order", &row_order);
+    m.impl("pair_plan", &pair_plan);
     m.impl("combine_partials_out", &combine_partials_out);
 }

@@ -14,7 +14,9 @@ for tracing.
     torch.ops.nngp.bf_sweep(coords, nbr, i0, kind, sigma2, phi, tau2, values, want_bf, algo, order=None, nu=-1.0)
         -> (B, F, partials)
     torch.ops.nngp.bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials,
-                                workspace, algo, nu=-1.0) -> ()       # the hot path: caller-owned buffers
+                                workspace, algo, nu=-1.0, plan=None, plan_info=None) -> ()
+                                                                      # the hot path: caller-owned buffers
+    torch.ops.nngp.pair_plan(nbr, order, i0, n_points, dim) -> (plan, plan_info)   # tile pair plan (setup)
     torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo, nu=-1.0) -> (B, F, mean)
     torch.ops.nngp.row_order(coords, i0, rows, nbr) -> (order, nbr_sorted)
     torch.ops.nngp.combine_partials_out(gathered, out) -> ()
@@ -78,8 +80,13 @@ def _register_fakes() -> None:
         return coords.new_empty((0, m)), coords.new_empty((0,)), coords.new_empty((4,))
 
     @fake("bf_sweep_out")
-    def _(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials, workspace, algo, nu=-1.0):
+    def _(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials, workspace, algo, nu=-1.0,
+          plan=None, plan_info=None):
         return None
+
+    @fake("pair_plan")
+    def _(nbr, order, i0, n_points, dim):
+        raise RuntimeError("pair_plan is a setup call (it synchronises to read its tile counts): build it eagerly")
 
     @fake("bf_cross")
     def _(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo, nu=-1.0):
@@ -111,12 +118,26 @@ def algo_code(algo: str) -> int:
 
 
 def bf_sweep_out(coords, nbr, order, i0, kind: str, theta, values, B, F, R, partials, workspace,
-                 algo: str = "auto") -> None:
+                 algo: str = "auto", plan=None) -> None:
     """The fused sweep into caller-owned buffers through ``torch.ops.nngp.bf_sweep_out``
     (stream-ordered on torch's current stream, no host synchronisation).  ``theta`` =
-    (sigma2, phi, tau2), or (sigma2, phi, tau2, nu) for the ``matern`` kind."""
+    (sigma2, phi, tau2), or (sigma2, phi, tau2, nu) for the ``matern`` kind.  ``plan``: a
+    ``(plan, plan_info)`` pair from :func:`pair_plan` for this nbr / order / i0."""
     load()
     nu = float(theta[3]) if len(theta) > 3 else -1.0
+    pbuf, pinfo = plan if plan is not None else (None, None)
     torch.ops.nngp.bf_sweep_out(coords, nbr, order, int(i0), kind_code(kind), float(theta[0]), float(theta[1]),
-                                float(theta[2]), values, B, F, R, partials, workspace, algo_code(algo), nu)
+                                float(theta[2]), values, B, F, R, partials, workspace, algo_code(algo), nu, pbuf,
+                                pinfo)
+
+
+def pair_plan(nbr, order, i0: int, n_points: int, dim: int):
+    """The tile pair plan of a sweep over ``nbr`` (``torch.ops.nngp.pair_plan``): ``(plan, plan_info)``.
+    A setup call (one host synchronisation); stale once nbr or order change."""
+    load()
+    return torch.ops.nngp.pair_plan(nbr, order, int(i0), int(n_points), int(dim))
+
+
+def pair_plan_supported(m: int, kind: str, dim: int) -> bool:
+    return _lib.pair_plan_supported(m, kind, dim)
 

@@ -17,6 +17,7 @@ the default compute is the HIP kernel through the native operator
 from __future__ import annotations
 
 import math
+import time
 from typing import Callable, Optional
 
 import torch
@@ -24,6 +25,10 @@ import torch.distributed as dist
 
 from . import _lib, ops
 from .nngp import Covariance, LOG_2PI, _raise_on_bad
+
+
+# ShardedLogLik(plan=None): sweep through a tile pair plan (pair_plan.h) whenever one serves the sweep
+PLAN_DEFAULT = True
 
 
 def shard_range(n: int, rank: int, world: int):
@@ -82,7 +87,7 @@ class ShardedLogLik:
     def __init__(self, coords: torch.Tensor, m: int, rank: int = 0, world: int = 1, group=None,
                  algo: str = "auto", build_nbr: Optional[Callable] = None, compute: Optional[Callable] = None,
                  spatial_order: bool = True, layout: str = "natural", build_perm: Optional[Callable] = None,
-                 api: str = "ops", collective: Optional[bool] = None):
+                 api: str = "ops", collective: Optional[bool] = None, plan: Optional[bool] = None):
         if layout not in ("natural", "storage"):
             raise ValueError(f"layout must be 'natural' or 'storage', got {layout!r}")
         if api not in ("ops", "ctypes"):
@@ -137,6 +142,28 @@ class ShardedLogLik:
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
             self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
             self._F = torch.empty((self.hi - self.lo,), dtype=torch.float64, device=coords.device)
+        # tile pair plan (pair_plan.h): every covariance a sweep tile shares evaluated once; built once here
+        # (one host synchronisation), used by every sweep of a kind it serves.  plan=None: when supported.
+        self._plan = self._plan_ctypes = None
+        self.plan_build_s = 0.0
+        want = plan if plan is not None else PLAN_DEFAULT
+        d = coords.shape[1]
+        if (compute is None and want and self.hi > self.lo and algo in ("auto", "pairb")
+                and _lib.pair_plan_supported(self.m, "exponential", d)):
+            t0 = time.perf_counter()
+            self._plan = ops.pair_plan(self._nbr_sweep, self.order, self.lo, self.n, d)
+            self.plan_build_s = time.perf_counter() - t0
+            self._plan_ctypes = _lib.PairPlan(self._plan[0], self._plan[1].tolist(), self._nbr_sweep, self.order)
+        elif plan:
+            raise ValueError(f"pair plans serve algo auto / pairb, 2 <= m <= 18, dim 1..3 (m={self.m}, dim={d})")
+
+    @property
+    def planned(self) -> bool:
+        """Whether sweeps of the plan-served kinds (exponential .. spherical) run through a pair plan."""
+        return self._plan is not None
+
+    def _plan_for(self, kind: str):
+        return self._plan if (self._plan is not None and _lib.KIND_CODES.get(kind, 99) <= 4) else None
 
     def to_storage(self, values: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Input-order per-location values -> storage order (layout 'storage')."""
@@ -153,14 +180,16 @@ class ShardedLogLik:
         B, F = (self._B, self._F) if want_bf else (None, None)
         p = self._partials if out is None else out
         s2, phi, tau2 = cov.theta
+        plan = self._plan_for(cov.kind)
         if self.api == "ctypes":  # the same C-ABI call without the dispatcher (A/B of the op overhead)
             _lib.bf_sweep(self._coords_sweep, self._nbr_sweep, self.lo, cov.kind, s2, phi, tau2, values=values,
                           want_bf=want_bf, algo=self.algo, B=B, F=F, partials=p, workspace=self._ws, order=self.order,
-                          nu=cov.nu_arg)
+                          nu=cov.nu_arg, plan=self._plan_ctypes if plan is not None else None)
             return p
+        pb, pi = plan if plan is not None else (None, None)
         self._sweep_op(self._coords_sweep, self._nbr_sweep, self.order, self.lo, ops.kind_code(cov.kind),
                        float(s2), float(phi), float(tau2), values, B, F, None, p, self._ws, self._algo_code,
-                       -1.0 if cov.nu_arg is None else cov.nu_arg)
+                       -1.0 if cov.nu_arg is None else cov.nu_arg, pb, pi)
         return p
 
     def partials(self, cov: Covariance, values: Optional[torch.Tensor], want_bf: bool = True,

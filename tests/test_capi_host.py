@@ -218,7 +218,7 @@ def test_blocks_entry_points_reject(lib):
     assert lib.nngp_bf_sweep_blocks(*args(m=33)) == -4
     assert "m <= 32" in lib.nngp_last_error().decode()
     assert lib.nngp_bf_sweep_blocks(*args(m=0)) == -4
-    assert lib.nngp_abi_version() == 2 and b"0.2.0" in lib.nngp_version()
+    assert lib.nngp_abi_version() == 3 and b"0.3.0" in lib.nngp_version()
     assert lib.nngp_bf_sweep_blocks(*args(cov=None)) == -1
     assert lib.nngp_joint_dist(P(256), 10, 4, P(256), 10, P(256), None, 10, 5, 0, P(256), None) == -4
     assert lib.nngp_joint_dist(P(256), 10, 2, P(256), 10, P(256), None, 11, 5, 0, P(256), None) == -1
