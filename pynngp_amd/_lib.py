@@ -576,7 +576,9 @@ def joint_diagonal(m: int) -> torch.Tensor:
 def bf_sweep_blocks(cov: torch.Tensor, nbr: torch.Tensor, n_points: int, i0: int = 0,
                     values: Optional[torch.Tensor] = None, qvalues: Optional[torch.Tensor] = None,
                     want_bf: bool = True, order: Optional[torch.Tensor] = None, R: Optional[torch.Tensor] = None,
-                    workspace: Optional[torch.Tensor] = None, n_locs: Optional[int] = None
+                    workspace: Optional[torch.Tensor] = None, n_locs: Optional[int] = None,
+                    B: Optional[torch.Tensor] = None, F: Optional[torch.Tensor] = None,
+                    partials: Optional[torch.Tensor] = None
                     ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor], torch.Tensor]:
     """The fused B/F + log-lik sweep with the joint blocks' covariances given (nngp_bf_sweep_blocks):
     ``cov`` float64 ((m+1)(m+2)/2, rows) in :func:`joint_dist`'s layout (the covariance function
@@ -606,10 +608,16 @@ def bf_sweep_blocks(cov: torch.Tensor, nbr: torch.Tensor, n_points: int, i0: int
     values = None if values is None else values.contiguous()
     qvalues = None if qvalues is None else qvalues.contiguous()
     dev = _require_gpu(cov, nbr, values, qvalues, order, R)
-    B = torch.empty((rows, m), dtype=torch.float64, device=dev) if want_bf else None
-    F = torch.empty((rows,), dtype=torch.float64, device=dev) if want_bf else None
+    if want_bf:
+        _check_out(B, "B", (rows, m), dev)
+        _check_out(F, "F", (rows,), dev)
+        B = torch.empty((rows, m), dtype=torch.float64, device=dev) if B is None else B
+        F = torch.empty((rows,), dtype=torch.float64, device=dev) if F is None else F
+    else:
+        B = F = None
     _check_out(R, "R", (rows,), dev)
-    partials = torch.empty(4, dtype=torch.float64, device=dev)
+    _check_out(partials, "partials", (4,), dev)
+    partials = torch.empty(4, dtype=torch.float64, device=dev) if partials is None else partials
     need = lib.nngp_bf_sweep_blocks_workspace_bytes(rows)
     if workspace is None or workspace.numel() < need:
         workspace = _workspace(need, dev)

@@ -195,17 +195,28 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
 
 // the separate fold of bf_pairb's tile records (pairb_fold_records, bf_pairb.h): one block of the same
 // kPairbThreads threads as the sweep's fused fold, so both give the same bits
+// The tile count comes from the workspace header the sweep wrote; a count outside [0, bound] means the
+// workspace does not hold a pair-kernel sweep of n_rows rows (e.g. a deferred Matern sweep that ran on the
+// wavefront kernel, finalised as PAIRB): the fold then reads nothing and the partials are NaN (advice r04).
 __global__ __launch_bounds__(kPairbThreads) void bf_finalize_pairb(const double4* __restrict__ rec,
                                                                    const int32_t* __restrict__ lexp,
-                                                                   const int64_t* __restrict__ hdr,
+                                                                   const int64_t* __restrict__ hdr, int64_t bound,
                                                                    double* __restrict__ partials) {
     __shared__ double sh[kPairbWaves][5];
-    pairb_fold_records(rec, lexp, hdr[0], partials, sh);
+    const int64_t n = hdr[0];
+    if (n < 0 || n > bound) {
+        if (threadIdx.x == 0) {
+            partials[0] = partials[1] = NAN;
+            partials[2] = partials[3] = -1.0;
+        }
+        return;
+    }
+    pairb_fold_records(rec, lexp, n, partials, sh);
 }
 
 hipError_t bf_finalize_pairb_launch(void* ws, int64_t n_rows, double* partials, hipStream_t s) {
     hipLaunchKernelGGL(bf_finalize_pairb, dim3(1), dim3(kPairbThreads), 0, s, (const double4*)pairb_rec(ws),
-                       pairb_lexp(ws, n_rows), (const int64_t*)pairb_hdr(ws), partials);
+                       pairb_lexp(ws, n_rows), (const int64_t*)pairb_hdr(ws), pairb_tiles_bound(n_rows), partials);
     return hipGetLastError();
 }
 

@@ -39,6 +39,9 @@ int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     if (algo != NNGP_ALGO_AUTO) return algo;
     // general-smoothness Matern: the pair kernel with the launch's table for m <= 24 (nu >= NNGP_MT_NU_MIN;
     // resolve_algo_nu decides for a given nu), the wavefront kernel (the direct Bessel evaluation) above
+    // (nngp_resolve_algo, nu unknown: the pair kernel's table covers nu >= ~0.45 only; a deferred sweep's
+    // finalize must use nngp_resolve_algo_nu's answer, and bf_finalize_pairb refuses a header that is not a
+    // pair-kernel sweep of that many rows)
     if (kind == NNGP_COV_MATERN) return m >= 1 && m <= 24 ? nngp::kAlgoPairB : nngp::kAlgoWave;
     if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
     if (m >= 25 && m <= 32) return nngp::kAlgoQuad;

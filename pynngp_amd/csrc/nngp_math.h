@@ -365,9 +365,12 @@ NNGP_HD void nngp_matern_bin_fit(const CovParams& p, int b, const double* rho_no
     coef[0] += vref;
 }
 
-// rho(phi d) from the table (tab: the launch's table, 16-B aligned), d2 = d^2 from the distance
+// rho(phi d) from the table (tab: the launch's table, 16-B aligned), d2 = d^2 from the distance.
+// t is clamped far past the last octave (rho = 0 there): a padding point's d2 ~ (m + 1)^2 1e300 times a
+// large phi^2 overflows to inf, whose frexp exponent (0 on the GPU) and mantissa (inf) would index the
+// table out of range and give NaN instead of an exact 0 (advice r04)
 NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2) {
-    const double t = d2 * P.mphi2;
+    const double t = fmin(d2 * P.mphi2, 0x1p1000);
 #ifdef NNGP_MATH_HOST
     int ex;
     const double mant = frexp(t, &ex);

@@ -8,6 +8,10 @@ exist.  This is the sampler those names describe, for the model of Datta et al.
     y = X beta + w + e,   e_i ~ N(0, tau2 v_i),   w ~ NNGP(0, sigma2 R(phi))
     beta ~ flat,  sigma2 ~ IG(a_s, b_s),  tau2 ~ IG(a_t, b_t),  phi ~ U(phi_lo, phi_hi)
 
+A covariance of the caller's own (``cov=``, the reference's plug-in ``cov(a, b)``, nngp.py:6,12) is
+held fixed: its joint blocks are evaluated once and factored by the covariance-blocks kernel; phi and
+sigma2 are then not sampled (the callable carries its own scale), w, tau2 and beta are.
+
 One iteration (``step``):
   1. phi | w, sigma2   -- Metropolis-Hastings, log-normal random walk; the proposal's
                           log density of w is one fused B/F sweep (nngp_bf_sweep at
@@ -96,11 +100,27 @@ class SeqNNGP:
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
                  seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
-                 ref=None, X_ref=None, nu: Optional[float] = None):
+                 ref=None, X_ref=None, nu: Optional[float] = None, cov=None, fix_phi: bool = False,
+                 fix_sigma2: bool = False):
         self.device = _default_device(device)
         dev = self.device
+        # a covariance of the caller's own (the reference's plug-in cov(a, b), nngp.py:6,12): the latent
+        # covariance is the callable itself, held fixed -- no phi / sigma2 updates (their proposals would
+        # re-run the caller's code on every joint block); B / F come from one covariance-blocks sweep
+        self._custom = None
+        if cov is not None:
+            from .nngp import CallableCovariance
+
+            fn = cov.fn if isinstance(cov, CallableCovariance) else cov
+            if not callable(fn):
+                raise TypeError("cov must be a callable cov(a, b) or a CallableCovariance")
+            mode = cov.mode if isinstance(cov, CallableCovariance) else None
+            # the latent field's covariance: the callable without a nugget (tau2 is the response model's)
+            self._custom = CallableCovariance(fn, 0.0, batch=mode)
+            kind, nu, fix_phi, fix_sigma2, sigma2, phi = "custom", None, True, True, 1.0, 0.0
+        self.fix_phi, self.fix_sigma2 = bool(fix_phi), bool(fix_sigma2)
         self.kind = kind
-        self._nu_arg = _lib._check_kind(kind, nu)  # the matern kind's (fixed) smoothness; -1 otherwise
+        self._nu_arg = -1.0 if self._custom is not None else _lib._check_kind(kind, nu)  # matern's nu; -1 otherwise
         self.nu = nu if kind == "matern" else None
         self.m = int(m)
         if not 1 <= self.m <= _lib.MAX_M:
@@ -292,9 +312,17 @@ class SeqNNGP:
         self._B2, self._Ft2, self._r2 = z(n, self.m), z(n), z(n)
         self._part = z(4)
         self._z = z(n)
-        self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
         ops.load()  # the sweep goes through torch.ops.nngp.bf_sweep_out (libnngp_torch_ops.so)
-        self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
+        if self._custom is not None:
+            if not 1 <= self.m <= _lib.BLOCKS_MAX_M:
+                raise ValueError(f"a callable covariance needs 1 <= m <= {_lib.BLOCKS_MAX_M} (m={self.m})")
+            # the caller's covariance on every joint block, once (the chain holds it fixed)
+            self._cblocks = self._custom.blocks(self.coords, self.nbr, 0)
+            self._ws = _lib._workspace(_lib.load().nngp_bf_sweep_blocks_workspace_bytes(n), dev)
+            self._kind_code, self._algo_code = -1, ops.algo_code(algo)
+        else:
+            self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
+            self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
         self._stats_buf = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
         self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k)
@@ -318,7 +346,12 @@ class SeqNNGP:
         return out
 
     def _sweep_into(self, phi, B, Ft, r):
-        """Factors of the unit-variance NNGP at phi, and residuals of the current w."""
+        """Factors of the unit-variance NNGP at phi, and residuals of the current w (a callable
+        covariance: the factors of the callable's own covariance, sigma2 = 1)."""
+        if self._custom is not None:
+            _lib.bf_sweep_blocks(self._cblocks, self.nbr, self.n, 0, values=self.w, qvalues=self.w, R=r, B=B, F=Ft,
+                                 partials=self._part, workspace=self._ws)
+            return
         torch.ops.nngp.bf_sweep_out(self.coords, self.nbr, None, 0, self._kind_code, 1.0, float(phi), 0.0, self.w, B,
                                     Ft, r, self._part, self._ws, self._algo_code, self._nu_arg)
 
@@ -339,6 +372,8 @@ class SeqNNGP:
     def update_phi(self):
         """phi | w, sigma2: log-normal random-walk Metropolis-Hastings; the proposal's log
         density of w is one fused B/F sweep over every node of the DAG."""
+        if self.fix_phi:
+            return
         phi_p = self.phi * math.exp(self.phi_tuning * self.rng.standard_normal())
         lo, hi = self.priors.phi_unif
         u = self.rng.random()
@@ -421,9 +456,10 @@ class SeqNNGP:
         """One iteration: phi; sigma2; update_wt; update_ws; tau2; beta; update_y_unobserved."""
         n = self.n
         self.update_phi()
-        # sigma2 | w, phi
-        a, b = self.priors.sigma2_ig
-        self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
+        # sigma2 | w, phi (held fixed on request, and with a callable covariance: its own scale)
+        if not self.fix_sigma2:
+            a, b = self.priors.sigma2_ig
+            self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
         # w | rest (colour steps, in place on w and r; the sweep's normals in one parallel pass)
         _lib.gibbs_normals(self._z, self.seed, self.iteration)
         self.update_wt()
@@ -468,6 +504,7 @@ class SeqNNGP:
     # ------------------------------------------------------------------ checkpoint / resume
     def _settings(self) -> dict:
         return {"algo": self.algo, "phi_tuning": self.phi_tuning, "fix_tau2": self.fix_tau2, "nu": self.nu,
+                "fix_phi": self.fix_phi, "fix_sigma2": self.fix_sigma2,
                 "priors": {k: list(v) for k, v in dataclasses.asdict(self.priors).items()},
                 "n_t": self.n_t, "n_obs": self.n_obs, "n_colors": int(self.n_colors)}
 
@@ -479,7 +516,7 @@ class SeqNNGP:
         import json
 
         h = hashlib.sha256()
-        for t in (self.coords, self.y, self.X, self.nbr, self.noise_w):
+        for t in (self.coords, self.y, self.X, self.nbr, self.noise_w, getattr(self, "_cblocks", None)):
             h.update(b"none" if t is None else t.contiguous().cpu().numpy().tobytes())
         h.update(json.dumps(self._settings(), sort_keys=True).encode())
         return h.hexdigest()

@@ -195,6 +195,9 @@ class ShardedSeqNNGP(SeqNNGP):
     def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
                  collective: Optional[bool] = None, graphs: Optional[bool] = None, exchange: str = "halo",
                  **kwargs):
+        if kwargs.get("cov") is not None:
+            raise NotImplementedError("ShardedSeqNNGP runs the built-in covariance kinds; a callable cov(a, b) "
+                                      "chain runs on one GPU (SeqNNGP(cov=...))")
         super().__init__(*args, **kwargs)
         inited = dist.is_available() and dist.is_initialized()
         self.rank = int(rank if rank is not None else (dist.get_rank(group) if inited else 0))

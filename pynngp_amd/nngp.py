@@ -194,7 +194,8 @@ class CallableCovariance:
     kind = "custom"
     MODES = ("torch", "numpy", "loop", "loop_torch")
 
-    def __init__(self, fn: Callable, tau2: float = 0.0, batch: Optional[str] = None, chunk_bytes: int = 1 << 28):
+    def __init__(self, fn: Callable, tau2: float = 0.0, batch: Optional[str] = None, chunk_bytes: int = 1 << 28,
+                 cache: bool = False):
         if not callable(fn):
             raise TypeError("cov must be callable as cov(a, b) on coordinate rows")
         if not tau2 >= 0:
@@ -203,6 +204,11 @@ class CallableCovariance:
             raise ValueError(f"batch must be one of {self.MODES} or None")
         self.fn, self.tau2, self.batch, self.chunk_bytes = fn, float(tau2), batch, int(chunk_bytes)
         self.mode = batch
+        # cache=True: NNGP keeps this covariance's evaluated joint blocks between sweeps (the caller promises
+        # fn is a fixed function: no state it reads changes).  Default off, as the reference, which calls cov
+        # on every evaluation (nngp.py:82,96): a mutable plug-in (an MLE loop over a closure's parameters)
+        # then always sees its current state.
+        self.cache = bool(cache)
 
     def __call__(self, a, b):
         return self.fn(a, b)
@@ -509,19 +515,28 @@ class NNGP:
         return wrapped
 
     def _field_blocks(self, cv):
-        """Joint blocks of the whole field (Z-order rows) for a :class:`CallableCovariance`: its
-        evaluation is the caller's code and the most expensive step, and it depends only on the
-        covariance and the neighbour sets, so it is kept for the next sweep (8 (m+1)(m+2)/2 bytes
-        per location of device memory); None for the other covariance forms."""
+        """Joint blocks of the whole field (Z-order rows) for a :class:`CallableCovariance` (None for the
+        other covariance forms).  Evaluating them is the caller's code and the most expensive step; with
+        ``CallableCovariance(fn, cache=True)`` they are kept for the next sweep (8 (m+1)(m+2)/2 bytes per
+        location of device memory), keyed on the object, its nugget and the neighbour sets
+        (:meth:`clear_cache` drops them); by default every sweep evaluates the plug-in again, as the
+        reference calls ``cov`` on every evaluation (advice r04: a mutable plug-in must not see stale
+        blocks)."""
         if not isinstance(cv, CallableCovariance):
             return None
         hit = getattr(self, "_blk_cache", None)
-        if hit is not None and hit[0] is cv and hit[1] is self._nbr_sorted:
-            return hit[2]
+        if cv.cache and hit is not None and hit[0] is cv and hit[1] is self._nbr_sorted and hit[2] == cv.tau2:
+            return hit[3]
         self._blk_cache = None
         blk = cv.blocks(self._s_dev, self._nbr_sorted, 0, order=self._order)
-        self._blk_cache = (cv, self._nbr_sorted, blk)
+        if cv.cache:
+            self._blk_cache = (cv, self._nbr_sorted, cv.tau2, blk)
         return blk
+
+    def clear_cache(self):
+        """Drop kept covariance blocks and factors (a cached plug-in's parameters changed)."""
+        self._blk_cache = None
+        self._B = self._F = None
 
     def _nbr_idx(self, i):
         row = self.nbr[i]
@@ -687,7 +702,10 @@ class NNGP:
         location, makes the noise heteroscedastic: variance tau2 eps_i^2 (see SeqNNGP;
         ``fix_tau2=True`` with tau2 = 1 for exactly eps_i^2).  Afterwards ``ws`` / ``wt``
         hold the current w at S / T and ``y_unobserved`` the current predictive draws.
-        Returns the sampler (its ``beta, sigma2, tau2, phi`` are the other draws)."""
+        Returns the sampler (its ``beta, sigma2, tau2, phi`` are the other draws).  With the
+        reference's plug-in ``cov(a, b)`` (a callable) the covariance is held fixed: its blocks are
+        evaluated once, and w, tau2 and beta are sampled (no phi / sigma2: the callable has no such
+        parameters; its nugget ``CallableCovariance(fn, tau2)`` starts tau2)."""
         y = np.asarray(self.y, dtype=np.float64)
         if y.ndim != 1:
             raise ValueError("oneSample needs one response per location (1-D y)")
@@ -695,18 +713,25 @@ class NNGP:
             from .gibbs import SeqNNGP
 
             cv = self._covariance()
-            if not isinstance(cv, Covariance):
-                raise TypeError("the Gibbs sampler (SeqNNGP) needs a built-in covariance kind, "
-                                "pynngp_amd.Covariance(kind, sigma2, phi, tau2[, nu]): its phi update re-evaluates the "
-                                f"fused kernel at proposed phi values (got {type(cv).__name__})")
-            tau2 = cv.tau2 if cv.tau2 > 0 else 0.1 * cv.sigma2
+            if isinstance(cv, IsotropicCovariance):
+                raise TypeError("the Gibbs sampler takes a built-in covariance kind (pynngp_amd.Covariance) or the "
+                                "reference's plug-in cov(a, b) (a callable / CallableCovariance), not an "
+                                "IsotropicCovariance: write it as cov(a, b)")
             if "eps" not in sampler_kw and self.eps is not None:
                 ev = np.asarray(self.eps, dtype=np.float64)
                 if ev.shape == y.shape and np.all(np.isfinite(ev)) and np.all(ev > 0):
                     sampler_kw["eps"] = ev
             ref = None if self._same_sets() else self.s
-            smp = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi, seed=seed,
-                          device=self.device, ref=ref, nu=cv.nu_arg, **sampler_kw)
+            if isinstance(cv, CallableCovariance):
+                # the plug-in held fixed: w, tau2, beta sampled; no phi / sigma2 (the callable carries its own
+                # scale); the nugget, when given, starts tau2
+                tau2 = cv.tau2 if cv.tau2 > 0 else 0.1
+                smp = SeqNNGP(self.t, y, X=X, m=self.m, cov=cv, tau2=tau2, seed=seed, device=self.device, ref=ref,
+                              **sampler_kw)
+            else:
+                tau2 = cv.tau2 if cv.tau2 > 0 else 0.1 * cv.sigma2
+                smp = SeqNNGP(self.t, y, X=X, m=self.m, kind=cv.kind, sigma2=cv.sigma2, tau2=tau2, phi=cv.phi,
+                              seed=seed, device=self.device, ref=ref, nu=cv.nu_arg, **sampler_kw)
             ws = np.asarray(self.ws, dtype=np.float64)
             smp.set_w(ws=np.where(np.isfinite(ws), ws, 0.0),
                       wt=None if ref is None else np.where(np.isfinite(self.wt), self.wt, 0.0))

@@ -92,8 +92,8 @@ def test_callable_cov_and_errors(dev):
     np.testing.assert_allclose(model._Bsi(10), Bo[10], rtol=0, atol=1e-10)
     assert abs(model._Fsi(10) - Fo[10]) <= 1e-10 * Fo[10]
     assert abs(model.loglik() - O.loglik_from_partials(po, 100)) <= 1e-12 * abs(O.loglik_from_partials(po, 100))
-    with pytest.raises(TypeError, match="built-in covariance"):  # the sampler needs a fused kind
-        model.oneSample()
+    smp = model.oneSample(seed=1)  # the sampler with the plug-in held fixed (w, tau2, beta; round 5)
+    assert smp.kind == "custom" and np.all(np.isfinite(model.ws))
     with pytest.raises(TypeError, match="needs a covariance"):
         NNGP(t, y, None, "S=T", 4, None).loglik()
     with pytest.raises(ValueError):

@@ -156,11 +156,45 @@ def test_nngp_class_with_reference_style_callable(dev):
     ll = model.loglik()
     want = O.loglik_from_partials(po, n)
     assert abs(ll - want) <= 1e-12 * abs(want)
-    assert model._blk_cache is not None  # the plug-in's blocks are kept for the next sweep
+    assert model._blk_cache is None  # a plain callable is evaluated on every sweep (the reference's semantics)
     assert model.loglik() == ll
     y2 = rng.standard_normal(n)
     _, _, p2 = O.bf_sweep_callable(t, nbr, user_cov, y2)
     assert abs(model.loglik(y2) - O.loglik_from_partials(p2, n)) <= 1e-12 * abs(model.loglik(y2))
+
+
+def test_callable_cache_opt_in_and_mutable_plugin(dev):
+    """advice r04: a plug-in whose state changes between sweeps (a closure over a parameter an MLE loop
+    moves) must see its current state -- the default re-evaluates; CallableCovariance(fn, cache=True) keeps
+    the blocks (keyed on the nugget too) until clear_cache()."""
+    from pynngp_amd import NNGP, CallableCovariance
+
+    rng = np.random.default_rng(41)
+    n, m = 1000, 10
+    t = rng.uniform(size=(n, 2))
+    y = rng.standard_normal(n)
+    state = {"s2": 1.0}
+
+    def cov(a, b):
+        return state["s2"] * _aniso(1.0, A1, 0.1)(a, b)
+
+    model = NNGP(t, y, None, "S=T", m, cov)
+    ll1 = model.loglik()
+    state["s2"] = 2.0
+    ll2 = model.loglik()
+    _, _, p2 = O.bf_sweep_callable(t, model.nbr.cpu().numpy(), cov, y)
+    assert ll2 != ll1 and abs(ll2 - O.loglik_from_partials(p2, n)) <= 1e-12 * abs(ll2)
+    cc = CallableCovariance(cov, cache=True)
+    model2 = NNGP(t, y, None, "S=T", m, cc)
+    ll_a = model2.loglik()
+    assert model2._blk_cache is not None
+    state["s2"] = 1.0
+    assert model2.loglik() == ll_a  # kept: the caller promised a fixed function
+    cc.tau2 = 0.05  # the nugget is part of the key
+    assert model2.loglik() != ll_a
+    model2.clear_cache()
+    cc.tau2 = 0.0
+    assert model2.loglik() == ll1
 
 
 def test_predict_with_callable(dev):
@@ -180,8 +214,76 @@ def test_predict_with_callable(dev):
     Bo, Fo, _ = O.bf_sweep_callable(t, nq, user_cov, y, qcoords=q, qvalues=np.zeros(300))
     np.testing.assert_allclose(var, Fo, rtol=1e-10)
     np.testing.assert_allclose(mean, (Bo * y[nq]).sum(1), rtol=0, atol=1e-9)
-    with pytest.raises(TypeError, match="built-in covariance"):
-        model.oneSample()
+    # the sampler with the plug-in held fixed (round 5; it raised TypeError before): a chain runs, w /
+    # tau2 / beta move, sigma2 and phi stay
+    smp = model.oneSample(seed=3)
+    for _ in range(20):
+        smp = model.oneSample()
+    assert smp.kind == "custom" and smp.sigma2 == 1.0 and smp.iteration == 21
+    assert np.all(np.isfinite(model.ws)) and np.isfinite(smp.tau2) and np.all(np.isfinite(smp.beta))
+
+
+def test_callable_w_sweep_matches_dense_oracle(dev):
+    """The chain's colour sweep with the anisotropic plug-in (B / F from its blocks) equals the dense
+    full-conditional sweep of the precision (I - B)^T F^-1 (I - B) + H / tau2 (given normals) -- the check
+    tests/test_gpu_gibbs.py::test_w_sweep_matches_dense_oracle makes for the built-in kinds."""
+    from oracle import nngp_gibbs_oracle as G
+    from pynngp_amd import CallableCovariance, _lib
+
+    rng = np.random.default_rng(5)
+    n, m, tau2 = 2000, 10, 0.2
+    x = rng.uniform(size=(n, 2))
+    c = torch.from_numpy(x).to(dev)
+    nbr = _lib.knn_prior(c, m)
+    w = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    cc = CallableCovariance(_aniso(1.3, A1))
+    blk = cc.blocks(c, nbr, 0)
+    R = torch.empty(n, dtype=torch.float64, device=dev)
+    B, F, p = _lib.bf_sweep_blocks(blk, nbr, n, 0, values=w, qvalues=w, R=R)
+    Bo, Fo, _ = O.bf_sweep_callable(x, nbr.cpu().numpy(), _aniso(1.3, A1), w.cpu().numpy())
+    np.testing.assert_allclose(F.cpu().numpy(), Fo, rtol=1e-10)
+    off, rev_j, rev_k = _lib.reverse_neighbors(nbr)
+    colors, nc = _lib.color_moral_graph(nbr.cpu().numpy(), off.cpu().numpy(), rev_j.cpu().numpy())
+    members = torch.from_numpy(np.argsort(colors, kind="stable").astype(np.int32)).to(dev)
+    color_off = np.concatenate([[0], np.cumsum(np.bincount(colors, minlength=nc))]).astype(np.int32)
+    yres = torch.from_numpy(rng.standard_normal(n) * 1.5).to(dev)
+    z = torch.from_numpy(rng.standard_normal(n)).to(dev)
+    nb_h, B_h, F_h = nbr.cpu().numpy(), B.cpu().numpy(), F.cpu().numpy()
+    P = G.precision(nb_h, B_h, F_h) + np.eye(n) / tau2
+    w_ref = G.color_sweep(P, yres.cpu().numpy() / tau2, w.cpu().numpy().copy(), colors, z.cpu().numpy())
+    prep = _lib.gibbs_prepare(B, F, off, rev_j, rev_k)
+    wg, rg = w.clone(), R.clone()
+    _lib.gibbs_w_sweep(members, color_off, prep, m, 1.0, tau2, yres, wg, rg, off, rev_j, 123, 0, z=z)
+    np.testing.assert_allclose(wg.cpu().numpy(), w_ref, rtol=1e-9, atol=1e-9 * np.abs(w_ref).max())
+
+
+def test_callable_chain_equals_builtin_with_phi_fixed(dev):
+    """An isotropic exponential written as the reference's plug-in runs the same chain as the built-in
+    exponential kind with phi and sigma2 held fixed (the same model; B / F differ only by the plug-in's
+    torch exp against the kernel's table exp, ~1 ulp, so the chains agree to ~1e-9, not bit for bit)."""
+    from pynngp_amd import SeqNNGP
+
+    rng = np.random.default_rng(17)
+    n, m, phi = 3000, 10, 12.0
+    x = rng.uniform(size=(n, 2))
+    y = np.sin(6 * x[:, 0]) + 0.3 * rng.standard_normal(n)
+
+    def cov(a, b):
+        lib = torch if isinstance(a, torch.Tensor) else np
+        t = a[..., :, None, :] - b[..., None, :, :]
+        return lib.exp(-phi * lib.sqrt((t ** 2).sum(-1)))
+
+    kw = dict(m=m, tau2=0.1, seed=9, device=dev)
+    ch_c = SeqNNGP(x, y, cov=cov, **kw)
+    ch_b = SeqNNGP(x, y, kind="exponential", sigma2=1.0, phi=phi, fix_phi=True, fix_sigma2=True, **kw)
+    for _ in range(25):
+        ch_c.step()
+        ch_b.step()
+    assert ch_c.phi == 0.0 and ch_b.phi == phi and ch_c.sigma2 == ch_b.sigma2 == 1.0
+    np.testing.assert_allclose(ch_c.tau2, ch_b.tau2, rtol=1e-8)
+    np.testing.assert_allclose(ch_c.beta, ch_b.beta, rtol=1e-8, atol=1e-10)
+    wc, wb = ch_c.w_t.cpu().numpy(), ch_b.w_t.cpu().numpy()
+    np.testing.assert_allclose(wc, wb, rtol=0, atol=1e-8 * np.abs(wb).max())
 
 
 def test_isotropic_and_callable_agree_at_m28(dev):

@@ -71,6 +71,33 @@ def test_matern_sweep_vs_oracle(lib, dev, c_oracle, nu, theta, m, dim, algo):
     _check(dev, lib, c_oracle, coords, nbr, theta, nu, y, algo)
 
 
+@pytest.mark.parametrize("m,phi,nu", [(15, 2000.0, 1.3), (24, 2000.0, 2.5), (15, 900.0, 0.6), (24, 5000.0, 10.0)])
+def test_matern_large_phi_padding_rows(lib, dev, c_oracle, m, phi, nu):
+    """advice r04: a padding point at (a + 1) 1e150 gives d2 ~ (m + 1)^2 1e300, and d2 phi^2 overflowed to
+    inf once phi > ~1.3e4 / (m + 1): the table lookup then read out of range and padded rows (the first m
+    rows) got NaN.  The argument is clamped past the table: exact zeros, finite B / F, oracle parity."""
+    coords, y = _field(1500, 31 + m)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    assert lib.resolve_algo("auto", m, "matern", 2, nu=nu) == "pairb"
+    _check(dev, lib, c_oracle, coords, nbr, (1.0, phi, 0.1), nu, y)
+
+
+def test_matern_deferred_finalize_wrong_algo(lib, dev, c_oracle):
+    """advice r04: a deferred sweep with nu below the table (the wavefront kernel ran) finalised as the pair
+    kernel's records: the fold refuses the foreign header (NaN partials), never reads past the workspace;
+    with nngp_resolve_algo_nu's answer it is the in-line fold's result"""
+    coords, y = _field(3000, 77)
+    nbr = torch.from_numpy(c_oracle.c_knn_prior(coords, 15)).to(dev)
+    c, v = torch.from_numpy(coords).to(dev), torch.from_numpy(y).to(dev)
+    ws = lib.bf_workspace(3000, 15, "auto", dev, kind="matern")
+    lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3, workspace=ws, defer=True)
+    bad = lib.bf_finalize(ws, 3000, 15, "matern", 2, algo="pairb").cpu().numpy()
+    assert np.isnan(bad[0]) and np.isnan(bad[1])
+    good = lib.bf_finalize(ws, 3000, 15, "matern", 2, algo=lib.resolve_algo("auto", 15, "matern", 2, nu=0.3))
+    _, _, ref = lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3)
+    assert torch.equal(good, ref)
+
+
 def test_matern_kernel_choice_and_explicit(lib, dev):
     """auto: the pair kernel with the table for m <= 24 and nu >= ~0.45, the wavefront kernel for smaller
     nu and m > 24; the two kernels agree within the parity tolerances; lane / an uncovered nu on the pair

@@ -124,9 +124,12 @@ def test_table_rho_limits_and_range(table_rho):
     """Coincident points give exactly 1, far points exactly 0 (exact decoupling of padding); nu below the
     table's range (its octaves from 1 - rho < 1e-18 to rho < 1e-18 exceed 160) reports no table (the
     sweep then runs the wavefront kernel); rho decreases along a fine grid."""
-    got, noct = table_rho([(1.3, 0.0), (1.3, 1e-200), (1.3, 1e6), (0.7, 0.0), (0.7, 5e3), (0.3, 1.0), (0.05, 1.0)])
+    got, noct = table_rho([(1.3, 0.0), (1.3, 1e-200), (1.3, 1e6), (0.7, 0.0), (0.7, 5e3), (0.3, 1.0), (0.05, 1.0),
+                           (1.3, 1e160), (0.7, 1e300), (49.0, 1e200)])
     assert got[0] == 1.0 and got[1] == 1.0 and got[2] == 0.0 and got[3] == 1.0 and got[4] == 0.0
     assert np.isnan(got[5]) and np.isnan(got[6]) and noct[5] == 0
+    # u^2 past the double range (a padding point at (m + 1) 1e150 with a large phi): exactly 0, not NaN
+    assert got[7] == 0.0 and got[8] == 0.0 and got[9] == 0.0
     us = np.linspace(0.001, 30.0, 400).tolist()
     r, _ = table_rho([(2.2, u) for u in us])
     assert all(a > b for a, b in zip(r, r[1:]))
