@@ -4,7 +4,7 @@ import pytest
 import torch
 
 OPS = ["knn_prior", "knn_prior_rows", "knn_query", "bf_sweep", "bf_sweep_out", "bf_cross", "row_order",
-       "combine_partials_out"]
+       "combine_partials_out", "pair_plan"]
 
 
 def test_op_library_registers_all_ops():
@@ -14,7 +14,7 @@ def test_op_library_registers_all_ops():
     for name in OPS:
         assert hasattr(torch.ops.nngp, name), name
     schema = str(torch.ops.nngp.bf_sweep_out.default._schema)
-    assert "Tensor(a!)? B" in schema and "Tensor(d!) partials" in schema
+    assert "Tensor(a!)? B" in schema and "Tensor(d!) partials" in schema and "Tensor? plan=None" in schema
     assert ops.kind_code("gaussian") == 3 and ops.algo_code("pairb") >= 0
     with pytest.raises(ValueError):
         ops.kind_code("cauchy")
@@ -29,6 +29,23 @@ def test_ops_refuse_cpu_tensors():
         torch.ops.nngp.knn_prior(c, 4, 0, 50)
     with pytest.raises(NotImplementedError):
         torch.ops.nngp.bf_sweep(c, torch.zeros((50, 4), dtype=torch.int32), 0, 0, 1.0, 5.0, 0.0, None, False, 0)
+    with pytest.raises(NotImplementedError):
+        torch.ops.nngp.pair_plan(torch.zeros((50, 4), dtype=torch.int32), None, 0, 50, 2)
+
+
+def test_config1_needs_the_gpu():
+    """BASELINE config 1 (N = 10^3, the reference's CPU-sized case) runs on the GPU like every
+    other config -- the product has no CPU path (a CPU result would come from code the GPU tests do not
+    exercise); without a GPU the drop-in class raises instead of computing."""
+    import numpy as np
+
+    from pynngp_amd import NNGP, _lib
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    t = np.random.default_rng(0).uniform(size=(1000, 2))
+    with pytest.raises(_lib.NNGPExtensionError, match="needs a ROCm GPU"):
+        NNGP(t, np.zeros(1000), None, "S=T", 10, None)
 
 
 def test_fake_kernels_trace_shapes():
