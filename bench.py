@@ -232,7 +232,7 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     ("replicas only": the w sweep's per-colour halo exchange would cost more than the sweep at this
     N); a step = one full iteration (phi MH with its fused B/F sweep, sigma2, the
     colour-ordered w sweep, tau2, beta)."""
-    from pynngp_amd import Priors, SeqNNGP, ShardedSeqNNGP
+    from pynngp_amd import Priors, SeqNNGP, SeqNNGPChains, ShardedSeqNNGP
 
     single = args.single_chain
     n = args.n * world if single else args.n  # single chain: n locations per GPU, one field over all
@@ -245,21 +245,30 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     # stream driven by its own host thread -- one chain leaves the GPU idle in its colour steps' launch
     # floors and its host synchronisations (tools/bench_gibbs_streams.py)
     cpg = 1 if single else max(1, args.chains_per_gpu)
-    streams = [torch.cuda.current_stream(dev)] if cpg == 1 else [torch.cuda.Stream(dev) for _ in range(cpg)]
+    batched = cpg > 1 and args.chain_mode == "batched"
+    streams = ([torch.cuda.current_stream(dev)] if cpg == 1 or batched
+               else [torch.cuda.Stream(dev) for _ in range(cpg)])
     chains = []
-    for k in range(cpg):
-        with torch.cuda.stream(streams[k]):
-            if single:
-                chains.append(ShardedSeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi,
-                                             phi_tuning=0.01, seed=1, device=dev, collective=distributed))
-            else:
-                chains.append(SeqNNGP(coords, y, X, m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi,
-                                      phi_tuning=0.01, seed=1 + rank * cpg + k, device=dev))
+    kw = dict(m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01, device=dev)
+    if single:
+        chains.append(ShardedSeqNNGP(coords, y, X, seed=1, collective=distributed, **kw))
+    elif batched:
+        # C chains advanced together: one launch per colour for all, two host synchronisations per iteration
+        multi = SeqNNGPChains(coords, y, X, seeds=[1 + rank * cpg + k for k in range(cpg)], **kw)
+        chains = list(multi.chains)
+    else:
+        for k in range(cpg):
+            with torch.cuda.stream(streams[k]):
+                chains.append(SeqNNGP(coords, y, X, seed=1 + rank * cpg + k, **kw))
     g = chains[0]
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
 
     def run_chains(iters):
+        if batched:
+            for _ in range(iters):
+                multi.step()
+            return
         if cpg == 1:
             for _ in range(iters):
                 g.step()
@@ -355,7 +364,9 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                 "parallelism": (f"one chain over {world} GPU(s): storage-row shards, one halo all-gather (the "
                                 "boundary members) per colour"
                                 if single else f"replicas x{world * cpg} ({cpg} independent chain(s) per GPU"
-                                + ("" if cpg == 1 else ", each on its own stream") + ")"),
+                                + ("" if cpg == 1 else (", advanced together: one launch per colour for all"
+                                                        if batched else ", each on its own stream")) + ")"),
+                "chain_mode": "batched" if batched else ("streams" if cpg > 1 else "single"),
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
@@ -425,6 +436,9 @@ def main():
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
     ap.add_argument("--chains-per-gpu", type=int, default=1,
                     help="config 5 replica mode: independent chains per GPU, one stream and host thread each")
+    ap.add_argument("--chain-mode", default="batched", choices=["batched", "streams"],
+                    help="--chains-per-gpu C > 1: advance the C chains together (SeqNNGPChains: one launch per colour "
+                         "for all) or each on its own stream and host thread")
     ap.add_argument("--single-chain", action="store_true",
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")

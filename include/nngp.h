@@ -324,6 +324,11 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  * nngp_gibbs_normals: z[i] = the Philox4x32-10 normal the sweep would draw for
  *   (seed, location i, sweep), for all n locations in one parallel pass; passing it
  *   as nngp_gibbs_w_sweep's z gives the bit-identical chain with shorter colour steps.
+ * nngp_gibbs_w_sweep_chains: nngp_gibbs_w_sweep for `chains` (1..8) independent chains of the same
+ *   field -- the same member_rows / colours / rev_j / noise_w, each chain c its own prep[c] (its
+ *   phi's factors), sigma2[c], tau2[c] (host arrays), yres[c], w[c], r[c] and given normals z[c]
+ *   (host arrays of device pointers) -- in ONE launch per colour; chain c's result is bit-identical
+ *   to nngp_gibbs_w_sweep on its own arguments (with z given).
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,
  *   out[2 + c] = sum_i h_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p));
  *   h_i = noise_w[i], or 1 when noise_w is NULL.
@@ -363,6 +368,10 @@ int nngp_gibbs_w_sweep(const int32_t *member_rows, const int32_t *color_off_host
                        int64_t n, int32_t m, double sigma2, double tau2, const double *yres, const double *noise_w,
                        double *w, double *r, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
                        void *stream);
+int nngp_gibbs_w_sweep_chains(const int32_t *member_rows, const int32_t *color_off_host, int32_t n_colors,
+                              int32_t chains, const void *const *prep, int64_t n, int32_t m, const double *sigma2,
+                              const double *tau2, const double *const *yres, const double *noise_w, double *const *w,
+                              double *const *r, const int32_t *rev_j, const double *const *z, void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
 int nngp_gibbs_prepare_range(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
                              const int32_t *rev_k, int64_t n, int32_t m, int64_t row0, int64_t row1, void *prep,

@@ -8,7 +8,7 @@ it -- the first call that needs it does, and fails loudly if it is missing.
 from ._lib import NNGPExtensionError, LIB_PATH, version  # noqa: F401
 from .nngp import NNGP, CallableCovariance, Covariance, IsotropicCovariance, NNGPNumericalError  # noqa: F401
 from .sweep import ShardedLogLik, shard_range, combine_partials  # noqa: F401
-from .gibbs import SeqNNGP, Priors  # noqa: F401
+from .gibbs import SeqNNGP, SeqNNGPChains, Priors  # noqa: F401
 from .gibbs_sharded import ShardedSeqNNGP  # noqa: F401
 
 __version__ = "0.3.0"

@@ -55,6 +55,7 @@ SYMBOLS = (
     "nngp_gibbs_w_apply",
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
+    "nngp_gibbs_w_sweep_chains",
     "nngp_pair_plan_supported",
     "nngp_pair_plan_bytes",
     "nngp_pair_plan_build",
@@ -164,6 +165,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
+    lib.nngp_gibbs_w_sweep_chains.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
+    lib.nngp_gibbs_w_sweep_chains.restype = ctypes.c_int
     lib.nngp_pair_plan_supported.argtypes = [I32, I32, I32]
     lib.nngp_pair_plan_supported.restype = ctypes.c_int
     lib.nngp_pair_plan_bytes.argtypes = [I64, I32, I32]
@@ -819,6 +822,36 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
                                      _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
+
+
+def gibbs_w_sweep_chains(member_rows: torch.Tensor, color_off_host, preps, m: int, sigma2s, tau2s, yres, w, r,
+                         rev_j: torch.Tensor, z, noise_w: Optional[torch.Tensor] = None) -> None:
+    """:func:`gibbs_w_sweep` for up to 8 independent chains of one field in ONE launch per colour
+    (nngp_gibbs_w_sweep_chains): ``member_rows`` / colours / ``rev_j`` / ``noise_w`` shared, per chain
+    lists of ``preps``, ``sigma2s``, ``tau2s``, ``yres``, ``w``, ``r`` and given normals ``z``.  Chain c's
+    result is bit-identical to :func:`gibbs_w_sweep` on its own arguments with its ``z``."""
+    import numpy as np
+
+    C = len(preps)
+    if not 1 <= C <= 8 or not all(len(v) == C for v in (sigma2s, tau2s, yres, w, r, z)):
+        raise ValueError("1..8 chains, one entry per chain in every list")
+    n = w[0].shape[0]
+    for t in list(yres) + list(w) + list(r) + list(z):
+        if t.dtype != torch.float64 or tuple(t.shape) != (n,) or not t.is_contiguous():
+            raise ValueError(f"per-chain vectors must be contiguous float64 ({n},)")
+    if member_rows.dtype != torch.int32 or member_rows.dim() != 2 or member_rows.shape[1] != 4 \
+            or not member_rows.is_contiguous():
+        raise ValueError("member_rows must be a contiguous int32 (n, 4) tensor from gibbs_member_rows")
+    dev = _require_gpu(member_rows, rev_j, noise_w, *preps, *yres, *w, *r, *z)
+    _check_noise_w(noise_w, n)
+    co = np.ascontiguousarray(color_off_host, dtype=np.int32)
+    P = ctypes.c_void_p * C
+    D = ctypes.c_double * C
+    _check(load().nngp_gibbs_w_sweep_chains(_ptr(member_rows), co.ctypes.data, len(co) - 1, C,
+                                            P(*[_ptr(t) for t in preps]), n, int(m), D(*map(float, sigma2s)),
+                                            D(*map(float, tau2s)), P(*[_ptr(t) for t in yres]), _ptr(noise_w),
+                                            P(*[_ptr(t) for t in w]), P(*[_ptr(t) for t in r]), _ptr(rev_j),
+                                            P(*[_ptr(t) for t in z]), _stream(dev)), "nngp_gibbs_w_sweep_chains")
 
 
 def gibbs_normals(z: torch.Tensor, seed: int, sweep: int) -> torch.Tensor:

@@ -581,6 +581,151 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- several chains, one launch per colour
+// C independent chains of the same field (the same DAG, colouring and member rows; each chain its own
+// B / F -- its own phi --, w, r, y - X beta, sigma2, tau2 and normals) advanced by ONE launch per colour
+// (nngp_gibbs_w_sweep_chains): a colour step's fixed cost (the launch and its dependent member-row /
+// reverse-entry round trips, ~5 us of the ~16 us per colour at N = 1e6) is paid once for all chains, the
+// member rows and child indices are read once, and each thread has C independent gathers in flight.
+// Per chain the arithmetic is gibbs_w_color's, operation for operation, so chain c's draws are
+// bit-identical to running it alone.
+constexpr int kMaxChains = 8;
+struct ChainPtrs {
+    const double* Brev[kMaxChains];
+    const double* Grev[kMaxChains];
+    const double* P[kMaxChains];
+    const double* invF[kMaxChains];
+    const double* yres[kMaxChains];
+    const double* z[kMaxChains];
+    double* w[kMaxChains];
+    double* r[kMaxChains];
+    double it2[kMaxChains], is2[kMaxChains];
+};
+
+template <int C>
+__global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restrict__ member_rows, int64_t n_members,
+                                                            const ChainPtrs cp, const double* __restrict__ noise_w,
+                                                            const int32_t* __restrict__ rev_j, int64_t m_cap) {
+    const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const int64_t g = t / kGroup;
+    const int l = (int)(t % kGroup);
+    const bool live = g < n_members;
+    const int4 mr = member_rows[live ? g : n_members - 1];
+    const int64_t i = mr.x;
+    const int32_t e0 = mr.y, e1 = live ? mr.z : mr.y;
+    const double hi = noise_w != nullptr ? noise_w[i] : 1.0;
+    double wi[C], ri[C], iF[C], Pi[C], yi[C], zl[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        wi[c] = cp.w[c][i];
+        ri[c] = cp.r[c][i];
+        iF[c] = cp.invF[c][i];
+        Pi[c] = cp.P[c][i];
+        yi[c] = cp.yres[c][i];
+        zl[c] = cp.z[c][i];
+    }
+    int64_t jf[kPer];
+    bool has[kPer];
+    double bf[C][kPer], gf[C][kPer], rf[C][kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int32_t ef = e0 + l + k * kGroup;
+        has[k] = ef < e1;
+        const int64_t es = has[k] ? ef : 0;
+        jf[k] = i;
+        int32_t jr = 0;
+        if (m_cap > 0) jr = rev_j[es];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            bf[c][k] = 0.0;
+            gf[c][k] = 0.0;
+            if (m_cap > 0) {
+                bf[c][k] = cp.Brev[c][es];
+                gf[c][k] = cp.Grev[c][es];
+            }
+        }
+        if (m_cap > 0) jf[k] = has[k] ? (int64_t)jr : i;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+#pragma unroll
+        for (int c = 0; c < C; ++c) rf[c][k] = cp.r[c][jf[k]];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            rf[c][k] = has[k] ? rf[c][k] : 0.0;
+            bf[c][k] = has[k] ? bf[c][k] : 0.0;
+            acc = k == 0 ? (has[0] ? gf[c][0] * rf[c][0] : 0.0) : (has[k] ? fma(gf[c][k], rf[c][k], acc) : acc);
+        }
+        for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(cp.Grev[c][e], cp.r[c][rev_j[e]], acc);
+#if NNGP_GIBBS_DPP
+        acc = group_sum<kGroup>(acc);
+#else
+#pragma unroll
+        for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+#endif
+        const double it2 = cp.it2[c], is2 = cp.is2[c];
+        const double it2i = noise_w != nullptr ? it2 * hi : it2;
+        const double prec = fma(iF[c] + Pi[c], is2, it2i);
+        const double lin = fma(yi[c], it2i, is2 * fma(wi[c] - ri[c], iF[c], fma(wi[c], Pi[c], acc)));
+        const double sd = nngp_rsqrt(prec);
+        const double wn = fma(zl[c], sd, lin / prec);
+        const double dw = wn - wi[c];
+        if (live && l == 0) {
+            cp.w[c][i] = wn;
+            cp.r[c][i] = ri[c] + dw;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+            if (has[k]) cp.r[c][jf[k]] = fma(-bf[c][k], dw, rf[c][k]);
+        for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) {
+            const int64_t j = rev_j[e];
+            cp.r[c][j] = fma(-cp.Brev[c][e], dw, cp.r[c][j]);
+        }
+    }
+}
+
+hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
+                                       int chains, const void* const* preps, int64_t n, int m, const double* sigma2,
+                                       const double* tau2, const double* const* yres, const double* noise_w,
+                                       double* const* w, double* const* r, const int32_t* rev_j,
+                                       const double* const* z, hipStream_t s) {
+    if (chains < 1 || chains > kMaxChains) return hipErrorInvalidValue;
+    ChainPtrs cp{};
+    for (int c = 0; c < chains; ++c) {
+        const GibbsPrep g = prep_layout((void*)preps[c], n, m);
+        cp.Brev[c] = g.Brev;
+        cp.Grev[c] = g.Grev;
+        cp.P[c] = g.P;
+        cp.invF[c] = g.invF;
+        cp.yres[c] = yres[c];
+        cp.z[c] = z[c];
+        cp.w[c] = w[c];
+        cp.r[c] = r[c];
+        cp.it2[c] = 1.0 / tau2[c];
+        cp.is2[c] = 1.0 / sigma2[c];
+    }
+    for (int k = 0; k < n_colors; ++k) {
+        const int64_t a = color_off_host[k], b = color_off_host[k + 1];
+        if (b <= a) continue;
+        const dim3 grid((unsigned)(((b - a) * kGroup + 255) / 256));
+        const int4* mr = (const int4*)member_rows + a;
+        const int64_t mc = n * (int64_t)m;
+        switch (chains) {
+#define NNGP_CHAINS_CASE(CC)                                                                                    \
+    case CC:                                                                                                   \
+        hipLaunchKernelGGL(gibbs_w_color_chains<CC>, grid, dim3(256), 0, s, mr, b - a, cp, noise_w, rev_j, mc); \
+        break;
+            NNGP_CHAINS_CASE(1) NNGP_CHAINS_CASE(2) NNGP_CHAINS_CASE(3) NNGP_CHAINS_CASE(4)
+            NNGP_CHAINS_CASE(5) NNGP_CHAINS_CASE(6) NNGP_CHAINS_CASE(7) NNGP_CHAINS_CASE(8)
+#undef NNGP_CHAINS_CASE
+        }
+    }
+    return hipGetLastError();
+}
+
 // Sharded chain (nngp_gibbs_w_apply): after a colour's exchange, each rank replays the updates of the
 // other ranks' members it keeps a replica of.  Row (i, e0, e1, src): w_new = wsrc[src] (the owner's
 // draw), dw = w_new - w_i computed from this rank's replica of w_i -- the owner's operands, so the

@@ -97,6 +97,8 @@ class SeqNNGP:
     nngp.py:45-47: the uniform 5-NN mean of the observed responses at every node).
     """
 
+    _use_plan = True  # the whole-field phi sweeps through a tile pair plan (the sharded chain sweeps shards)
+
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
                  seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
@@ -323,6 +325,12 @@ class SeqNNGP:
         else:
             self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
             self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
+        # tile pair plan for the phi-proposal sweeps (pair_plan.h; the same B / F / r bits, each shared
+        # covariance of a tile evaluated once): built once, the DAG never changes
+        self._plan = (None, None)
+        if (self._use_plan and self._custom is None and algo in ("auto", "pairb")
+                and _lib.pair_plan_supported(self.m, kind, self.coords.shape[1])):
+            self._plan = ops.pair_plan(self.nbr, None, 0, n, self.coords.shape[1])
         self._stats_buf = z(2 + self.p)
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
         self._prep = _lib.gibbs_prepare(self.B, self.Ft, self.off, self.rev_j, self.rev_k)
@@ -353,7 +361,7 @@ class SeqNNGP:
                                  partials=self._part, workspace=self._ws)
             return
         torch.ops.nngp.bf_sweep_out(self.coords, self.nbr, None, 0, self._kind_code, 1.0, float(phi), 0.0, self.w, B,
-                                    Ft, r, self._part, self._ws, self._algo_code, self._nu_arg)
+                                    Ft, r, self._part, self._ws, self._algo_code, self._nu_arg, *self._plan)
 
     @staticmethod
     def _check(p):
@@ -372,14 +380,25 @@ class SeqNNGP:
     def update_phi(self):
         """phi | w, sigma2: log-normal random-walk Metropolis-Hastings; the proposal's log
         density of w is one fused B/F sweep over every node of the DAG."""
+        prop = self._phi_draw()
+        if prop is not None:
+            self._phi_decide(prop, self._propose(prop[0]))
+
+    def _phi_draw(self):
+        """The host draws of a phi move: (phi_p, u), or None (phi fixed, or the proposal outside the
+        prior's support -- the draws are made either way, as the sampler always did)."""
         if self.fix_phi:
-            return
+            return None
         phi_p = self.phi * math.exp(self.phi_tuning * self.rng.standard_normal())
         lo, hi = self.priors.phi_unif
         u = self.rng.random()
         if not lo <= phi_p <= hi:
-            return
-        ph = self._propose(phi_p)
+            return None
+        return phi_p, u
+
+    def _phi_decide(self, prop, ph):
+        """Accept / reject a proposal given its sweep's host partials ``ph``."""
+        phi_p, u = prop
         if ph[2] >= 0:
             # the proposal's latent factor is not positive definite (near-duplicate locations
             # with tau2 = 0 and a large phi): zero density there, so the move is rejected
@@ -408,8 +427,18 @@ class SeqNNGP:
 
     def _stats(self):
         """[sum r^2/F, sum h (yres - w)^2, X'H(y - w)] on the host (the sharded chain: folded over ranks)."""
+        return self._stats_dev().cpu().numpy()
+
+    def _stats_dev(self):
+        """The same statistics, stream-ordered on the device (no host synchronisation)."""
         return _lib.gibbs_stats(self.r, self.Ft, self.yres, self.y, self.X, self.w, out=self._stats_buf,
-                                noise_w=self.noise_w).cpu().numpy()
+                                noise_w=self.noise_w)
+
+    def _member_rows_t(self):
+        """The colour-ordered member rows (location, reverse-entry range), built once."""
+        if getattr(self, "_member_rows", None) is None and self.members.numel() > 0:
+            self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
+        return getattr(self, "_member_rows", None)
 
     def _assemble(self, t):
         """A per-node (storage order) result as every rank sees it (identity on one GPU)."""
@@ -420,8 +449,7 @@ class SeqNNGP:
 
     def _sweep_colours(self, c0, c1):
         if c1 > c0:
-            if getattr(self, "_member_rows", None) is None:  # (location, reverse-entry range) per member, once
-                self._member_rows = _lib.gibbs_member_rows(self.members, self.off)
+            self._member_rows_t()  # (location, reverse-entry range) per member, once
             _lib.gibbs_w_sweep(self.members, self.color_off[c0:c1 + 1], self._prep, self.m, self.sigma2, self.tau2,
                                self.yres, self.w, self.r, self.off, self.rev_j, self.seed, self.iteration, z=self._z,
                                noise_w=self.noise_w, member_rows=self._member_rows)
@@ -454,17 +482,22 @@ class SeqNNGP:
 
     def step(self):
         """One iteration: phi; sigma2; update_wt; update_ws; tau2; beta; update_y_unobserved."""
-        n = self.n
         self.update_phi()
-        # sigma2 | w, phi (held fixed on request, and with a callable covariance: its own scale)
-        if not self.fix_sigma2:
-            a, b = self.priors.sigma2_ig
-            self.sigma2 = self._ig(a + 0.5 * n, b + 0.5 * self.quad)
-        # w | rest (colour steps, in place on w and r; the sweep's normals in one parallel pass)
-        _lib.gibbs_normals(self._z, self.seed, self.iteration)
+        self._before_w()
         self.update_wt()
         self.update_ws()
-        st = self._stats()
+        self._after_w(self._stats())
+
+    def _before_w(self):
+        """sigma2 | w, phi (held fixed on request, and with a callable covariance: its own scale), then the
+        w sweep's normals in one parallel pass."""
+        if not self.fix_sigma2:
+            a, b = self.priors.sigma2_ig
+            self.sigma2 = self._ig(a + 0.5 * self.n, b + 0.5 * self.quad)
+        _lib.gibbs_normals(self._z, self.seed, self.iteration)
+
+    def _after_w(self, st):
+        """tau2, beta, y - X beta, the predictive draws, from the host statistics ``st`` of the new w."""
         self.quad = float(st[0])
         # tau2 | y, beta, w (weighted residual sum of squares over the observed; held fixed on request)
         if not self.fix_tau2:
@@ -500,6 +533,30 @@ class SeqNNGP:
         self._sweep_into(self.phi, self.B, self.Ft, self.r)
         ph = self._part.cpu().numpy()
         self.sum_logF, self.quad = float(ph[0]), float(ph[1])
+
+    def clone(self, seed: int) -> "SeqNNGP":
+        """A chain on the same field, data and settings started as ``SeqNNGP(..., seed=seed)`` would be:
+        the DAG, colouring, reverse lists, plan and covariance blocks are shared (read-only), the state
+        and every buffer a step writes are its own.  Cloned before the first step it runs the chain of
+        ``seed`` bit for bit (the constructor's state does not depend on the seed)."""
+        import copy
+
+        if self.iteration != 0:
+            raise ValueError("clone a sampler before its first step")
+        c = copy.copy(self)
+        c.seed = int(seed)
+        c.rng = np.random.default_rng(seed)
+        c.beta = np.array(self.beta)
+        own = lambda t: None if t is None else t.clone()  # noqa: E731
+        c.w, c.r, c.B, c.Ft = own(self.w), own(self.r), own(self.B), own(self.Ft)
+        c._B2, c._Ft2, c._r2 = torch.empty_like(self._B2), torch.empty_like(self._Ft2), torch.empty_like(self._r2)
+        c._part, c._z, c._stats_buf = own(self._part), torch.empty_like(self._z), own(self._stats_buf)
+        c._ws = own(self._ws)
+        c._prep = own(self._prep)
+        c._yres_buf = own(self._yres_buf)
+        c.yres = c._yres_buf
+        c.y_unobserved, c._zy = own(self.y_unobserved), torch.empty_like(self._zy)
+        return c
 
     # ------------------------------------------------------------------ checkpoint / resume
     def _settings(self) -> dict:
@@ -626,3 +683,77 @@ class SeqNNGP:
         if self.y_unobserved.numel():
             res["y_unobserved_mean"] = self._assemble_unobserved(y_sum / max(kept, 1)).cpu().numpy()
         return res
+
+
+class SeqNNGPChains:
+    """``C`` independent :class:`SeqNNGP` chains of one field advanced together (BASELINE config 5's
+    replica mode, several chains per GPU): chain k is ``SeqNNGP(..., seed=seeds[k])`` bit for bit, but
+    the chains share the DAG and colouring, their colour steps run as ONE launch per colour for all
+    chains (nngp_gibbs_w_sweep_chains: the launch and member-row round trips paid once, C independent
+    gathers in flight per thread), and each iteration synchronises the host twice for all chains
+    (the phi proposals' partials, the conjugate statistics) instead of twice per chain.
+
+        chains = SeqNNGPChains(coords, y, seeds=[1, 2, 3, 4], m=15, ...)
+        chains.step()                 # one iteration of every chain
+        chains[k].beta, chains[k].w   # chain k's state (a SeqNNGP)
+    """
+
+    def __init__(self, coords, y, X=None, seeds=(0,), **kw):
+        seeds = [int(s) for s in seeds]
+        if not 1 <= len(seeds) <= 8:
+            raise ValueError("1 to 8 chains per batch")
+        if "seed" in kw:
+            raise ValueError("give the chains' seeds as seeds=[...]")
+        first = SeqNNGP(coords, y, X, seed=seeds[0], **kw)
+        if type(first)._use_plan is False:
+            raise ValueError("SeqNNGPChains runs SeqNNGP chains")
+        self.chains = [first] + [first.clone(s) for s in seeds[1:]]
+
+    def __len__(self):
+        return len(self.chains)
+
+    def __getitem__(self, k) -> SeqNNGP:
+        return self.chains[k]
+
+    def step(self):
+        cs = self.chains
+        # phi: every chain's host draws and proposal sweep, then ONE synchronisation for all partials
+        props = [c._phi_draw() for c in cs]
+        parts = []
+        for c, p in zip(cs, props):
+            if p is not None:
+                c._sweep_into(p[0], c._B2, c._Ft2, c._r2)
+                parts.append(c._part.clone())
+        ph = torch.stack(parts).cpu().numpy() if parts else None
+        k = 0
+        for c, p in zip(cs, props):
+            if p is not None:
+                c._phi_decide(p, ph[k])
+                k += 1
+        for c in cs:
+            c._before_w()
+        # w | rest: update_wt (the leaves' colour) then update_ws, one launch per colour for all chains
+        c0 = cs[0]
+        if c0._member_rows_t() is not None:
+            for lo, hi in ((c0.n_colors_ref, c0.n_colors), (0, c0.n_colors_ref)):
+                if hi > lo:
+                    _lib.gibbs_w_sweep_chains(c0._member_rows, c0.color_off[lo:hi + 1], [c._prep for c in cs], c0.m,
+                                              [c.sigma2 for c in cs], [c.tau2 for c in cs], [c.yres for c in cs],
+                                              [c.w for c in cs], [c.r for c in cs], c0.rev_j, [c._z for c in cs],
+                                              noise_w=c0.noise_w)
+        # the conjugate statistics of every chain, ONE synchronisation
+        st = torch.stack([c._stats_dev() for c in cs]).cpu().numpy()
+        for c, s_ in zip(cs, st):
+            c._after_w(s_)
+
+    def sample(self, n_iter: int):
+        """Run n_iter iterations of every chain; returns per-chain arrays of beta, sigma2, tau2, phi."""
+        out = [{"beta": [], "sigma2": [], "tau2": [], "phi": []} for _ in self.chains]
+        for _ in range(n_iter):
+            self.step()
+            for o, c in zip(out, self.chains):
+                o["beta"].append(c.beta.copy())
+                o["sigma2"].append(c.sigma2)
+                o["tau2"].append(c.tau2)
+                o["phi"].append(c.phi)
+        return [{k: np.asarray(v) for k, v in o.items()} for o in out]

@@ -192,6 +192,8 @@ class ShardedSeqNNGP(SeqNNGP):
     boundary members per colour, default) or "all" (every member, round 3's all-gather).
     """
 
+    _use_plan = False  # the phi sweeps cover this rank's rows and halo, not the whole field
+
     def __init__(self, *args, rank: Optional[int] = None, world: Optional[int] = None, group=None,
                  collective: Optional[bool] = None, graphs: Optional[bool] = None, exchange: str = "halo",
                  **kwargs):
