@@ -301,6 +301,11 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  * nngp_color_moral_graph (HOST pointers, host computation): greedy colouring
  *   of the moral graph (i ~ N(i); co-parents of a child ~ each other) in index
  *   order; returns the number of colours (or a negative NNGP_E* code).
+ * nngp_color_moral_graph_dev: the same colouring (bit for bit: node i takes the smallest colour
+ *   no moral neighbour k < i holds) on the device, in parallel rounds (nbr, off, rev_j, color:
+ *   device; workspace: >= 256 device bytes); a setup call that synchronises the stream once per 16
+ *   rounds.  Returns the number of colours, or a negative NNGP_E* code (NNGP_EUNSUP past 256
+ *   colours: use the host version).
  * nngp_gibbs_prepare: fold the factors of the unit-variance field (sigma2 = 1,
  *   tau2 = 0; B (n, m) and Ft (n,) from nngp_bf_sweep) into reverse-list order for
  *   the w sweeps: B_{j,i} and B_{j,i}/F_j per reverse entry, sum_e B_{j,i}^2/F_j and
@@ -359,6 +364,8 @@ int nngp_reverse_neighbors(const int32_t *nbr, int64_t n, int32_t m, int32_t *of
                            void *workspace, size_t workspace_bytes, void *stream);
 int64_t nngp_color_moral_graph(const int32_t *nbr_host, const int32_t *off_host, const int32_t *rev_j_host,
                                int64_t n, int32_t m, int32_t *color_host);
+int64_t nngp_color_moral_graph_dev(const int32_t *nbr, const int32_t *off, const int32_t *rev_j, int64_t n, int32_t m,
+                                   int32_t *color, void *workspace, size_t workspace_bytes, void *stream);
 size_t nngp_gibbs_prep_bytes(int64_t n, int32_t m);
 int nngp_gibbs_prepare(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
                        const int32_t *rev_k, const int32_t *order, int64_t n, int32_t m, void *prep,

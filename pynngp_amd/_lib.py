@@ -56,6 +56,7 @@ SYMBOLS = (
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
     "nngp_gibbs_w_sweep_chains",
+    "nngp_color_moral_graph_dev",
     "nngp_pair_plan_supported",
     "nngp_pair_plan_bytes",
     "nngp_pair_plan_build",
@@ -165,6 +166,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_gibbs_stats.argtypes = [I64, P, P, P, P, P, I32, P, P, P, P, SZ, P]
     lib.nngp_gibbs_stats.restype = ctypes.c_int
     lib.nngp_bf_sweep.restype = ctypes.c_int
+    lib.nngp_color_moral_graph_dev.argtypes = [P, P, P, I64, I32, P, P, SZ, P]
+    lib.nngp_color_moral_graph_dev.restype = I64
     lib.nngp_gibbs_w_sweep_chains.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
     lib.nngp_gibbs_w_sweep_chains.restype = ctypes.c_int
     lib.nngp_pair_plan_supported.argtypes = [I32, I32, I32]
@@ -714,6 +717,24 @@ def color_moral_graph(nbr_host, off_host, rev_j_host):
     if nc < 0:
         _check(int(nc), "nngp_color_moral_graph")
     return colors, int(nc)
+
+
+def color_moral_graph_dev(nbr: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor):
+    """:func:`color_moral_graph` on the device (nngp_color_moral_graph_dev, the same colours bit for bit):
+    (colors int32 (n,) device tensor, n_colors).  Falls back to the host greedy past 256 colours."""
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError("nbr must be int32 (n, m)")
+    dev = _require_gpu(nbr, off, rev_j)
+    n, m = nbr.shape
+    color = torch.empty(n, dtype=torch.int32, device=dev)
+    ws = _workspace(256, dev)
+    nc = load().nngp_color_moral_graph_dev(_ptr(nbr.contiguous()), _ptr(off), _ptr(rev_j), n, m, _ptr(color), _ptr(ws),
+                                           ws.numel(), _stream(dev))
+    if nc == -4:  # NNGP_EUNSUP: more than 256 colours
+        c, k = color_moral_graph(nbr.cpu().numpy(), off.cpu().numpy(), rev_j.cpu().numpy())
+        return torch.from_numpy(c).to(dev), k
+    _check(0 if nc >= 0 else int(nc), "nngp_color_moral_graph_dev")
+    return color, int(nc)
 
 
 def gibbs_prepare(B: torch.Tensor, Ft: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor, rev_k: torch.Tensor,

@@ -401,6 +401,19 @@ int64_t nngp_color_moral_graph(const int32_t* nbr, const int32_t* off, const int
     return nngp::color_moral_graph_host(nbr, off, rev_j, n, m, color);
 }
 
+int64_t nngp_color_moral_graph_dev(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int32_t m,
+                                   int32_t* color, void* workspace, size_t workspace_bytes, void* stream) {
+    if (n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n or m");
+    if (n > 0 && (off == nullptr || color == nullptr || workspace == nullptr || (m > 0 && (nbr == nullptr || rev_j == nullptr))))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (workspace_bytes < 256) return fail(NNGP_EINVAL, "workspace too small: %zu < 256 bytes", workspace_bytes);
+    hipError_t e;
+    const int64_t nc = nngp::color_moral_graph_device(nbr, off, rev_j, n, m, color, workspace, (hipStream_t)stream, &e);
+    if (nc == -2) return hip_fail(e, "color_moral_graph rounds");
+    if (nc == -1) return fail(NNGP_EUNSUP, "more than 256 colours: colour on the host (nngp_color_moral_graph)");
+    return nc;
+}
+
 size_t nngp_gibbs_prep_bytes(int64_t n, int32_t m) {
     if (n < 0 || m < 0 || m > NNGP_MAX_M) return 0;
     return nngp::gibbs_prep_bytes(n, m);

@@ -191,6 +191,98 @@ int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int
     return n_colors;
 }
 
+// ---------------------------------------------------------------- moral-graph colouring (device)
+// The same greedy colouring as color_moral_graph_host -- node i takes the smallest colour no moral
+// neighbour k < i holds -- computed in parallel rounds (Jones-Plassmann with the index as priority): in a
+// round every uncoloured node whose lower moral neighbours are all coloured takes its colour.  A colour
+// is final once written and a node reads its neighbours only when all are final, so the result is the
+// sequential greedy's, whatever the timing (a stale "uncoloured" read -- another XCD's L2 -- only defers a
+// node to a later round).  Rounds = the longest index-decreasing path of the moral graph (549 at
+// N = 1e6, m = 15, measured on the host: tools note in DESIGN.md 4.5); a node scans its ~m + m^2 lower
+// neighbours once, when it is coloured, and stops at the first uncoloured one before.  Up to 256 colours
+// (a 256-bit mask); more sets *overflow and the caller colours on the host.
+__global__ __launch_bounds__(256) void color_round_kernel(const int32_t* __restrict__ nbr, const int32_t* __restrict__ off,
+                                                          const int32_t* __restrict__ rev_j, int64_t n, int m,
+                                                          int32_t* color, unsigned long long* __restrict__ done,
+                                                          int32_t* __restrict__ overflow, int32_t* __restrict__ maxc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (color[i] >= 0) return;
+    uint64_t used[4] = {0, 0, 0, 0};
+    // true when k is a lower neighbour that is still uncoloured (not ready); marks its colour otherwise
+    auto lower = [&](int64_t k) -> bool {
+        if (k < 0 || k >= i) return false;
+        const int32_t c = color[k];
+        if (c < 0) return true;
+        used[(c >> 6) & 3] |= c < 256 ? (1ull << (c & 63)) : 0ull;
+        return false;
+    };
+    const int32_t* row = nbr + i * m;
+    for (int s = 0; s < m; ++s)
+        if (lower(row[s])) return;
+    for (int32_t e = off[i]; e < off[i + 1]; ++e) {
+        const int64_t j = rev_j[e];
+        if (lower(j)) return;
+        const int32_t* rj = nbr + j * m;
+        for (int s = 0; s < m; ++s) {
+            const int64_t k = rj[s];
+            if (k != i && lower(k)) return;
+        }
+    }
+    int c = 0;
+    while (c < 256 && ((used[c >> 6] >> (c & 63)) & 1ull)) ++c;
+    if (c >= 256) {
+        *overflow = 1;
+        return;
+    }
+    color[i] = c;
+    atomicAdd(done, 1ull);
+    atomicMax(maxc, c);
+}
+
+// colour -1 everywhere, the counters zero
+__global__ __launch_bounds__(256) void color_init_kernel(int32_t* __restrict__ color, int64_t n,
+                                                         unsigned long long* done, int32_t* overflow, int32_t* maxc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) color[i] = -1;
+    if (i == 0) {
+        *done = 0ull;
+        *overflow = 0;
+        *maxc = -1;
+    }
+}
+
+// rounds until every node is coloured (the host reads the count every kColorCheck rounds: one
+// synchronisation per check, ~40 at N = 1e6); returns the number of colours, -1 on overflow (more than
+// 256 colours: colour on the host), -2 on a HIP error (*err)
+int64_t color_moral_graph_device(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
+                                 int32_t* color, void* workspace, hipStream_t s, hipError_t* err) {
+    constexpr int kColorCheck = 16;
+    unsigned long long* done = (unsigned long long*)workspace;
+    int32_t* overflow = (int32_t*)((char*)workspace + 8);
+    int32_t* maxc = (int32_t*)((char*)workspace + 12);
+    *err = hipSuccess;
+    if (n == 0) return 0;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(color_init_kernel, grid, dim3(256), 0, s, color, n, done, overflow, maxc);
+    struct {
+        unsigned long long done;
+        int32_t overflow, maxc;
+    } h{0, 0, -1};
+    // (a round colours at least the lowest uncoloured node: n rounds always suffice)
+    for (int64_t round = 0; round <= n; round += kColorCheck) {
+        for (int k = 0; k < kColorCheck; ++k)
+            hipLaunchKernelGGL(color_round_kernel, grid, dim3(256), 0, s, nbr, off, rev_j, n, m, color, done, overflow,
+                               maxc);
+        if ((*err = hipGetLastError()) != hipSuccess) return -2;
+        if ((*err = hipMemcpyAsync(&h, workspace, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return -2;
+        if ((*err = hipStreamSynchronize(s)) != hipSuccess) return -2;
+        if (h.overflow) return -1;
+        if ((int64_t)h.done >= n) break;
+    }
+    return (int64_t)h.maxc + 1;
+}
+
 // ---------------------------------------------------------------- per-phi preparation
 // Everything of the w full conditionals that depends on B / F only (i.e. changes only
 // when a new phi is accepted) is folded once into reverse-list order:

@@ -171,6 +171,8 @@ hipError_t reverse_launch(const int32_t* nbr, int64_t n, int m, int32_t* off, in
                           void* workspace, hipStream_t s);
 int64_t color_moral_graph_host(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
                                int32_t* color);
+int64_t color_moral_graph_device(const int32_t* nbr, const int32_t* off, const int32_t* rev_j, int64_t n, int m,
+                                 int32_t* color, void* workspace, hipStream_t s, hipError_t* err);
 size_t gibbs_prep_bytes(int64_t n, int m);
 hipError_t philox_normals_launch(int64_t n, uint64_t seed, uint64_t sweep, double* z, hipStream_t s);
 hipError_t gibbs_prepare_launch(const double* B, const double* Ft, const int32_t* off, const int32_t* rev_j,

@@ -60,10 +60,19 @@ def _as_points(a, what):
 
 def colour_dag(nbr, off, rev_j, n_s):
     """Colour the moral graph of the DAG whose first ``n_s`` nodes are the reference points
-    and the rest leaves (host arrays in model order: nbr (n, m), reverse CSR off / rev_j).
-    Greedy over the reference points (leaves come later, so only their co-parent edges
+    and the rest leaves (in model order: nbr (n, m), reverse CSR off / rev_j -- host numpy arrays
+    (the host greedy) or device tensors (nngp_color_moral_graph_dev: the same colours, in parallel
+    rounds)).  Greedy over the reference points (leaves come later, so only their co-parent edges
     constrain S); the leaves, never parents and so pairwise non-adjacent, share one last
-    colour.  Returns (colors, n_colors, n_colors_ref)."""
+    colour.  Returns (colors, n_colors, n_colors_ref), colors of the inputs' kind."""
+    if isinstance(nbr, torch.Tensor):
+        colors, n_colors = _lib.color_moral_graph_dev(nbr, off, rev_j)
+        n = colors.shape[0]
+        if n > n_s:
+            n_colors = int(colors[:n_s].max().item()) + 1 if n_s else 0
+            colors[n_s:] = n_colors
+            return colors, n_colors + 1, n_colors
+        return colors, n_colors, n_colors
     colors, n_colors = _lib.color_moral_graph(nbr, off, rev_j)
     n = colors.shape[0]
     if n > n_s:
@@ -260,14 +269,15 @@ class SeqNNGP:
         # locations outside S) are never parents, hence pairwise non-adjacent: they form one
         # last colour of their own, swept by update_wt.
         off0, rev_j0, _ = _lib.reverse_neighbors(nbr0)
-        colors0, self.n_colors, self.n_colors_ref = colour_dag(nbr0.cpu().numpy(), off0.cpu().numpy(),
-                                                               rev_j0.cpu().numpy(), n_s)
-        colors = colors0[self.perm.cpu().numpy()]
-        self.colors = colors
+        # on the device (round 5: the host greedy took ~10 s at N = 1e7; the same colours)
+        colors0, self.n_colors, self.n_colors_ref = colour_dag(nbr0, off0, rev_j0, n_s)
+        del off0, rev_j0
+        colors_d = colors0[self.perm]
+        self.colors = colors_d.cpu().numpy()
         # members grouped by colour, storage (= Z) order inside a colour
-        self.members = torch.from_numpy(np.argsort(colors, kind="stable").astype(np.int32)).to(dev)
-        self.color_off = np.concatenate([[0], np.cumsum(np.bincount(colors, minlength=self.n_colors))]).astype(
-            np.int32)
+        self.members = torch.sort(colors_d, stable=True)[1].to(torch.int32)
+        self.color_off = np.concatenate([[0], np.cumsum(torch.bincount(colors_d, minlength=self.n_colors).cpu().numpy())
+                                         ]).astype(np.int32)
         pos_h = self.pos.cpu().numpy()
         self._un_nodes = torch.from_numpy(pos_h[un_nodes].astype(np.int64)).to(dev)  # storage slots
         self._un_sd = to(un_sd)
