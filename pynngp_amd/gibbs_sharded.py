@@ -66,88 +66,108 @@ class GibbsShardPlan:
     allgather_bytes: int    # ... had every member been all-gathered (sum_c world * maxc[c] * 8)
 
 
+def _tt(a, dev, dtype=torch.int64):
+    """an input array as a torch tensor on dev (device tensors stay where they are)"""
+    t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+    return t.to(device=dev, dtype=dtype)
+
+
 def gibbs_shard_plan(nbr, off, rev_j, colors, members, color_off, world: int, rank: int,
-                     exchange: str = "halo") -> GibbsShardPlan:
-    """Plan rank ``rank`` of ``world`` for the DAG in storage order (host numpy arrays: nbr (n, m),
-    reverse CSR off / rev_j, colours, members grouped by colour ascending inside a colour, colour
-    offsets).  Every rank computes the same runs, slot sizes and sources.  ``exchange="halo"`` moves
+                     exchange: str = "halo", device=None) -> GibbsShardPlan:
+    """Plan rank ``rank`` of ``world`` for the DAG in storage order (nbr (n, m), reverse CSR off / rev_j,
+    colours, members grouped by colour ascending inside a colour, colour offsets -- numpy arrays or
+    torch tensors).  Every rank computes the same runs, slot sizes and sources.  ``exchange="halo"`` moves
     the boundary members only; ``"all"`` every member (round 3's all-gather: the A/B reference, and at
-    one rank the only way to put a collective in the colour loop)."""
+    one rank the only way to put a collective in the colour loop).  The array work runs in torch on
+    ``device`` (default: the inputs' device; a sharded chain plans on its GPU -- round 5: 12 s per rank
+    at N = 1e7 in host numpy); the plan's fields come back as numpy arrays."""
     if exchange not in ("halo", "all"):
         raise ValueError("exchange must be 'halo' or 'all'")
-    nbr = np.asarray(nbr)
-    off = np.asarray(off, dtype=np.int64)
-    rev_j = np.asarray(rev_j)
-    colors = np.asarray(colors, dtype=np.int64)
-    members = np.asarray(members, dtype=np.int64)
-    color_off = np.asarray(color_off, dtype=np.int64)
+    dev = torch.device(device) if device is not None else (nbr.device if isinstance(nbr, torch.Tensor)
+                                                           else torch.device("cpu"))
+    nbr = _tt(nbr, dev, torch.int64)
+    off = _tt(off, dev)
+    rev_j = _tt(rev_j, dev)
+    colors = _tt(colors, dev)
+    members = _tt(members, dev)
+    color_off = _tt(color_off, dev)
     n = nbr.shape[0]
-    n_colors = len(color_off) - 1
-    bounds = np.array([shard_range(n, r, world)[0] for r in range(world)] + [n], dtype=np.int64)
-    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-    run = np.empty((n_colors, world + 1), dtype=np.int64)
-    for c in range(n_colors):
-        seg = members[color_off[c]:color_off[c + 1]]
-        if seg.size > 1 and not np.all(seg[1:] > seg[:-1]):
-            raise ValueError("members must ascend inside each colour (storage order)")
-        run[c] = color_off[c] + np.searchsorted(seg, bounds)
-    counts = np.diff(run, axis=1)
-    maxc = counts.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
-    send_off = np.concatenate([[0], np.cumsum(maxc)]).astype(np.int64)
-    exported = gibbs_boundary(nbr, bounds) if exchange == "halo" else np.ones(nbr.shape[0], dtype=bool)
+    n_colors = color_off.numel() - 1
+    bounds_l = [shard_range(n, r, world)[0] for r in range(world)] + [n]
+    bounds = torch.tensor(bounds_l, dtype=torch.int64, device=dev)
+    lo, hi = bounds_l[rank], bounds_l[rank + 1]
+    # members ascend inside each colour and the colours are contiguous runs: (colour, member) keys ascend
+    # over the whole array, so one searchsorted gives every (colour, rank) run
+    key_cm = colors[members] * (n + 1) + members if n_colors else members
+    if members.numel() > 1 and not bool((key_cm[1:] > key_cm[:-1]).all()):
+        raise ValueError("members must ascend inside each colour (storage order)")
+    cidx = torch.arange(n_colors, dtype=torch.int64, device=dev)
+    run = torch.searchsorted(key_cm, (cidx[:, None] * (n + 1) + bounds[None, :]).contiguous()) if n_colors else \
+        torch.zeros((0, world + 1), dtype=torch.int64, device=dev)
+    counts = run[:, 1:] - run[:, :-1]
+    maxc = counts.max(dim=1).values if world > 0 and n_colors else torch.zeros(n_colors, dtype=torch.int64, device=dev)
+    send_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(maxc, 0)])
+    exported = gibbs_boundary(nbr, bounds) if exchange == "halo" else torch.ones(n, dtype=torch.bool, device=dev)
     # each (colour, rank) run ordered boundary members first (ascending), then the rest: the colour
     # step's publish slot then starts with exactly the values the other ranks replay.  (Members of a
     # colour are independent and their normals are keyed by location, so the order changes no bit.)
-    key = np.repeat(np.arange(n_colors * world, dtype=np.int64), counts.ravel())  # (colour, rank) run of a slot
-    xo = np.lexsort((members, ~exported[members], key))
-    members_x = members[xo]
-    cs = np.concatenate([[0], np.cumsum(exported[members_x], dtype=np.int64)])
+    key = torch.repeat_interleave(torch.arange(n_colors * world, dtype=torch.int64, device=dev), counts.reshape(-1))
+    xkey = (key << 33) | ((~exported[members]).to(torch.int64) << 32) | members
+    members_x = members[torch.sort(xkey)[1]]
+    cs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(exported[members_x].to(torch.int64), 0)])
     bcount = cs[run[:, 1:]] - cs[run[:, :-1]]
-    bmax = bcount.max(axis=1) if world > 0 and n_colors else np.zeros(n_colors, dtype=np.int64)
-    recv_off = np.concatenate([[0], np.cumsum(bmax * world)]).astype(np.int64)
+    bmax = bcount.max(dim=1).values if world > 0 and n_colors else torch.zeros(n_colors, dtype=torch.int64, device=dev)
+    recv_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(bmax * world, 0)])
     # halo: children of the own rows outside the shard; V: own rows, halo, parents of both
-    ch = rev_j[off[lo]:off[hi]].astype(np.int64)
-    halo = np.unique(ch[(ch < lo) | (ch >= hi)])
-    par = np.concatenate([nbr[lo:hi].ravel(), nbr[halo].ravel()]).astype(np.int64)
+    ch = rev_j[int(off[lo]):int(off[hi])]
+    halo = torch.unique(ch[(ch < lo) | (ch >= hi)])
+    par = torch.cat([nbr[lo:hi].reshape(-1), nbr[halo].reshape(-1)])
     par = par[(par >= 0) & (par < n)]
-    replica = np.unique(np.concatenate([np.arange(lo, hi), halo, par]))
+    replica = torch.unique(torch.cat([torch.arange(lo, hi, dtype=torch.int64, device=dev), halo, par]))
     foreign = replica[(replica < lo) | (replica >= hi)]
-    if not np.all(exported[foreign]):
+    if not bool(exported[foreign].all()):
         raise AssertionError("a foreign replica row is not on its owner's boundary")
-    pos = np.empty(n, dtype=np.int64)
-    pos[members_x] = np.arange(n)
+    pos = torch.empty(n, dtype=torch.int64, device=dev)
+    pos[members_x] = torch.arange(n, dtype=torch.int64, device=dev)
     cf = colors[foreign]
-    owner = np.searchsorted(bounds, foreign, side="right") - 1
+    owner = torch.searchsorted(bounds, foreign, right=True) - 1
     k = pos[foreign] - run[cf, owner]  # rank among the owner's boundary members of the colour
     src = recv_off[cf] + owner * bmax[cf] + k
-    order = np.argsort(cf, kind="stable")
-    apply_rows = np.stack([foreign, off[foreign], off[foreign + 1], src], axis=1)[order].astype(np.int32)
-    apply_off = np.concatenate([[0], np.cumsum(np.bincount(cf, minlength=n_colors))]).astype(np.int64)
-    return GibbsShardPlan(world, rank, lo, hi, bounds, run, maxc, send_off, recv_off, halo, replica,
-                          np.ascontiguousarray(apply_rows), apply_off, members_x.astype(np.int32), exported, bcount,
-                          bmax, int(8 * world * bmax.sum()), int(8 * world * maxc.sum()))
+    order = torch.sort(cf, stable=True)[1]
+    apply_rows = torch.stack([foreign, off[foreign], off[foreign + 1], src], dim=1)[order].to(torch.int32)
+    apply_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
+                           torch.cumsum(torch.bincount(cf, minlength=n_colors), 0)])
+    h = lambda t: t.cpu().numpy()  # noqa: E731
+    return GibbsShardPlan(world, rank, lo, hi, h(bounds), h(run), h(maxc), h(send_off), h(recv_off), h(halo),
+                          h(replica), np.ascontiguousarray(h(apply_rows)), h(apply_off), h(members_x.to(torch.int32)),
+                          h(exported), h(bcount), h(bmax), int(8 * world * int(bmax.sum())),
+                          int(8 * world * int(maxc.sum())))
 
 
-def gibbs_boundary(nbr, bounds) -> np.ndarray:
+def gibbs_boundary(nbr, bounds):
     """exported[i]: row i is in the replica set V(r) = own(r) + H(r) + parents of both of some rank r
     other than its owner (H(r): the out-of-shard children of own(r)).  i is in V(r), r != owner(i),
     exactly when i has a parent owned by r (i in H(r)), or i is a parent of a row j that r owns or that
     has a parent owned by r (i in parents(own(r) + H(r))).  With T(j) = {owner(j)} + owners of j's
     parents: exported[i] = T(i) != {owner(i)} or T(j) != {owner(i)} for some child j of i -- one pass over
-    the parent lists (nbr, -1 padded), identical on every rank."""
-    nbr = np.asarray(nbr)
+    the parent lists (nbr, -1 padded), identical on every rank.  numpy or torch in, the same kind out."""
+    as_np = not isinstance(nbr, torch.Tensor)
+    nbr = _tt(nbr, torch.device("cpu") if as_np else nbr.device)
+    bounds = _tt(bounds, nbr.device)
     n = nbr.shape[0]
-    own = np.repeat(np.arange(len(bounds) - 1, dtype=np.int32), np.diff(bounds)).astype(np.int32)
+    own = torch.repeat_interleave(torch.arange(bounds.numel() - 1, dtype=torch.int64, device=nbr.device),
+                                  bounds[1:] - bounds[:-1])
     valid = (nbr >= 0) & (nbr < n)
-    on = np.where(valid, own[np.where(valid, nbr, 0)], -1)
-    tmin = np.minimum(own, np.where(valid, on, np.iinfo(np.int32).max).min(axis=1)) if nbr.shape[1] else own
-    tmax = np.maximum(own, on.max(axis=1)) if nbr.shape[1] else own
+    on = torch.where(valid, own[torch.where(valid, nbr, 0)], -1)
+    big = torch.iinfo(torch.int64).max
+    tmin = torch.minimum(own, torch.where(valid, on, big).min(dim=1).values) if nbr.shape[1] else own
+    tmax = torch.maximum(own, on.max(dim=1).values) if nbr.shape[1] else own
     exported = (tmin != own) | (tmax != own)
-    jj, ss = np.nonzero(valid)
+    jj, ss = torch.nonzero(valid, as_tuple=True)
     pi = nbr[jj, ss]
     hit = (tmin[jj] != own[pi]) | (tmax[jj] != own[pi])
     exported[pi[hit]] = True
-    return exported
+    return exported.cpu().numpy() if as_np else exported
 
 
 class ColourExchange:
@@ -210,9 +230,8 @@ class ShardedSeqNNGP(SeqNNGP):
             raise ValueError("a sharded chain over several ranks needs a torch.distributed process group")
         dev = self.device
         n, m = self.n, self.m
-        self.plan = p = gibbs_shard_plan(self.nbr.cpu().numpy(), self.off.cpu().numpy(), self.rev_j.cpu().numpy(),
-                                         self.colors, self.members.cpu().numpy(), self.color_off, self.world,
-                                         self.rank, exchange=exchange)
+        self.plan = p = gibbs_shard_plan(self.nbr, self.off, self.rev_j, self.colors, self.members, self.color_off,
+                                         self.world, self.rank, exchange=exchange, device=dev)
         self.lo, self.hi = p.lo, p.hi
         # the colour runs in the plan's order (boundary members first: the head of each publish slot)
         self._member_rows = _lib.gibbs_member_rows(torch.from_numpy(p.members_x).to(dev), self.off)

@@ -36,7 +36,12 @@ def main():
     ap.add_argument("--m", type=int, default=15)
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--gpu", action="store_true",
+                    help="the round-5 device path: SeqNNGP's whole setup (kNN, Z-order, reverse lists, the device "
+                         "colouring, the pair plan) and the shard plan on the GPU, timed")
     a = ap.parse_args()
+    if a.gpu:
+        return main_gpu(a)
     from oracle import nngp_oracle as O
     from pynngp_amd import _lib
     from pynngp_amd.gibbs_sharded import gibbs_shard_plan
@@ -86,6 +91,44 @@ def main():
         print(json.dumps(res["ranks"][-1]), flush=True)
     res.update(t)
     res["host"] = {"cpus": os.cpu_count()}
+    print(json.dumps(res))
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+def main_gpu(a):
+    import torch
+
+    from pynngp_amd import SeqNNGP
+    from pynngp_amd.gibbs_sharded import gibbs_shard_plan
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(2)
+    coords = rng.uniform(0, 1, (a.n, 2))
+    y = np.sin(6 * coords[:, 0]) + 0.3 * rng.standard_normal(a.n)
+    torch.ones(1, device=dev).sum().item()  # context
+    res = {"n": a.n, "m": a.m, "world": a.world, "device": torch.cuda.get_device_name(0), "ranks": []}
+    for rep in range(2):  # the first pays one-time library / allocator warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s = SeqNNGP(coords, y, m=a.m, sigma2=1.0, tau2=0.1, phi=30.0, device=dev)
+        torch.cuda.synchronize()
+        res[f"seqnngp_setup_s_{rep}"] = time.perf_counter() - t0
+        res["n_colors"] = int(s.n_colors)
+        if rep == 0:
+            del s
+    for rank in (0, a.world // 2, a.world - 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        p = gibbs_shard_plan(s.nbr, s.off, s.rev_j, s.colors, s.members, s.color_off, a.world, rank, device=dev)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        res["ranks"].append({"rank": rank, "plan_s": el, "own_rows": p.hi - p.lo, "halo": int(p.halo.size),
+                             "replica": int(p.replica.size), "exchange_bytes_per_sweep": p.exchange_bytes,
+                             "allgather_bytes_per_sweep": p.allgather_bytes})
+        print(json.dumps(res["ranks"][-1]), flush=True)
     print(json.dumps(res))
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)

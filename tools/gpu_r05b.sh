@@ -7,7 +7,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 o=gpurun_out/r05b
 mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests/test_gpu_plan.py tests/test_gpu_gibbs_chains.py tests/test_gpu_callable_cov.py \
-  tests/test_gpu_matern.py tests/test_gpu_api.py -x -v --timeout 120 --timeout-method thread \
+  tests/test_gpu_matern.py tests/test_gpu_api.py tests/test_gpu_gibbs.py -x -v --timeout 120 --timeout-method thread \
   > $o/pytest_new.txt 2>&1 || { tail -60 $o/pytest_new.txt; exit 1; }
 tail -3 $o/pytest_new.txt
 for r in 1 2; do
