@@ -46,14 +46,15 @@ extern "C" {
 #define NNGP_COV_SPHERICAL 4   /* sigma2 (1 - 3u/2 + u^3/2) for u < 1, else 0       */
 #define NNGP_COV_MATERN 5      /* sigma2 u^nu K_nu(u) / (2^(nu-1) Gamma(nu)), 0 < nu <= 50: spNNGP's
                                   "matern" of any smoothness nu (the `nu` argument of the sweeps;
-                                  ignored by the other kinds).  m <= 24: the pair kernel evaluating
-                                  rho from a per-launch table in (phi d)^2 (nu >= ~0.45, whose table
-                                  fits 160 octaves); smaller nu and m > 24: the wavefront kernel's
-                                  direct Bessel evaluation. */
+                                  ignored by the other kinds).  m <= 24 (pair kernel) and 25..32
+                                  (four-lane kernel): rho from a per-launch table in t = (phi d)^2,
+                                  every nu; for nu < 0.9 whose table would pass 160 octaves, below
+                                  t = 2^-64 the small-t expansion 1 - A t^nu.  m > 32: the wavefront
+                                  kernel's direct Bessel evaluation. */
 
 /* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE serves 2-D
  * exponential / Matern-3/2 only, QUAD kinds 0..4 in every dimension, PAIRB and WAVE every kind
- * (PAIRB: NNGP_COV_MATERN with nu >= ~0.45).  (3 and 7 were comparison-only kernels of earlier
+ * (PAIRB and QUAD: NNGP_COV_MATERN through its table).  (3 and 7 were comparison-only kernels of earlier
  * builds; they are rejected as unknown.) */
 #define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above (matern: see kind 5) */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */

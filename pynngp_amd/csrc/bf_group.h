@@ -78,13 +78,29 @@ __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coord
                                                 double* __restrict__ bpart, int dim, const double* __restrict__ cblk) {
     static_assert(D == 0 || D == 2, "bf_group: 2-D or runtime dimension");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
+    // KIND == NNGP_KIND_MATERN: rho from the launch's Matern table (cblk, copied to dynamic LDS; nngp_math.h
+    // "Matern-nu by table"), sigma2 rho per entry -- the general-smoothness Matern at m = 25..32
+    constexpr bool MT = KIND == NNGP_KIND_MATERN;
+    extern __shared__ double4 grp_mtab[];
     static_assert(!CM || M <= 32, "the validity mask holds one bit per neighbour slot");
     constexpr int NR = M + 1;               // joint rows 0..M (row M = the location)
     constexpr int S = (NR + P - 1) / P;     // local rows per lane
     constexpr int DA = point_arity<D>();
     const int ds = D == 0 ? dim : 2;
-    __shared__ double etab[NNGP_EXP_TAB_N];
-    if constexpr (!CM) nngp_exp_table_load(etab, Pc.sigma2);
+    __shared__ double etab[MT ? 1 : NNGP_EXP_TAB_N];
+    if constexpr (MT) {
+        const int n4 = Pc.mt_noct * (NNGP_MT_K * NNGP_MT_NC / 4);
+        const double4* g = (const double4*)cblk;
+        for (int k = (int)threadIdx.x; k < n4; k += blockDim.x) grp_mtab[k] = g[k];
+        __syncthreads();
+    } else if constexpr (!CM) {
+        nngp_exp_table_load(etab, Pc.sigma2);
+    }
+    // the covariance of one entry at squared distance d2
+    auto cov = [&](double d2) -> double {
+        if constexpr (MT) return Pc.sigma2 * nngp_matern_tab(Pc, (const double*)grp_mtab, d2);
+        else return nngp_cov_d2<KIND>(Pc, etab, d2);
+    };
     const int64_t blk = xcd_logical_block(blockIdx.x, gridDim.x);
     const int64_t tid = blk * blockDim.x + threadIdx.x;
     const int q = (int)(threadIdx.x % P);
@@ -172,9 +188,9 @@ __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coord
             for (int b = 0; b < NR; ++b) {
                 if (b >= P * s + P) continue;  // beyond this local row's width
                 if (b < P * s) {
-                    R[s][b] = nngp_cov_d2<KIND>(Pc, etab, point_d2<DA>(o[s], X[b]));
+                    R[s][b] = cov(point_d2<DA>(o[s], X[b]));
                 } else if (b < P * s + P - 1) {  // diagonal block: lane-dependent
-                    const double c = nngp_cov_d2<KIND>(Pc, etab, point_d2<DA>(o[s], X[b]));
+                    const double c = cov(point_d2<DA>(o[s], X[b]));
                     R[s][b] = b < a ? c : (b == a ? Pc.diag : 0.0);
                 } else {
                     R[s][b] = b == a ? Pc.diag : 0.0;
@@ -263,7 +279,8 @@ __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coord
 template <int M, int KIND, int P, int D = 2>
 static void launch_group_mkp(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
     const int64_t blocks = (a.n_rows * P + 255) / 256;
-    hipLaunchKernelGGL((bf_group<M, KIND, P, D>), dim3((unsigned)blocks), dim3(256), 0, s, a.coords, a.n_points, a.nbr,
+    const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
+    hipLaunchKernelGGL((bf_group<M, KIND, P, D>), dim3((unsigned)blocks), dim3(256), lds, s, a.coords, a.n_points, a.nbr,
                        a.order, a.n_rows, a.i0, Pc, a.values, a.qcoords, a.qvalues, a.B, a.F, a.R, a.bpart, a.dim,
                        a.cblk);
 }
@@ -279,6 +296,15 @@ static bool launch_group_if(const BfArgs& a, const CovParams& Pc, hipStream_t s)
         launch_group_mkp<M, 0, P>(a, Pc, s);
     else
         launch_group_mkp<M, NNGP_KIND_GENERIC, P, 0>(a, Pc, s);
+    return true;
+}
+
+// general-smoothness Matern from the launch's table (a.cblk, bf_launch) at m = 25..32 (bf_quad_matern_*.hip:
+// units of their own, these fully unrolled kernels compile for minutes each)
+template <int M>
+static bool launch_group_matern_if(const BfArgs& a, const CovParams& Pc, hipStream_t s) {
+    if (a.m != M) return false;
+    launch_group_mkp<M, NNGP_KIND_MATERN, 4, 0>(a, Pc, s);
     return true;
 }
 

@@ -9,6 +9,8 @@ namespace nngp {
 
 bool bf_quad_launch_b(const BfArgs&, const CovParams&, hipStream_t);
 bool bf_quad_launch_c(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_quad_matern_launch_b(const BfArgs&, const CovParams&, hipStream_t);
+bool bf_quad_matern_launch_c(const BfArgs&, const CovParams&, hipStream_t);
 
 int64_t bf_group_blocks(int64_t n_rows, int P) { return (n_rows * P + 255) / 256; }
 
@@ -18,6 +20,8 @@ bool bf_group_supported(int m, int P) {
 
 bool bf_group_launch(const BfArgs& a, const CovParams& Pc, int P, hipStream_t s) {
     if (!bf_group_supported(a.m, P)) return false;
+    if (a.kind == NNGP_KIND_MATERN)  // the launch's table in a.cblk
+        return a.m <= 28 ? bf_quad_matern_launch_b(a, Pc, s) : bf_quad_matern_launch_c(a, Pc, s);
     return a.m <= 28 ? bf_quad_launch_b(a, Pc, s) : bf_quad_launch_c(a, Pc, s);
 }
 

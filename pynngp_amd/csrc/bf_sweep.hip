@@ -308,7 +308,7 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
             // the launch's Matern table (a function of nu only: t = phi^2 d^2) after the tile records
             nngp_matern_setup(Pu, a.nu);
             Pu.mphi2 = a.phi * a.phi;
-            if (!matern_table_extent(a.nu, &Pu.mt_e0, &Pu.mt_noct)) return hipErrorInvalidValue;
+            if (!matern_table_params(a.nu, &Pu)) return hipErrorInvalidValue;
             double* tab = (double*)((char*)a.bpart + bf_pairb_workspace_bytes(a.n_rows));
             hipError_t e = matern_table_launch(Pu, tab, s);
             if (e != hipSuccess) return e;
@@ -320,8 +320,21 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         if (e != hipSuccess || a.partials == nullptr || pairb_fuse_fold(a)) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoQuad) {
-        ok = bf_group_launch(a, P, 4, s);
         nb = bf_group_blocks(a.n_rows, 4);
+        if (a.kind == NNGP_KIND_MATERN) {
+            // the launch's Matern table after the block records (as the pair kernel's after its tile records)
+            CovParams Pm = P;
+            Pm.mphi2 = a.phi * a.phi;
+            if (!matern_table_params(a.nu, &Pm)) return hipErrorInvalidValue;
+            double* tab = (double*)((char*)a.bpart + ((size_t)nb * 4 * sizeof(double) + 255) / 256 * 256);
+            hipError_t e = matern_table_launch(Pm, tab, s);
+            if (e != hipSuccess) return e;
+            BfArgs b = a;
+            b.cblk = tab;
+            ok = bf_group_launch(b, Pm, 4, s);
+        } else {
+            ok = bf_group_launch(a, P, 4, s);
+        }
     } else {
         nb = bf_wave_blocks(a.n_rows);
         ok = bf_wave_launch(a, P, nb, s);

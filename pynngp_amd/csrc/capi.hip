@@ -37,22 +37,23 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
-    // general-smoothness Matern: the pair kernel with the launch's table for m <= 24 (nu >= NNGP_MT_NU_MIN;
-    // resolve_algo_nu decides for a given nu), the wavefront kernel (the direct Bessel evaluation) above
-    // (nngp_resolve_algo, nu unknown: the pair kernel's table covers nu >= ~0.45 only; a deferred sweep's
-    // finalize must use nngp_resolve_algo_nu's answer, and bf_finalize_pairb refuses a header that is not a
-    // pair-kernel sweep of that many rows)
-    if (kind == NNGP_COV_MATERN) return m >= 1 && m <= 24 ? nngp::kAlgoPairB : nngp::kAlgoWave;
+    // general-smoothness Matern: the launch's table on the pair kernel for m <= 24 and on the four-lane
+    // kernel for 25..32 (since round 5 every nu in (0, 50]: below 2^-64 in t the small-t expansion,
+    // nngp_math.h), the wavefront kernel (the direct Bessel evaluation) above.  (A deferred sweep's finalize
+    // takes the resolved algo; bf_finalize_pairb refuses a header that is not a pair-kernel sweep of that
+    // many rows.)
+    if (kind == NNGP_COV_MATERN)
+        return m >= 1 && m <= 24 ? nngp::kAlgoPairB : (m >= 25 && m <= 32 ? nngp::kAlgoQuad : nngp::kAlgoWave);
     if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
     if (m >= 25 && m <= 32) return nngp::kAlgoQuad;
     return nngp::kAlgoWave;
 }
 
-// ... for a given smoothness: the Matern table must fit NNGP_MT_MAX_OCT octaves (nu >= ~0.45), else the
-// wavefront kernel
+// ... for a given smoothness: the Matern table must fit NNGP_MT_MAX_OCT octaves (every nu in (0, 50] since
+// the small-t expansion took over below 2^-64; kept as the guard), else the wavefront kernel
 int resolve_algo_nu(int32_t algo, int32_t m, int32_t kind, int32_t dim, double nu) {
     const int a = resolve_algo(algo, m, kind, dim);
-    if (algo != NNGP_ALGO_AUTO || kind != NNGP_COV_MATERN || a != nngp::kAlgoPairB) return a;
+    if (algo != NNGP_ALGO_AUTO || kind != NNGP_COV_MATERN || (a != nngp::kAlgoPairB && a != nngp::kAlgoQuad)) return a;
     int e0, noct;
     return nu > 0.0 && nu <= NNGP_MATERN_NU_MAX && nngp::matern_table_extent(nu, &e0, &noct) ? a : nngp::kAlgoWave;
 }
@@ -92,11 +93,16 @@ size_t nngp_bf_sweep_workspace_bytes(int64_t n_rows, int32_t m, int32_t kind, in
     const int a = resolve_algo(algo, m, kind, dim);
     const int64_t nbw = n_rows > 0 ? bf_blocks(n_rows, nngp::kAlgoWave, m) : 0;
     if (kind == NNGP_COV_MATERN && a == nngp::kAlgoPairB) {
-        // tile records + exponent sums + the Matern table; AUTO (nu unknown here) also covers the
-        // wavefront kernel's records, which serve nu below the table's range
+        // tile records + exponent sums + the Matern table (AUTO also covers the wavefront kernel's records)
         const size_t pb = nngp::bf_pairb_workspace_bytes(n_rows) + align256(NNGP_MT_BYTES(NNGP_MT_MAX_OCT));
         const size_t wb = align256((size_t)nbw * 4 * sizeof(double));
         return algo == NNGP_ALGO_AUTO && wb > pb ? wb : pb;
+    }
+    if (kind == NNGP_COV_MATERN && a == nngp::kAlgoQuad) {  // block records + the Matern table
+        const int64_t nq = n_rows > 0 ? bf_blocks(n_rows, nngp::kAlgoQuad, m) : 0;
+        const size_t qb = align256((size_t)nq * 4 * sizeof(double)) + align256(NNGP_MT_BYTES(NNGP_MT_MAX_OCT));
+        const size_t wb = align256((size_t)nbw * 4 * sizeof(double));
+        return algo == NNGP_ALGO_AUTO && wb > qb ? wb : qb;
     }
     if (a == nngp::kAlgoPairB) return nngp::bf_pairb_workspace_bytes(n_rows);  // tile records + exponent sums
     const int64_t nb = n_rows > 0 ? bf_blocks(n_rows, a, m) : 0;
@@ -128,10 +134,10 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
     int a = resolve_algo_nu(algo, m, kind, dim, nu);
     if (a != nngp::kAlgoLane && a != nngp::kAlgoWave && a != nngp::kAlgoQuad && a != nngp::kAlgoPairB)
         return fail(NNGP_EINVAL, "unknown algo %d", algo);
-    if (kind == NNGP_COV_MATERN && a != nngp::kAlgoWave && a != nngp::kAlgoPairB)
-        return fail(NNGP_EUNSUP, "the matern kind runs on the pair kernel (m <= 24) or the wavefront kernel, not algo %d",
-                    algo);
-    if (kind == NNGP_COV_MATERN && a == nngp::kAlgoPairB) {
+    if (kind == NNGP_COV_MATERN && a != nngp::kAlgoWave && a != nngp::kAlgoPairB && a != nngp::kAlgoQuad)
+        return fail(NNGP_EUNSUP, "the matern kind runs on the pair (m <= 24), four-lane (25..32) or wavefront kernel, "
+                                 "not algo %d", algo);
+    if (kind == NNGP_COV_MATERN && (a == nngp::kAlgoPairB || a == nngp::kAlgoQuad)) {
         int e0, noct;
         if (!nngp::matern_table_extent(nu, &e0, &noct))
             return fail(NNGP_EUNSUP, "matern nu=%g needs %d table octaves (> %d; nu below ~%g): use NNGP_ALGO_AUTO or "

@@ -68,25 +68,37 @@ hipError_t matern_table_launch(const CovParams& P, double* tab, hipStream_t s) {
     return hipGetLastError();
 }
 
-// table extent for smoothness nu (nngp_matern_table_setup at phi = 1), cached per thread for the last
-// few nu: the setup evaluates rho and the small-t bound a few hundred times on the host
-bool matern_table_extent(double nu, int* e0, int* noct) {
+// the table geometry of nu (nngp_matern_table_setup: a few thousand host evaluations of rho), cached per
+// thread for the last few nu: mt_e0, mt_noct, mt_series, mt_A into *p; false when it does not fit
+bool matern_table_params(double nu, CovParams* p) {
     constexpr int kSlots = 8;
     thread_local double c_nu[kSlots] = {0, 0, 0, 0, 0, 0, 0, 0};
-    thread_local int c_e0[kSlots], c_noct[kSlots], c_next = 0;
+    thread_local CovParams c_p[kSlots];
+    thread_local int c_next = 0;
+    int hit = -1;
     for (int i = 0; i < kSlots; ++i)
-        if (c_nu[i] == nu) {
-            *e0 = c_e0[i];
-            *noct = c_noct[i];
-            return *noct <= NNGP_MT_MAX_OCT;
-        }
-    CovParams p = nngp_cov_params_nu(NNGP_KIND_MATERN, 1.0, 1.0, 0.0, nu);
-    nngp_matern_table_setup(p);
-    c_nu[c_next] = nu;
-    c_e0[c_next] = *e0 = p.mt_e0;
-    c_noct[c_next] = *noct = p.mt_noct;
-    c_next = (c_next + 1) % kSlots;
-    return *noct <= NNGP_MT_MAX_OCT;
+        if (c_nu[i] == nu) hit = i;
+    if (hit < 0) {
+        CovParams q = nngp_cov_params_nu(NNGP_KIND_MATERN, 1.0, 1.0, 0.0, nu);
+        nngp_matern_table_setup(q);
+        hit = c_next;
+        c_nu[hit] = nu;
+        c_p[hit] = q;
+        c_next = (c_next + 1) % kSlots;
+    }
+    p->mt_e0 = c_p[hit].mt_e0;
+    p->mt_noct = c_p[hit].mt_noct;
+    p->mt_series = c_p[hit].mt_series;
+    p->mt_A = c_p[hit].mt_A;
+    return p->mt_noct <= NNGP_MT_MAX_OCT;
+}
+
+bool matern_table_extent(double nu, int* e0, int* noct) {
+    CovParams p{};
+    const bool ok = matern_table_params(nu, &p);
+    *e0 = p.mt_e0;
+    *noct = p.mt_noct;
+    return ok;
 }
 
 }  // namespace nngp

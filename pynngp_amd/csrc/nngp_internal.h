@@ -128,6 +128,7 @@ bool bf_group_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCK
 bool bf_group_blocks_supported(int m);
 hipError_t matern_table_launch(const CovParams& P, double* tab, hipStream_t s);  // matern_table.hip
 bool matern_table_extent(double nu, int* e0, int* noct);  // false: more than NNGP_MT_MAX_OCT octaves
+bool matern_table_params(double nu, CovParams* p);        // ... and the below-table series (mt_series, mt_A)
 hipError_t matern_eval_launch(const double* u, int64_t n, double nu, double* out, hipStream_t s);
 hipError_t joint_dist_launch(const double* coords, int64_t n_points, int dim, const double* qcoords,
                              const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int64_t i0, double* dist,

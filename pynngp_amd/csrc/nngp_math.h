@@ -96,6 +96,10 @@ struct CovParams {
     // the table's first octave exponent and octave count
     double mphi2;
     int mt_e0, mt_noct;
+    // ... below the table (t < 2^mt_e0) when the octaves from 1 - rho < eps would not fit (nu < ~0.45):
+    // rho = 1 - mt_A t^nu (mt_series = 1), else rho = 1 there
+    double mt_A;
+    int mt_series;
 };
 
 NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double tau2) {
@@ -130,6 +134,10 @@ NNGP_HD CovParams nngp_cov_params(int kind, double sigma2, double phi, double ta
     p.gauss = kind == NNGP_KIND_GAUSSIAN;
     p.nu = p.mu = p.mg1 = p.mg2 = p.mgp = p.mgm = p.mfac = p.mscale = 0.0;
     p.mnl = 0;
+    p.mphi2 = 0.0;
+    p.mt_e0 = p.mt_noct = 0;
+    p.mt_A = 0.0;
+    p.mt_series = 0;
     return p;
 }
 
@@ -280,7 +288,8 @@ NNGP_HD double nngp_matern_rho(const CovParams& P, double u) {
 // mpmath (nu = 0.5 .. 50, 4 bins per octave, degree 13): <= 1.2e-17 absolute; the table inherits the
 // accuracy of nngp_matern_rho (<= 1.3e-15 absolute).  Per covariance: 11 VALU for the index and the
 // local variable, 13 FMAs, NNGP_MT_NC / 2 LDS reads of 16 B.  The octaves from 1 - rho < eps to
-// rho < eps fit NNGP_MT_MAX_OCT for nu >= NNGP_MT_NU_MIN; smaller nu stay on the wavefront kernel.
+// rho < eps fit NNGP_MT_MAX_OCT for nu >= NNGP_MT_NU_MIN; smaller nu start the table at 2^-64 and take
+// the small-t expansion below it (NNGP_MT_SERIES_E): every nu in (0, 50] runs on the pair kernel.
 #define NNGP_MT_K 4
 #define NNGP_MT_NC 14
 #define NNGP_MT_MAX_OCT 160
@@ -299,6 +308,24 @@ NNGP_HD double nngp_matern_small_bound(double nu, double t) {
     return 2.0 * b;
 }
 
+// Below the table.  For small nu the octaves down to 1 - rho < eps are too many (rho = 1 - A t^nu + ...
+// reaches 1 - 1e-18 only at t ~ 1e-18^(1/nu): ~200 octaves at nu = 0.3), so from NNGP_MT_SERIES_E down
+// the kernel uses the expansion (u = sqrt t; u^nu K_nu(u) through I_{-nu} and I_nu):
+//   rho = 1 + t / (4 (1 - nu)) - A t^nu (1 + t / (4 (1 + nu))) + O(t^2),  A = Gamma(1 - nu) / (4^nu Gamma(1 + nu)),
+// where below t = 2^-64 every term but 1 - A t^nu is under 1e-19: rho = 1 - A t^nu (one pow per such
+// covariance -- near-coincident points, phi d < 2^-32 -- on a branch the other lanes skip).
+#define NNGP_MT_SERIES_E (-64)
+// 1 - A t^nu below the table: a real call on the GPU (ocml's pow would otherwise be inlined at each of a
+// fully unrolled kernel's hundreds of covariance sites -- 4x the code -- for a branch that near-coincident
+// points alone take)
+#ifdef NNGP_MATH_HOST
+static inline double nngp_matern_below(double A, double t, double nu) { return fma(-A, pow(t, nu), 1.0); }
+#else
+__device__ __attribute__((noinline)) static double nngp_matern_below(double A, double t, double nu) {
+    return fma(-A, pow(t, nu), 1.0);
+}
+#endif
+
 // table extent for P (nngp_matern_setup done): returns false when it would exceed NNGP_MT_MAX_OCT
 NNGP_HD bool nngp_matern_table_setup(CovParams& p) {
     p.mphi2 = p.phi * p.phi;
@@ -306,6 +333,13 @@ NNGP_HD bool nngp_matern_table_setup(CovParams& p) {
     while (ez < 1100 && !(nngp_matern_rho(p, sqrt(ldexp(1.0, ez))) < NNGP_MT_EPS)) ++ez;
     int e0 = 0;  // largest E <= 0 with the small-t bound below eps at 2^E (the bound increases with t)
     while (e0 > -1074 && !(nngp_matern_small_bound(p.nu, ldexp(1.0, e0)) < NNGP_MT_EPS)) --e0;
+    p.mt_series = 0;
+    p.mt_A = 0.0;
+    if (ez - e0 + 2 > NNGP_MT_MAX_OCT && p.nu < 0.9 && e0 < NNGP_MT_SERIES_E) {
+        e0 = NNGP_MT_SERIES_E;  // the series serves t < 2^e0
+        p.mt_series = 1;
+        p.mt_A = tgamma(1.0 - p.nu) / (pow(4.0, p.nu) * tgamma(1.0 + p.nu));
+    }
     p.mt_e0 = e0;
     p.mt_noct = ez - e0 + 2;
     return p.mt_noct <= NNGP_MT_MAX_OCT;
@@ -382,6 +416,7 @@ NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2)
     const double f = __builtin_amdgcn_fract(s);
 #endif
     const int j = (int)s - NNGP_MT_K;
+    if (P.mt_series && ex <= P.mt_e0) return nngp_matern_below(P.mt_A, t, P.nu);  // below the table (rare)
     int o = ex - P.mt_e0;
     o = o < 0 ? 0 : (o > P.mt_noct - 1 ? P.mt_noct - 1 : o);
     const double* c = tab + (o * NNGP_MT_K + j) * NNGP_MT_NC;

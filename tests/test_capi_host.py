@@ -103,9 +103,8 @@ def _sweep(lib, **kw):
     (dict(kind=5, nu=0.0), -1, "nu"),  # general-smoothness Matern: 0 < nu <= 50
     (dict(kind=5, nu=50.5), -1, "nu"),
     (dict(kind=5, nu=float("nan")), -1, "nu"),
-    (dict(kind=5, nu=0.3, algo=5), -4, "table octaves"),  # the pair kernel's Matern table: nu >= ~0.45
-    (dict(kind=5, nu=1.2, algo=1, m=8), -4, "pair kernel (m <= 24) or the wavefront kernel"),
-    (dict(kind=5, nu=1.2, algo=4, m=28), -4, "pair kernel (m <= 24) or the wavefront kernel"),
+    (dict(kind=5, nu=1.2, algo=1, m=8), -4, "pair (m <= 24), four-lane (25..32) or wavefront kernel"),
+    (dict(kind=5, nu=0.3, algo=1, m=8), -4, "pair (m <= 24), four-lane (25..32) or wavefront kernel"),
 ])
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code
@@ -168,24 +167,19 @@ def test_check_partials_codes(lib):
 
 def test_resolve_algo_table(lib):
     """auto: the blocked pair kernel for 1 <= m <= 24 and the four-lane kernel for 25..32 at kinds
-    0..4 and every dimension, the wavefront kernel above; the general-smoothness Matern kind (5): the
-    pair kernel with its table for m <= 24 when nu's table fits (nu >= ~0.45), else and above m = 24
-    the wavefront kernel; explicit codes pass through."""
+    0..4 and every dimension, the wavefront kernel above; the general-smoothness Matern kind (5) the same
+    for every nu in (0, 50] (since round 5 the launch's table serves small nu too: below t = 2^-64 the
+    small-t expansion 1 - A t^nu); explicit codes pass through."""
     for m in (1, 15, 20, 24, 25, 32):
-        for kind in range(5):
+        for kind in range(6):
             for dim in (1, 2, 3):
                 assert lib.nngp_resolve_algo(0, m, kind, dim) == (5 if m <= 24 else 4)
     assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
     assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
     assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1
-    for m in (1, 15, 24):
-        assert lib.nngp_resolve_algo(0, m, 5, 2) == 5
-        for nu in (0.45, 0.5, 1.0, 2.5, 49.0):
-            assert lib.nngp_resolve_algo_nu(0, m, 5, 2, nu) == 5
-        for nu in (0.05, 0.3, 0.4):
-            assert lib.nngp_resolve_algo_nu(0, m, 5, 2, nu) == 2
-    for m in (25, 40):
-        assert lib.nngp_resolve_algo(0, m, 5, 2) == 2 and lib.nngp_resolve_algo_nu(0, m, 5, 2, 1.5) == 2
+    for m in (1, 15, 24, 25, 32, 33, 40):
+        for nu in (0.01, 0.05, 0.3, 0.44, 0.45, 0.5, 1.0, 2.5, 49.0, 50.0):
+            assert lib.nngp_resolve_algo_nu(0, m, 5, 2, nu) == (5 if m <= 24 else 4 if m <= 32 else 2), (m, nu)
     assert lib.nngp_resolve_algo_nu(2, 15, 5, 2, 1.5) == 2 and lib.nngp_resolve_algo_nu(0, 15, 0, 2, 1.5) == 5
 
 

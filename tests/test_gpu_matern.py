@@ -1,6 +1,7 @@
-"""GPU parity: the general-smoothness Matern kind (NNGP_COV_MATERN): the pair kernel evaluating rho
-from the launch's table (m <= 24, nu >= ~0.45, `auto`) and the wavefront kernel's direct Bessel
-evaluation (smaller nu, m > 24, or algo="wave").
+"""GPU parity: the general-smoothness Matern kind (NNGP_COV_MATERN): the pair kernel (m <= 24) and the
+four-lane kernel (m = 25..32) evaluating rho from the launch's table for every nu in (0, 50] (below
+t = 2^-64 the small-t expansion 1 - A t^nu when nu < 0.9 would need more than 160 octaves), and the
+wavefront kernel's direct Bessel evaluation (m > 32, or algo="wave").
 
 Against the C oracle (oracle/nngp_oracle.c: K_nu by a long-double trapezoidal integral, a method
 independent of the kernel's Temme series / continued fraction) on the same neighbour sets, with
@@ -60,7 +61,12 @@ def _check(dev, lib, O, coords, nbr, theta, nu, y, algo="auto"):
     (1.3, (1.0, 10.0, 0.1), 15, 3),
     (2.2, (1.0, 18.0, 0.1), 40, 2),  # the NR = 64 instantiation
     (11.0, (1.0, 60.0, 0.3), 5, 2),
-    (0.45, (1.0, 15.0, 0.05), 15, 2),  # the smallest nu whose table fits
+    (0.45, (1.0, 15.0, 0.05), 15, 2),
+    (0.05, (1.0, 10.0, 0.1), 15, 2),  # small nu: the table from 2^-64 (round 5; the wavefront kernel before)
+    (0.2, (1.0, 30.0, 0.05), 24, 2),
+    (0.3, (1.0, 20.0, 0.1), 28, 2),  # m = 25..32: the four-lane kernel with the table
+    (1.7, (1.0, 12.0, 0.1), 32, 3),
+    (6.0, (1.0, 40.0, 0.1), 26, 1),
     (35.0, (1.0, 80.0, 0.1), 20, 2),
     (1.0, (1.0, 12.0, 0.1), 24, 3),
 ])
@@ -83,28 +89,28 @@ def test_matern_large_phi_padding_rows(lib, dev, c_oracle, m, phi, nu):
 
 
 def test_matern_deferred_finalize_wrong_algo(lib, dev, c_oracle):
-    """advice r04: a deferred sweep with nu below the table (the wavefront kernel ran) finalised as the pair
-    kernel's records: the fold refuses the foreign header (NaN partials), never reads past the workspace;
-    with nngp_resolve_algo_nu's answer it is the in-line fold's result"""
+    """advice r04: a deferred sweep on the wavefront kernel finalised as the pair kernel's records: the fold
+    refuses the foreign header (NaN partials), never reads past the workspace; with the algo that ran it is
+    the in-line fold's result"""
     coords, y = _field(3000, 77)
     nbr = torch.from_numpy(c_oracle.c_knn_prior(coords, 15)).to(dev)
     c, v = torch.from_numpy(coords).to(dev), torch.from_numpy(y).to(dev)
     ws = lib.bf_workspace(3000, 15, "auto", dev, kind="matern")
-    lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3, workspace=ws, defer=True)
+    lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3, workspace=ws, defer=True, algo="wave")
     bad = lib.bf_finalize(ws, 3000, 15, "matern", 2, algo="pairb").cpu().numpy()
     assert np.isnan(bad[0]) and np.isnan(bad[1])
-    good = lib.bf_finalize(ws, 3000, 15, "matern", 2, algo=lib.resolve_algo("auto", 15, "matern", 2, nu=0.3))
-    _, _, ref = lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3)
+    good = lib.bf_finalize(ws, 3000, 15, "matern", 2, algo="wave")
+    _, _, ref = lib.bf_sweep(c, nbr, 0, "matern", 1.0, 20.0, 0.1, values=v, nu=0.3, algo="wave")
     assert torch.equal(good, ref)
 
 
 def test_matern_kernel_choice_and_explicit(lib, dev):
-    """auto: the pair kernel with the table for m <= 24 and nu >= ~0.45, the wavefront kernel for smaller
-    nu and m > 24; the two kernels agree within the parity tolerances; lane / an uncovered nu on the pair
-    kernel are refused."""
-    assert lib.resolve_algo("auto", 15, "matern", 2, nu=1.2) == "pairb"
-    assert lib.resolve_algo("auto", 15, "matern", 2, nu=0.3) == "wave"
-    assert lib.resolve_algo("auto", 40, "matern", 2, nu=1.2) == "wave"
+    """auto: the pair kernel with the table for m <= 24, the four-lane kernel with it for 25..32 (every nu),
+    the wavefront kernel above; the kernels agree within the parity tolerances; lane is refused."""
+    for nu in (0.05, 0.3, 1.2, 49.0):
+        assert lib.resolve_algo("auto", 15, "matern", 2, nu=nu) == "pairb"
+        assert lib.resolve_algo("auto", 28, "matern", 2, nu=nu) == "quad"
+        assert lib.resolve_algo("auto", 40, "matern", 2, nu=nu) == "wave"
     coords, y = _field(5000, 2)
     c = torch.from_numpy(coords).to(dev)
     v = torch.from_numpy(y).to(dev)
@@ -117,21 +123,24 @@ def test_matern_kernel_choice_and_explicit(lib, dev):
     assert abs(pa[1].item() - pw[1].item()) <= 1e-11 * abs(pw[1].item())
     with pytest.raises(lib.NNGPExtensionError, match="pair kernel"):
         lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=1.2, algo="lane")
-    with pytest.raises(lib.NNGPExtensionError, match="table octaves"):
-        lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1, nu=0.3, algo="pairb")
+    nb28 = lib.knn_prior(c, 28)
+    Bq, Fq, pq = lib.bf_sweep(c, nb28, 0, "matern", 1.0, 10.0, 0.1, values=v, nu=0.3)
+    Bw, Fw, pw = lib.bf_sweep(c, nb28, 0, "matern", 1.0, 10.0, 0.1, values=v, nu=0.3, algo="wave")
+    assert torch.all((Fq - Fw).abs() <= RTOL_F * Fw) and torch.all((Bq - Bw).abs() <= ATOL_B * (1 + Bw.abs()))
+    assert abs(pq[1].item() - pw[1].item()) <= 1e-11 * abs(pw[1].item())
     with pytest.raises(ValueError, match="nu"):
         lib.bf_sweep(c, nb, 0, "matern", 1.0, 10.0, 0.1)
 
 
 def test_matern_m1_covariance_vs_mpmath(lib, dev, c_oracle):
-    """m = 1 isolates the device covariance: B_i = C(d_i) / (sigma2 + tau2)."""
+    """m = 1 isolates the device covariance: B_i = C(d_i) / (sigma2 + tau2) (auto: through the table)."""
     coords, _ = _field(4000, 7)
     nbr = c_oracle.c_knn_prior(coords, 1)
     sigma2, phi, tau2 = 1.3, 9.0, 0.4
     c = torch.from_numpy(coords).to(dev)
     mp.mp.dps = 40
-    for nu, algo in ((0.4, "auto"), (0.6, "auto"), (1.0, "auto"), (2.3, "auto"), (7.5, "auto"), (42.0, "auto"),
-                     (1.0, "wave"), (7.5, "wave")):  # 0.4: the wavefront kernel; the others through the table
+    for nu, algo in ((0.05, "auto"), (0.2, "auto"), (0.4, "auto"), (0.6, "auto"), (1.0, "auto"), (2.3, "auto"),
+                     (7.5, "auto"), (42.0, "auto"), (0.2, "wave"), (1.0, "wave"), (7.5, "wave")):
         B, _, p = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", sigma2, phi, tau2, nu=nu, algo=algo)
         cov = B.cpu().numpy()[1:, 0] * (sigma2 + tau2)
         j = nbr[1:, 0]
@@ -140,6 +149,35 @@ def test_matern_m1_covariance_vs_mpmath(lib, dev, c_oracle):
             u = phi * mp.sqrt(mp.mpf(float(d2[k])))
             ref = sigma2 * u ** nu * mp.besselk(nu, u) / (mp.mpf(2) ** (nu - 1) * mp.gamma(nu))
             assert abs(cov[k] - float(ref)) <= 4e-15 * sigma2, (nu, k, cov[k], float(ref))
+
+
+@pytest.mark.parametrize("nu", [0.05, 0.2, 0.4])
+def test_matern_small_nu_near_coincident_points(lib, dev, nu):
+    """Small nu below the table: points 1e-30 .. 1e-9 apart (t < 2^-64 with phi = 9) and exact duplicates
+    take rho = 1 - A t^nu; the covariance against mpmath (m = 1), the pair and four-lane kernels."""
+    rng = np.random.default_rng(40)
+    base = rng.uniform(0, 1, (500, 2))
+    off = rng.standard_normal((500, 2)) * (10.0 ** rng.uniform(-30, -9, 500))[:, None]
+    off[::50] = 0.0  # exact duplicates
+    coords = np.empty((1000, 2))
+    coords[0::2], coords[1::2] = base, base + off
+    nbr = np.full((1000, 1), -1, np.int32)
+    nbr[1::2, 0] = np.arange(0, 1000, 2)
+    nbr[2::2, 0] = np.arange(1, 999, 2)  # the previous pair's second point (an ordinary distance)
+    sigma2, phi, tau2 = 1.0, 9.0, 0.5
+    c = torch.from_numpy(coords).to(dev)
+    B, _, _ = lib.bf_sweep(c, torch.from_numpy(nbr).to(dev), 0, "matern", sigma2, phi, tau2, nu=nu)
+    cov = B.cpu().numpy()[:, 0] * (sigma2 + tau2)
+    mp.mp.dps = 50
+    for i in range(1, 1000):
+        j = nbr[i, 0]
+        d = mp.sqrt(mp.mpf(float(coords[i, 0] - coords[j, 0])) ** 2 + mp.mpf(float(coords[i, 1] - coords[j, 1])) ** 2)
+        if d == 0:
+            ref = mp.mpf(sigma2)
+        else:
+            u = phi * d
+            ref = sigma2 * u ** nu * mp.besselk(nu, u) / (mp.mpf(2) ** (nu - 1) * mp.gamma(nu))
+        assert abs(cov[i] - float(ref)) <= 4e-15 * sigma2, (nu, i, cov[i], float(ref))
 
 
 @pytest.mark.parametrize("nu,kind", [(0.5, "exponential"), (1.5, "matern32"), (2.5, "matern52")])

@@ -103,7 +103,7 @@ def table_rho(tmp_path_factory):
     return run
 
 
-TABLE_NUS = tuple(nu for nu in NUS if nu >= 0.45) + (0.45, 1.0000001, 1.97, 2.0, 3.0)
+TABLE_NUS = tuple(NUS) + (0.45, 1.0000001, 1.97, 2.0, 3.0, 0.05, 0.2, 0.3, 0.44)
 
 
 def test_table_rho_vs_mpmath(table_rho):
@@ -127,12 +127,30 @@ def test_table_rho_limits_and_range(table_rho):
     got, noct = table_rho([(1.3, 0.0), (1.3, 1e-200), (1.3, 1e6), (0.7, 0.0), (0.7, 5e3), (0.3, 1.0), (0.05, 1.0),
                            (1.3, 1e160), (0.7, 1e300), (49.0, 1e200)])
     assert got[0] == 1.0 and got[1] == 1.0 and got[2] == 0.0 and got[3] == 1.0 and got[4] == 0.0
-    assert np.isnan(got[5]) and np.isnan(got[6]) and noct[5] == 0
+    # round 5: small nu has a table too (from t = 2^-64 up; the small-t expansion below it)
+    assert 0 < noct[5] <= 160 and 0 < noct[6] <= 160
+    assert abs(got[5] - float(_ref(0.3, 1.0))) <= 2e-15 and abs(got[6] - float(_ref(0.05, 1.0))) <= 2e-15
     # u^2 past the double range (a padding point at (m + 1) 1e150 with a large phi): exactly 0, not NaN
     assert got[7] == 0.0 and got[8] == 0.0 and got[9] == 0.0
     us = np.linspace(0.001, 30.0, 400).tolist()
     r, _ = table_rho([(2.2, u) for u in us])
     assert all(a > b for a, b in zip(r, r[1:]))
+
+
+def test_table_small_nu_below_the_table(table_rho):
+    """nu < ~0.45: the table starts at t = 2^-64 and rho = 1 - A t^nu below it (A = Gamma(1 - nu) /
+    (4^nu Gamma(1 + nu)); the t and t^(1+nu) terms are under 1e-19 there) -- against mpmath from the
+    table's start down to coincident points (u = 0 gives exactly 1)."""
+    worst = 0.0
+    for nu in (0.02, 0.05, 0.1, 0.2, 0.3, 0.4, 0.44):
+        us = [2.0 ** -e for e in (31, 32, 33, 40, 60, 100, 200, 400)] + [2.0 ** -31.9, 1e-12, 1e-100]
+        got, noct = table_rho([(nu, u) for u in us] + [(nu, 0.0)])
+        assert all(0 < k <= 160 for k in noct)
+        # u = 0 is the kernels' floor d^2 = 2^-1000 (coincident points): rho(2^-500), 1 - A 2^(-1000 nu)
+        assert abs(got[-1] - float(_ref(nu, 2.0 ** -500))) <= 2e-15
+        for u, g in zip(us, got):
+            worst = max(worst, float(abs(g - _ref(nu, u))))
+    assert worst <= 2e-15, worst
 
 
 def test_c_oracle_rho_vs_mpmath(c_oracle):

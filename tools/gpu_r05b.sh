@@ -7,7 +7,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 o=gpurun_out/r05b
 mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests/test_gpu_plan.py tests/test_gpu_gibbs_chains.py tests/test_gpu_callable_cov.py \
-  tests/test_gpu_matern.py tests/test_gpu_api.py tests/test_gpu_gibbs.py -x -v --timeout 120 --timeout-method thread \
+  tests/test_gpu_matern.py tests/test_gpu_api.py tests/test_gpu_gibbs.py tests/test_gpu_gibbs_sharded.py -x -v --timeout 120 --timeout-method thread \
   > $o/pytest_new.txt 2>&1 || { tail -60 $o/pytest_new.txt; exit 1; }
 tail -3 $o/pytest_new.txt
 for r in 1 2; do
@@ -30,3 +30,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 
   > $o/prof.log 2>&1 || exit 1
 find $o/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $o/kernel_stats_plan.csv
 head -8 $o/kernel_stats_plan.csv
+timeout -k 10 300 python tools/bench_shard_plan.py --gpu --n 10000000 --out $o/shard_plan_gpu.json > $o/shard_plan.log 2>&1 || { tail -20 $o/shard_plan.log; exit 1; }
+tail -1 $o/shard_plan.log
