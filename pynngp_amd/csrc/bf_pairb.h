@@ -463,10 +463,21 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                         : M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W
                                                               : NNGP_PAIRB_LEFT_LDS_ROWS;
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
-    __shared__ double lrow[KL > 0 ? KL * (KL + 1) : 1][KL > 0 ? kPairbThreads : 1];
+    // the left-looking kernel's LDS in one object: the exp table first (its reads fold the base into the
+    // 16-bit offset field; the LDS lowering sorts separate objects by size, which put it above 64 KB), the
+    // finished factor rows, then the late state -- the neighbour indices (its values are gathered late),
+    // the row, the bad-index flag: held in registers through its factorisation they spilled 13 dwords per
+    // lane to scratch, written once and reloaded at the end (+95 B of HBM writes per location at m = 20,
+    // profiles/r04e)
+    constexpr int LXW = (NP + 3 + 1) / 2;  // doubles per thread of the late state
+    __shared__ double lbuf[LEFT ? NNGP_EXP_TAB_N + (KL * (KL + 1) + LXW) * kPairbThreads : 1];
+    double(*const lrow)[kPairbThreads] = (double(*)[kPairbThreads])(lbuf + NNGP_EXP_TAB_N);
+    int32_t(*const lidx)[kPairbThreads] =
+        (int32_t(*)[kPairbThreads])(lbuf + NNGP_EXP_TAB_N + KL * (KL + 1) * kPairbThreads);
     constexpr bool ZLDS = NOZ && M >= NNGP_PAIRB_ZLDS_MIN;
     __shared__ double zsh[ZLDS ? NP : 1][ZLDS ? kPairbThreads : 1];
-    __shared__ double etab[MT ? 1 : NNGP_EXP_TAB_N];
+    __shared__ double etab_own[MT || LEFT ? 1 : NNGP_EXP_TAB_N];
+    double* const etab = LEFT ? lbuf : etab_own;
     extern __shared__ double4 pairb_mtab[];  // MT: the Matern table (dynamic LDS, NNGP_MT_BYTES(noct))
     const double* ctab = MT ? (const double*)pairb_mtab : etab;  // the covariance evaluation's table
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
@@ -539,6 +550,13 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             for (int s = 0; s < NP; ++s) zsh[s][threadIdx.x] = z[s];  // read back by this thread only
         }
         const bool bad_index = (int64_t)jmax >= n_points || jmin < -1;
+        if constexpr (LEFT) {  // the late state waits in LDS (read back by this thread only)
+#pragma unroll
+            for (int s = 0; s < NP; ++s) lidx[s][threadIdx.x] = jn[s];
+            lidx[NP][threadIdx.x] = (int32_t)(uint32_t)(uint64_t)rr;
+            lidx[NP + 1][threadIdx.x] = (int32_t)(uint32_t)((uint64_t)rr >> 32);
+            lidx[NP + 2][threadIdx.x] = bad_index ? 1 : 0;
+        }
         const uint8_t* pslot = PL ? pp.slots + tile * pp.slot_bytes : nullptr;
         double badi_plan = INFINITY;
 
@@ -977,6 +995,15 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         };
         bad |= !(Fu > 0.0);
         const double F = Fu * sigma2;  // the unit-variance pivot scaled back
+        int64_t rrl = rr, il = i;
+        bool bidx = bad_index;
+        if constexpr (LEFT) {
+            // (the fence keeps the compiler from forwarding the stores' registers past the factorisation)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            rrl = (int64_t)(((uint64_t)(uint32_t)lidx[NP + 1][threadIdx.x] << 32) | (uint32_t)lidx[NP][threadIdx.x]);
+            il = i0 + rrl;
+            bidx = lidx[NP + 2][threadIdx.x] != 0;
+        }
 
         if (NOZ || Bout != nullptr) {
             // B = L_N^{-T} v, v = row M of L (lane M % 2, local row M / 2).  Lane q ends with
@@ -991,9 +1018,9 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 #pragma unroll
                 for (int s = 0; s < NP; ++s) {
                     const int a = 2 * s + q;
-                    const int32_t j = a < M ? nbr[rl * M + a] : -1;
+                    const int32_t j = a < M ? lidx[s][threadIdx.x] : -1;
                     const bool in_range = (uint32_t)j < n32;
-                    const double* pv = a == M ? (qvalues != nullptr ? qvalues + i : kZeroValue)
+                    const double* pv = a == M ? (qvalues != nullptr ? qvalues + il : kZeroValue)
                                               : ((values != nullptr && in_range) ? values + j : kZeroValue);
                     z[s] = *pv;
                 }
@@ -1058,19 +1085,19 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 #pragma unroll
                 for (int s = 0; s < NP; ++s) {
                     const int a = 2 * s + q;
-                    if (a < M) Bout[rr * M + a] = bown[s] * bscale;
+                    if (a < M) Bout[rrl * M + a] = bown[s] * bscale;
                 }
             }
         }
         NNGP_PHASE(tail);
         const bool lead = live && lead0;
-        if (Fout != nullptr && lead) Fout[rr] = bad ? NAN : F;
-        if (Rout != nullptr && lead) Rout[rr] = bad ? NAN : res;
+        if (Fout != nullptr && lead) Fout[rrl] = bad ? NAN : F;
+        if (Rout != nullptr && lead) Rout[rrl] = bad ? NAN : res;
         // this lane's terms of the tile record (lead lanes; a NaN F -- a bad pivot -- propagates
         // into the mantissa product as log(NaN) would; the flag is what callers check)
         pairb_tile_store(lead ? __builtin_amdgcn_frexp_mant(F) : 1.0, lead ? __builtin_amdgcn_frexp_exp(F) : 0,
-                         lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)i : INFINITY,
-                         PL ? badi_plan : ((live && bad_index) ? (double)i : INFINITY), sh, 0, rec, lexp, tile);
+                         lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)il : INFINITY,
+                         PL ? badi_plan : ((live && bidx) ? (double)il : INFINITY), sh, 0, rec, lexp, tile);
         __syncthreads();
         if (fused == nullptr) {
             if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
