@@ -335,7 +335,9 @@ NNGP_HD bool nngp_matern_table_setup(CovParams& p) {
     while (e0 > -1074 && !(nngp_matern_small_bound(p.nu, ldexp(1.0, e0)) < NNGP_MT_EPS)) --e0;
     p.mt_series = 0;
     p.mt_A = 0.0;
-    if (ez - e0 + 2 > NNGP_MT_MAX_OCT && p.nu < 0.9 && e0 < NNGP_MT_SERIES_E) {
+    // (every nu < 0.9 whose table would reach below 2^-64, not only those past NNGP_MT_MAX_OCT: ~45 fewer
+    // octaves at nu = 0.5 -- 25 KB less LDS per block, the occupancy advice r04 asked about)
+    if (p.nu < 0.9 && e0 < NNGP_MT_SERIES_E) {
         e0 = NNGP_MT_SERIES_E;  // the series serves t < 2^e0
         p.mt_series = 1;
         p.mt_A = tgamma(1.0 - p.nu) / (pow(4.0, p.nu) * tgamma(1.0 + p.nu));
