@@ -583,9 +583,14 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             // overlap the staging below), then the points, the distinct pairs, the joint block from LDS
             constexpr int CHE = plan_map_chunks(M), CHL = plan_loc_chunks(M);
             // (block-uniform: scalar loads and branches)
-            const int nU = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[0]);
-            const int nE = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[1]);
-            badi_plan = threadIdx.x == 0 ? ((const double*)pslot)[1] : INFINITY;  // the region's first bad location
+            const int nU0 = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[0]);
+            const int nE0 = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[1]);
+            // a region past this kernel's caps (a foreign or damaged plan) stays inside LDS and comes out NaN
+            const bool over = nU0 < 0 || nU0 > PU - 1 || nE0 < 0 || nE0 > PE - 1;
+            const int nU = over ? 0 : nU0, nE = over ? 0 : nE0;
+            bad = over;
+            // the region's first bad location
+            badi_plan = threadIdx.x == 0 ? *(const double*)(pslot + kPlanHdrBadOff) : INFINITY;
             // the slot through a buffer descriptor (uniform base, per-lane voffset, per-load soffset: no
             // 64-bit address arithmetic per load)
             const __amdgpu_buffer_rsrc_t srd =

@@ -27,7 +27,9 @@ namespace nngp {
 constexpr int kPlanThreads = 256;        // = kPairbThreads (bf_pairb.h): 128 locations per tile
 constexpr int kPlanUMax = 512;           // LDS point slots (slot 0 = no point): nU <= 511
 constexpr int kPlanEMax = 8192;          // LDS covariance slots (slot 0 = exact zero): nE <= 8191
-constexpr int kPlanHdrBytes = 64;        // int32 nU, nE, status; double first bad-index location (or +inf)
+constexpr int kPlanHdrBytes = 64;        // int32 nU, nE, status (bytes 0..11); double at kPlanHdrBadOff
+constexpr int kPlanHdrBadOff = 16;       // the region's first bad-index location (or +inf): clear of the status
+                                         // word (at byte 8 its low half overwrote it: direct regions read as planned)
 constexpr int kPlanUOff = kPlanHdrBytes;                     // int32 U list
 constexpr int kPlanPairOff = kPlanUOff + 4 * kPlanUMax;      // uint32 pair words u_a | u_b << 16
 constexpr int kPlanMapOff = kPlanPairOff + 4 * kPlanEMax;    // uint4 chunks, chunk-major over the threads

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
             hdr[0] = nU;
             hdr[1] = -1;
             hdr[2] = 1;
-            ((double*)slot)[1] = badr;
+            *(double*)(slot + kPlanHdrBadOff) = badr;
         }
         return;
     }
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
             hdr[0] = nU;
             hdr[1] = nE;
             hdr[2] = 1;
-            ((double*)slot)[1] = badr;
+            *(double*)(slot + kPlanHdrBadOff) = badr;
         }
         return;
     }
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
         hdr[0] = nU;
         hdr[1] = nE;
         hdr[2] = 0;
-        ((double*)slot)[1] = badr;
+        *(double*)(slot + kPlanHdrBadOff) = badr;
     }
 }
 
