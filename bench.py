@@ -444,7 +444,7 @@ def main():
                          "of one chain per GPU")
     ap.add_argument("--plan", default="auto", choices=["auto", "on", "off"],
                     help="tile pair plans (shared covariances evaluated once per tile; built with the neighbour "
-                         "sets, outside the timed region): auto = wherever they serve the sweep")
+                         "sets, outside the timed region): auto = sweep.PLAN_DEFAULT (off: measured slower, DESIGN.md 4.1b)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
     args = ap.parse_args()

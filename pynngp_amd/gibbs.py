@@ -106,7 +106,9 @@ class SeqNNGP:
     nngp.py:45-47: the uniform 5-NN mean of the observed responses at every node).
     """
 
-    _use_plan = True  # the whole-field phi sweeps through a tile pair plan (the sharded chain sweeps shards)
+    # the whole-field phi sweeps through a tile pair plan?  Off: slower than the unplanned kernel
+    # (sweep.PLAN_DEFAULT, profiles/r05f); set True on an instance's class to opt in
+    _use_plan = False
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
@@ -715,8 +717,6 @@ class SeqNNGPChains:
         if "seed" in kw:
             raise ValueError("give the chains' seeds as seeds=[...]")
         first = SeqNNGP(coords, y, X, seed=seeds[0], **kw)
-        if type(first)._use_plan is False:
-            raise ValueError("SeqNNGPChains runs SeqNNGP chains")
         self.chains = [first] + [first.clone(s) for s in seeds[1:]]
 
     def __len__(self):

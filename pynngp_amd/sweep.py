@@ -27,8 +27,11 @@ from . import _lib, ops
 from .nngp import Covariance, LOG_2PI, _raise_on_bad
 
 
-# ShardedLogLik(plan=None): sweep through a tile pair plan (pair_plan.h) whenever one serves the sweep
-PLAN_DEFAULT = True
+# ShardedLogLik(plan=None): sweep through a tile pair plan (pair_plan.h)?  Off by default: measured on the
+# same box (profiles/r05f), the planned kernel executes 28 % fewer VALU instructions at m = 15 but runs 20 %
+# longer (176.8 -> 212.2 us at N = 1e6; config 2 28.1 -> 30.2 us): its plan loads and the two barriers
+# around the shared evaluation leave the memory latency exposed at two blocks per CU.  plan=True opts in.
+PLAN_DEFAULT = False
 
 
 def shard_range(n: int, rank: int, world: int):

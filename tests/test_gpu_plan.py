@@ -167,7 +167,8 @@ def test_plan_direct_tiles(dev, lib):
     allrnd = (torch.rand((c.shape[0], 15), generator=g) * torch.arange(c.shape[0]).clamp(min=1)[:, None].double()
               ).long().to(torch.int32).to(dev)
     (a, b), plan = _both(lib, c, allrnd, "matern32", THETA["matern32"], v)
-    assert plan.n_planned == 0
+    # (the first tile's rows draw from a few hundred earlier points: it fits)
+    assert plan.n_planned <= 2 and plan.n_direct >= (c.shape[0] + 127) // 128 - 2, (plan.n_planned, plan.n_direct)
     _assert_same(a, b)
 
 

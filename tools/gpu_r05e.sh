@@ -28,7 +28,7 @@ for c in 2 4 8; do
   timeout -k 10 400 python bench.py --config 5 --chains-per-gpu $c --cpu-seconds 0 --steps 300 --warmup 50 > $o/bench_c5_$c.json 2> $o/bench_c5_$c.err; rc=$?; stop $rc bench5c
   python -c "import json; d=json.load(open('$o/bench_c5_$c.json')); print('c5 x$c', d['value'], d['ms_per_step'])" || true
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run -- python3 bench.py --plan on --cpu-seconds 0 > $o/prof.log 2>&1; rc=$?; stop $rc rocprof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof -o run -- python3 bench.py --plan on --cpu-seconds 0 > $o/prof.log 2>&1; rc=$?; stop $rc rocprof
 find $o/prof -name "*kernel_stats.csv" -exec cp {} $o/kernel_stats_plan.csv \;
 head -6 $o/kernel_stats_plan.csv
 timeout -k 10 300 python tools/bench_shard_plan.py --gpu --n 10000000 --out $o/shard_plan_gpu.json > $o/shard_plan.log 2>&1; rc=$?; stop $rc shard
