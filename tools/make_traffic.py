@@ -29,13 +29,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # preset -> (bench key fields, kernels: (role, name prefix))
 PRESETS = {
     3: ({"n_per_gpu": 1_000_000, "m": 15, "kind": "exponential", "layout": "storage", "write_BF": True},
-        [("sweep", "void nngp::bf_pairb<15, 0, 2>")]),
+        [("sweep", "void nngp::bf_pairb<15, 0, 2, false>")]),
     2: ({"n_per_gpu": 100_000, "m": 15, "kind": "matern32", "layout": "storage", "write_BF": True},
-        [("sweep", "void nngp::bf_pairb<15, 1, 2>")]),
+        [("sweep", "void nngp::bf_pairb<15, 1, 2, false>")]),
     4: ({"n_per_gpu": 10_000_000, "m": 20, "kind": "exponential", "layout": "storage", "write_BF": True},
-        [("sweep", "void nngp::bf_pairb<20, 0, 2>")]),
+        [("sweep", "void nngp::bf_pairb<20, 0, 2, false>")]),
     5: ({"preset": 5, "n_per_gpu": 1_000_000, "m": 15, "kind": "exponential"},
-        [("sweep", "void nngp::bf_pairb<15, 0, 2>"), ("colour", "void nngp::gibbs_w_color<false>")]),
+        [("sweep", "void nngp::bf_pairb<15, 0, 2, false>"), ("colour", "void nngp::gibbs_w_color<false>")]),
 }
 BYTES_PER_LOC = {3: 36 * 15 + 32, 2: 36 * 15 + 32, 4: 36 * 20 + 32, 5: 36 * 15 + 32 + 8}
 ROWS = {3: 1e6, 2: 1e5, 4: 1e7, 5: 1e6}
