@@ -548,7 +548,8 @@ def main():
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
     p = per_sweep[-1].cpu().numpy()
-    assert np.all(per_sweep.cpu().numpy() == p), "sweeps of the same field must give identical partials"
+    assert all(np.array_equal(q, p, equal_nan=True) for q in per_sweep.cpu().numpy()), \
+        "sweeps of the same field must give identical partials"
     ll = -0.5 * (n_total * np.log(2 * np.pi) + p[0] + p[1])
 
     if rank == 0:
