@@ -79,8 +79,9 @@ const char *nngp_version(void);
  * (0.1.0): nngp_bf_finalize takes workspace_bytes as its 2nd argument; nngp_gibbs_w_sweep reads
  * (n, 4) member rows (nngp_gibbs_member_rows) and lost its `off` argument; nngp_bf_sweep /
  * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32.  Revision 3
- * (library 0.3.0) adds the tile pair plans (nngp_pair_plan_*, nngp_bf_sweep_plan); nothing
- * earlier moved. */
+ * (library 0.3.0) adds the tile pair plans (nngp_pair_plan_*, nngp_bf_sweep_plan), the batched
+ * chains' sweep (nngp_gibbs_w_sweep_chains) and the device colouring (nngp_color_moral_graph_dev);
+ * NNGP_ALGO_AUTO / PAIRB / QUAD take the general Matern kind for every nu; nothing earlier moved. */
 #define NNGP_ABI_VERSION 3
 int32_t nngp_abi_version(void);
 
