@@ -80,7 +80,7 @@ const char *nngp_version(void);
  * (n, 4) member rows (nngp_gibbs_member_rows) and lost its `off` argument; nngp_bf_sweep /
  * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32.  Revision 3
  * (library 0.3.0) adds the tile pair plans (nngp_pair_plan_*, nngp_bf_sweep_plan), the batched
- * chains' sweep (nngp_gibbs_w_sweep_chains) and the device colouring (nngp_color_moral_graph_dev);
+ * chains' sweeps (nngp_gibbs_w_sweep_chains, _il) and the device colouring (nngp_color_moral_graph_dev);
  * NNGP_ALGO_AUTO / PAIRB / QUAD take the general Matern kind for every nu; nothing earlier moved. */
 #define NNGP_ABI_VERSION 3
 int32_t nngp_abi_version(void);
@@ -336,6 +336,10 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  *   phi's factors), sigma2[c], tau2[c] (host arrays), yres[c], w[c], r[c] and given normals z[c]
  *   (host arrays of device pointers) -- in ONE launch per colour; chain c's result is bit-identical
  *   to nngp_gibbs_w_sweep on its own arguments (with z given).
+ * nngp_gibbs_w_sweep_chains_il: the same with every chain's w and r interleaved in two (n, chains)
+ *   row-major arrays (chain c of location i at [i * chains + c]): a child's r_j of all chains is one
+ *   contiguous run, so the colour steps' scattered accesses move one sector for all chains; the
+ *   results are the per-chain call's, bit for bit.
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,
  *   out[2 + c] = sum_i h_i X[i, c] (y_i - w_i) for c < p (X row-major (n, p));
  *   h_i = noise_w[i], or 1 when noise_w is NULL.
@@ -381,6 +385,10 @@ int nngp_gibbs_w_sweep_chains(const int32_t *member_rows, const int32_t *color_o
                               int32_t chains, const void *const *prep, int64_t n, int32_t m, const double *sigma2,
                               const double *tau2, const double *const *yres, const double *noise_w, double *const *w,
                               double *const *r, const int32_t *rev_j, const double *const *z, void *stream);
+int nngp_gibbs_w_sweep_chains_il(const int32_t *member_rows, const int32_t *color_off_host, int32_t n_colors,
+                                 int32_t chains, const void *const *prep, int64_t n, int32_t m, const double *sigma2,
+                                 const double *tau2, const double *const *yres, const double *noise_w, double *w_il,
+                                 double *r_il, const int32_t *rev_j, const double *const *z, void *stream);
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double *z, void *stream);
 int nngp_gibbs_prepare_range(const double *B, const double *Ft, const int32_t *off, const int32_t *rev_j,
                              const int32_t *rev_k, int64_t n, int32_t m, int64_t row0, int64_t row1, void *prep,

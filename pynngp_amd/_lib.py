@@ -56,6 +56,7 @@ SYMBOLS = (
     "nngp_gibbs_stats_workspace_bytes",
     "nngp_gibbs_stats",
     "nngp_gibbs_w_sweep_chains",
+    "nngp_gibbs_w_sweep_chains_il",
     "nngp_color_moral_graph_dev",
     "nngp_pair_plan_supported",
     "nngp_pair_plan_bytes",
@@ -170,6 +171,8 @@ def load() -> ctypes.CDLL:
     lib.nngp_color_moral_graph_dev.restype = I64
     lib.nngp_gibbs_w_sweep_chains.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
     lib.nngp_gibbs_w_sweep_chains.restype = ctypes.c_int
+    lib.nngp_gibbs_w_sweep_chains_il.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
+    lib.nngp_gibbs_w_sweep_chains_il.restype = ctypes.c_int
     lib.nngp_pair_plan_supported.argtypes = [I32, I32, I32]
     lib.nngp_pair_plan_supported.restype = ctypes.c_int
     lib.nngp_pair_plan_bytes.argtypes = [I64, I32, I32]
@@ -849,30 +852,44 @@ def gibbs_w_sweep_chains(member_rows: torch.Tensor, color_off_host, preps, m: in
                          rev_j: torch.Tensor, z, noise_w: Optional[torch.Tensor] = None) -> None:
     """:func:`gibbs_w_sweep` for up to 8 independent chains of one field in ONE launch per colour
     (nngp_gibbs_w_sweep_chains): ``member_rows`` / colours / ``rev_j`` / ``noise_w`` shared, per chain
-    lists of ``preps``, ``sigma2s``, ``tau2s``, ``yres``, ``w``, ``r`` and given normals ``z``.  Chain c's
-    result is bit-identical to :func:`gibbs_w_sweep` on its own arguments with its ``z``."""
+    lists of ``preps``, ``sigma2s``, ``tau2s``, ``yres`` and given normals ``z``; ``w`` and ``r`` either
+    per-chain lists of (n,) vectors or two contiguous (n, C) tensors holding the chains interleaved
+    (nngp_gibbs_w_sweep_chains_il: one sector per scattered access for all chains).  Chain c's result is
+    bit-identical to :func:`gibbs_w_sweep` on its own arguments with its ``z``."""
     import numpy as np
 
     C = len(preps)
-    if not 1 <= C <= 8 or not all(len(v) == C for v in (sigma2s, tau2s, yres, w, r, z)):
+    il = isinstance(w, torch.Tensor)
+    if il != isinstance(r, torch.Tensor):
+        raise ValueError("w and r: both per-chain lists or both (n, C) tensors")
+    per = (sigma2s, tau2s, yres, z) if il else (sigma2s, tau2s, yres, w, r, z)
+    if not 1 <= C <= 8 or not all(len(v) == C for v in per):
         raise ValueError("1..8 chains, one entry per chain in every list")
-    n = w[0].shape[0]
-    for t in list(yres) + list(w) + list(r) + list(z):
+    n = w.shape[0] if il else w[0].shape[0]
+    if il:
+        for t in (w, r):
+            if t.dtype != torch.float64 or tuple(t.shape) != (n, C) or not t.is_contiguous():
+                raise ValueError(f"interleaved w / r must be contiguous float64 ({n}, {C})")
+    vecs = list(yres) + list(z) + ([] if il else list(w) + list(r))
+    for t in vecs:
         if t.dtype != torch.float64 or tuple(t.shape) != (n,) or not t.is_contiguous():
             raise ValueError(f"per-chain vectors must be contiguous float64 ({n},)")
     if member_rows.dtype != torch.int32 or member_rows.dim() != 2 or member_rows.shape[1] != 4 \
             or not member_rows.is_contiguous():
         raise ValueError("member_rows must be a contiguous int32 (n, 4) tensor from gibbs_member_rows")
-    dev = _require_gpu(member_rows, rev_j, noise_w, *preps, *yres, *w, *r, *z)
+    dev = _require_gpu(member_rows, rev_j, noise_w, *preps, *vecs, *((w, r) if il else ()))
     _check_noise_w(noise_w, n)
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
     P = ctypes.c_void_p * C
     D = ctypes.c_double * C
-    _check(load().nngp_gibbs_w_sweep_chains(_ptr(member_rows), co.ctypes.data, len(co) - 1, C,
-                                            P(*[_ptr(t) for t in preps]), n, int(m), D(*map(float, sigma2s)),
-                                            D(*map(float, tau2s)), P(*[_ptr(t) for t in yres]), _ptr(noise_w),
-                                            P(*[_ptr(t) for t in w]), P(*[_ptr(t) for t in r]), _ptr(rev_j),
-                                            P(*[_ptr(t) for t in z]), _stream(dev)), "nngp_gibbs_w_sweep_chains")
+    head = (_ptr(member_rows), co.ctypes.data, len(co) - 1, C, P(*[_ptr(t) for t in preps]), n, int(m),
+            D(*map(float, sigma2s)), D(*map(float, tau2s)), P(*[_ptr(t) for t in yres]), _ptr(noise_w))
+    tail = (_ptr(rev_j), P(*[_ptr(t) for t in z]), _stream(dev))
+    if il:
+        _check(load().nngp_gibbs_w_sweep_chains_il(*head, _ptr(w), _ptr(r), *tail), "nngp_gibbs_w_sweep_chains_il")
+    else:
+        _check(load().nngp_gibbs_w_sweep_chains(*head, P(*[_ptr(t) for t in w]), P(*[_ptr(t) for t in r]), *tail),
+               "nngp_gibbs_w_sweep_chains")
 
 
 def gibbs_normals(z: torch.Tensor, seed: int, sweep: int) -> torch.Tensor:

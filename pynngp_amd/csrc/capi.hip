@@ -559,6 +559,33 @@ int nngp_gibbs_w_sweep_chains(const int32_t* member_rows, const int32_t* color_o
     return NNGP_OK;
 }
 
+int nngp_gibbs_w_sweep_chains_il(const int32_t* member_rows, const int32_t* color_off_host, int32_t n_colors,
+                                 int32_t chains, const void* const* prep, int64_t n, int32_t m, const double* sigma2,
+                                 const double* tau2, const double* const* yres, const double* noise_w, double* w_il,
+                                 double* r_il, const int32_t* rev_j, const double* const* z, void* stream) {
+    if (chains < 1 || chains > 8) return fail(NNGP_EINVAL, "chains=%d outside [1, 8]", chains);
+    if (member_rows == nullptr || color_off_host == nullptr || prep == nullptr || sigma2 == nullptr ||
+        tau2 == nullptr || yres == nullptr || w_il == nullptr || r_il == nullptr || z == nullptr ||
+        (m > 0 && rev_j == nullptr))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
+    if (((uintptr_t)w_il & 7) != 0 || ((uintptr_t)r_il & 7) != 0) return fail(NNGP_EINVAL, "w_il / r_il misaligned");
+    if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
+    if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
+    for (int c = 0; c < chains; ++c) {
+        if (prep[c] == nullptr || yres[c] == nullptr || z[c] == nullptr)
+            return fail(NNGP_EINVAL, "null pointer for chain %d", c);
+        if (((uintptr_t)prep[c] & 255) != 0) return fail(NNGP_EINVAL, "prep[%d] must be 256-byte aligned", c);
+        if (!(sigma2[c] > 0.0) || !(tau2[c] > 0.0) || !isfinite(sigma2[c]) || !isfinite(tau2[c]))
+            return fail(NNGP_EINVAL, "chain %d needs sigma2 > 0 and tau2 > 0 (finite)", c);
+    }
+    hipError_t e = nngp::gibbs_w_sweep_chains_launch(member_rows, n_colors, color_off_host, chains, prep, n, m, sigma2,
+                                                     tau2, yres, noise_w, nullptr, nullptr, rev_j, z,
+                                                     (hipStream_t)stream, w_il, r_il);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep_chains_il launch");
+    return NNGP_OK;
+}
+
 int nngp_gibbs_normals(int64_t n, uint64_t seed, uint64_t sweep, double* z, void* stream) {
     if (n < 0 || (n > 0 && z == nullptr)) return fail(NNGP_EINVAL, "bad n or null z");
     hipError_t e = nngp::philox_normals_launch(n, seed, sweep, z, (hipStream_t)stream);

@@ -691,13 +691,25 @@ struct ChainPtrs {
     const double* z[kMaxChains];
     double* w[kMaxChains];
     double* r[kMaxChains];
+    double* wil;  // IL: w and r interleaved, (n, C) row-major -- chain c of location i at [i C + c]
+    double* ril;
     double it2[kMaxChains], is2[kMaxChains];
 };
 
-template <int C>
+// IL (interleaved w and r): a child's r_j of all C chains sits in one 8C-byte run, so its gather and
+// scatter move one sector for every chain instead of one per chain -- the colour step is bound by those
+// scattered 8-byte accesses (54 MB of HBM per launch for 32 k members, profiles/r05g), not by the launch
+template <int C, bool IL>
+__device__ __forceinline__ double& chain_at(double* const* per, double* il, int c, int64_t idx) {
+    return IL ? il[idx * C + c] : per[c][idx];
+}
+
+template <int C, bool IL>
 __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restrict__ member_rows, int64_t n_members,
                                                             const ChainPtrs cp, const double* __restrict__ noise_w,
                                                             const int32_t* __restrict__ rev_j, int64_t m_cap) {
+#define CW(c, idx) chain_at<C, IL>(cp.w, cp.wil, (c), (idx))
+#define CR(c, idx) chain_at<C, IL>(cp.r, cp.ril, (c), (idx))
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
@@ -709,8 +721,8 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
     double wi[C], ri[C], iF[C], Pi[C], yi[C], zl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        wi[c] = cp.w[c][i];
-        ri[c] = cp.r[c][i];
+        wi[c] = CW(c, i);
+        ri[c] = CR(c, i);
         iF[c] = cp.invF[c][i];
         Pi[c] = cp.P[c][i];
         yi[c] = cp.yres[c][i];
@@ -741,7 +753,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
 #pragma unroll
-        for (int c = 0; c < C; ++c) rf[c][k] = cp.r[c][jf[k]];
+        for (int c = 0; c < C; ++c) rf[c][k] = CR(c, jf[k]);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         double acc = 0.0;
@@ -751,7 +763,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
             bf[c][k] = has[k] ? bf[c][k] : 0.0;
             acc = k == 0 ? (has[0] ? gf[c][0] * rf[c][0] : 0.0) : (has[k] ? fma(gf[c][k], rf[c][k], acc) : acc);
         }
-        for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(cp.Grev[c][e], cp.r[c][rev_j[e]], acc);
+        for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(cp.Grev[c][e], CR(c, rev_j[e]), acc);
 #if NNGP_GIBBS_DPP
         acc = group_sum<kGroup>(acc);
 #else
@@ -766,26 +778,31 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
         const double wn = fma(zl[c], sd, lin / prec);
         const double dw = wn - wi[c];
         if (live && l == 0) {
-            cp.w[c][i] = wn;
-            cp.r[c][i] = ri[c] + dw;
+            CW(c, i) = wn;
+            CR(c, i) = ri[c] + dw;
         }
 #pragma unroll
         for (int k = 0; k < kPer; ++k)
-            if (has[k]) cp.r[c][jf[k]] = fma(-bf[c][k], dw, rf[c][k]);
+            if (has[k]) CR(c, jf[k]) = fma(-bf[c][k], dw, rf[c][k]);
         for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) {
             const int64_t j = rev_j[e];
-            cp.r[c][j] = fma(-cp.Brev[c][e], dw, cp.r[c][j]);
+            CR(c, j) = fma(-cp.Brev[c][e], dw, CR(c, j));
         }
     }
 }
+#undef CW
+#undef CR
 
 hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
                                        int chains, const void* const* preps, int64_t n, int m, const double* sigma2,
                                        const double* tau2, const double* const* yres, const double* noise_w,
                                        double* const* w, double* const* r, const int32_t* rev_j,
-                                       const double* const* z, hipStream_t s) {
+                                       const double* const* z, hipStream_t s, double* w_il, double* r_il) {
     if (chains < 1 || chains > kMaxChains) return hipErrorInvalidValue;
+    const bool il = w_il != nullptr;
     ChainPtrs cp{};
+    cp.wil = w_il;
+    cp.ril = r_il;
     for (int c = 0; c < chains; ++c) {
         const GibbsPrep g = prep_layout((void*)preps[c], n, m);
         cp.Brev[c] = g.Brev;
@@ -794,8 +811,8 @@ hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors,
         cp.invF[c] = g.invF;
         cp.yres[c] = yres[c];
         cp.z[c] = z[c];
-        cp.w[c] = w[c];
-        cp.r[c] = r[c];
+        cp.w[c] = il ? nullptr : w[c];
+        cp.r[c] = il ? nullptr : r[c];
         cp.it2[c] = 1.0 / tau2[c];
         cp.is2[c] = 1.0 / sigma2[c];
     }
@@ -806,9 +823,14 @@ hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors,
         const int4* mr = (const int4*)member_rows + a;
         const int64_t mc = n * (int64_t)m;
         switch (chains) {
-#define NNGP_CHAINS_CASE(CC)                                                                                    \
-    case CC:                                                                                                   \
-        hipLaunchKernelGGL(gibbs_w_color_chains<CC>, grid, dim3(256), 0, s, mr, b - a, cp, noise_w, rev_j, mc); \
+#define NNGP_CHAINS_CASE(CC)                                                                                      \
+    case CC:                                                                                                     \
+        if (il)                                                                                                  \
+            hipLaunchKernelGGL((gibbs_w_color_chains<CC, true>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w,  \
+                               rev_j, mc);                                                                       \
+        else                                                                                                     \
+            hipLaunchKernelGGL((gibbs_w_color_chains<CC, false>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w, \
+                               rev_j, mc);                                                                       \
         break;
             NNGP_CHAINS_CASE(1) NNGP_CHAINS_CASE(2) NNGP_CHAINS_CASE(3) NNGP_CHAINS_CASE(4)
             NNGP_CHAINS_CASE(5) NNGP_CHAINS_CASE(6) NNGP_CHAINS_CASE(7) NNGP_CHAINS_CASE(8)

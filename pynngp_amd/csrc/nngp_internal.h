@@ -198,7 +198,8 @@ hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors,
                                        int chains, const void* const* preps, int64_t n, int m, const double* sigma2,
                                        const double* tau2, const double* const* yres, const double* noise_w,
                                        double* const* w, double* const* r, const int32_t* rev_j,
-                                       const double* const* z, hipStream_t s);
+                                       const double* const* z, hipStream_t s, double* w_il = nullptr,
+                                       double* r_il = nullptr);
 size_t gibbs_stats_workspace_bytes(int64_t n, int p);
 hipError_t gibbs_stats_launch(int64_t n, const double* r, const double* Ft, const double* yres, const double* y,
                               const double* X, int p, const double* w, const double* noise_w, double* out,

@@ -710,8 +710,11 @@ class SeqNNGPChains:
         chains[k].beta, chains[k].w   # chain k's state (a SeqNNGP)
     """
 
-    def __init__(self, coords, y, X=None, seeds=(0,), **kw):
+    def __init__(self, coords, y, X=None, seeds=(0,), interleave: bool = True, **kw):
         seeds = [int(s) for s in seeds]
+        # interleave: the colour steps read the chains' w and r from (n, C) copies (one sector per scattered
+        # access for all chains; packed before and unpacked after each iteration's colour sweeps)
+        self.interleave = bool(interleave)
         if not 1 <= len(seeds) <= 8:
             raise ValueError("1 to 8 chains per batch")
         if "seed" in kw:
@@ -745,12 +748,20 @@ class SeqNNGPChains:
         # w | rest: update_wt (the leaves' colour) then update_ws, one launch per colour for all chains
         c0 = cs[0]
         if c0._member_rows_t() is not None:
+            if self.interleave:
+                W = torch.stack([c.w for c in cs], dim=1)
+                R = torch.stack([c.r for c in cs], dim=1)
+            else:
+                W, R = [c.w for c in cs], [c.r for c in cs]
             for lo, hi in ((c0.n_colors_ref, c0.n_colors), (0, c0.n_colors_ref)):
                 if hi > lo:
                     _lib.gibbs_w_sweep_chains(c0._member_rows, c0.color_off[lo:hi + 1], [c._prep for c in cs], c0.m,
                                               [c.sigma2 for c in cs], [c.tau2 for c in cs], [c.yres for c in cs],
-                                              [c.w for c in cs], [c.r for c in cs], c0.rev_j, [c._z for c in cs],
-                                              noise_w=c0.noise_w)
+                                              W, R, c0.rev_j, [c._z for c in cs], noise_w=c0.noise_w)
+            if self.interleave:
+                for k, c in enumerate(cs):
+                    c.w.copy_(W[:, k])
+                    c.r.copy_(R[:, k])
         # the conjugate statistics of every chain, ONE synchronisation
         st = torch.stack([c._stats_dev() for c in cs]).cpu().numpy()
         for c, s_ in zip(cs, st):

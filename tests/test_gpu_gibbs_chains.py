@@ -32,14 +32,15 @@ def _same(a, b):
     assert torch.equal(a.y_unobserved, b.y_unobserved)
 
 
-@pytest.mark.parametrize("C", [1, 2, 4, 8])
-def test_chains_equal_single_runs(dev, C):
+@pytest.mark.parametrize("interleave", [True, False])
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 8])
+def test_chains_equal_single_runs(dev, C, interleave):
     from pynngp_amd import Priors, SeqNNGP, SeqNNGPChains
 
     x, X, y = _field(12_000, 5)
     kw = dict(m=10, priors=Priors(phi_unif=(2.0, 60.0)), sigma2=1.0, tau2=0.1, phi=12.0, phi_tuning=0.3, device=dev)
     seeds = [11 + 7 * k for k in range(C)]
-    multi = SeqNNGPChains(x, y, X, seeds=seeds, **kw)
+    multi = SeqNNGPChains(x, y, X, seeds=seeds, interleave=interleave, **kw)
     for _ in range(12):
         multi.step()
     assert sum(c.n_accept for c in multi.chains) > 0  # phi moves (accepted proposals re-prepare B / F)
@@ -94,15 +95,23 @@ def test_sweep_chains_kernel_equals_per_chain(dev):
         prep = _lib.gibbs_prepare(B, F, off, rev_j, rev_k)
         yres = torch.from_numpy(rng.standard_normal(n)).to(dev)
         z = torch.from_numpy(rng.standard_normal(n)).to(dev)
-        st.append(dict(prep=prep, w=w, r=R, yres=yres, z=z, s2=0.5 + 0.3 * k, t2=0.1 + 0.05 * k))
+        st.append(dict(prep=prep, w=w, r=R, w0=w.clone(), r0=R.clone(), yres=yres, z=z, s2=0.5 + 0.3 * k,
+                       t2=0.1 + 0.05 * k))
     ref = []
     for d in st:
         w, r = d["w"].clone(), d["r"].clone()
         _lib.gibbs_w_sweep(members, color_off, d["prep"], m, d["s2"], d["t2"], d["yres"], w, r, off, rev_j, 0, 0,
                            z=d["z"], noise_w=noise, member_rows=mrows)
         ref.append((w, r))
+    # the interleaved entry point: (n, C) copies of w and r, the same results bit for bit
+    W = torch.stack([d["w0"] for d in st], dim=1)
+    R = torch.stack([d["r0"] for d in st], dim=1)
+    _lib.gibbs_w_sweep_chains(mrows, color_off, [d["prep"] for d in st], m, [d["s2"] for d in st],
+                              [d["t2"] for d in st], [d["yres"] for d in st], W, R, rev_j, [d["z"] for d in st],
+                              noise_w=noise)
     _lib.gibbs_w_sweep_chains(mrows, color_off, [d["prep"] for d in st], m, [d["s2"] for d in st],
                               [d["t2"] for d in st], [d["yres"] for d in st], [d["w"] for d in st],
                               [d["r"] for d in st], rev_j, [d["z"] for d in st], noise_w=noise)
-    for d, (w, r) in zip(st, ref):
+    for k, (d, (w, r)) in enumerate(zip(st, ref)):
         assert torch.equal(d["w"], w) and torch.equal(d["r"], r)
+        assert torch.equal(W[:, k], w) and torch.equal(R[:, k], r)
