@@ -245,7 +245,7 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     # stream driven by its own host thread -- one chain leaves the GPU idle in its colour steps' launch
     # floors and its host synchronisations (tools/bench_gibbs_streams.py)
     cpg = 1 if single else max(1, args.chains_per_gpu)
-    batched = cpg > 1 and args.chain_mode == "batched"
+    batched = cpg > 1 and args.chain_mode in ("batched", "batched-percopy")
     streams = ([torch.cuda.current_stream(dev)] if cpg == 1 or batched
                else [torch.cuda.Stream(dev) for _ in range(cpg)])
     chains = []
@@ -254,7 +254,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
         chains.append(ShardedSeqNNGP(coords, y, X, seed=1, collective=distributed, **kw))
     elif batched:
         # C chains advanced together: one launch per colour for all, two host synchronisations per iteration
-        multi = SeqNNGPChains(coords, y, X, seeds=[1 + rank * cpg + k for k in range(cpg)], **kw)
+        multi = SeqNNGPChains(coords, y, X, seeds=[1 + rank * cpg + k for k in range(cpg)],
+                              interleave=args.chain_mode == "batched", **kw)
         chains = list(multi.chains)
     else:
         for k in range(cpg):
@@ -366,7 +367,7 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                                 if single else f"replicas x{world * cpg} ({cpg} independent chain(s) per GPU"
                                 + ("" if cpg == 1 else (", advanced together: one launch per colour for all"
                                                         if batched else ", each on its own stream")) + ")"),
-                "chain_mode": "batched" if batched else ("streams" if cpg > 1 else "single"),
+                "chain_mode": args.chain_mode if batched else ("streams" if cpg > 1 else "single"),
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
@@ -436,9 +437,10 @@ def main():
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
     ap.add_argument("--chains-per-gpu", type=int, default=1,
                     help="config 5 replica mode: independent chains per GPU, one stream and host thread each")
-    ap.add_argument("--chain-mode", default="batched", choices=["batched", "streams"],
+    ap.add_argument("--chain-mode", default="batched", choices=["batched", "batched-percopy", "streams"],
                     help="--chains-per-gpu C > 1: advance the C chains together (SeqNNGPChains: one launch per colour "
-                         "for all) or each on its own stream and host thread")
+                         "for all, w / r interleaved; batched-percopy: per-chain w / r) or each on its own stream "
+                         "and host thread")
     ap.add_argument("--single-chain", action="store_true",
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")

@@ -793,6 +793,138 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
 #undef CW
 #undef CR
 
+// The interleaved form with every access to w / r of all chains as ONE run of 8C bytes (dwordx4 pairs:
+// half the load / store instructions of per-chain scalars, which is what the colour step's random r_j
+// traffic costs -- the interleaving alone moved the bytes but not the instruction count).  Chains inner:
+// each chain's operations and their order are gibbs_w_color's (its sums, then its draw, then its
+// scatter), so chain c is still bit-identical; across chains only the interleaving of independent
+// operations changes.
+template <int C>
+__device__ __forceinline__ void il_load(const double* p, double (&v)[C]) {
+#pragma unroll
+    for (int q = 0; q + 1 < C; q += 2) {
+        const double2 t = *(const double2*)(p + q);
+        v[q] = t.x;
+        v[q + 1] = t.y;
+    }
+    if (C % 2 == 1) v[C - 1] = p[C - 1];
+}
+template <int C>
+__device__ __forceinline__ void il_store(double* p, const double (&v)[C]) {
+#pragma unroll
+    for (int q = 0; q + 1 < C; q += 2) *(double2*)(p + q) = make_double2(v[q], v[q + 1]);
+    if (C % 2 == 1) p[C - 1] = v[C - 1];
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void gibbs_w_color_chains_il(const int4* __restrict__ member_rows,
+                                                               int64_t n_members, const ChainPtrs cp,
+                                                               const double* __restrict__ noise_w,
+                                                               const int32_t* __restrict__ rev_j, int64_t m_cap) {
+    const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    const int64_t g = t / kGroup;
+    const int l = (int)(t % kGroup);
+    const bool live = g < n_members;
+    const int4 mr = member_rows[live ? g : n_members - 1];
+    const int64_t i = mr.x;
+    const int32_t e0 = mr.y, e1 = live ? mr.z : mr.y;
+    const double hi = noise_w != nullptr ? noise_w[i] : 1.0;
+    double* __restrict__ W = cp.wil;
+    double* __restrict__ R = cp.ril;
+    double wi[C], ri[C], iF[C], Pi[C], yi[C], zl[C];
+    il_load<C>(W + i * C, wi);
+    il_load<C>(R + i * C, ri);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        iF[c] = cp.invF[c][i];
+        Pi[c] = cp.P[c][i];
+        yi[c] = cp.yres[c][i];
+        zl[c] = cp.z[c][i];
+    }
+    int64_t jf[kPer];
+    bool has[kPer];
+    double bf[C][kPer], gf[C][kPer], rf[kPer][C];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int32_t ef = e0 + l + k * kGroup;
+        has[k] = ef < e1;
+        const int64_t es = has[k] ? ef : 0;
+        jf[k] = i;
+        int32_t jr = 0;
+        if (m_cap > 0) jr = rev_j[es];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            bf[c][k] = 0.0;
+            gf[c][k] = 0.0;
+            if (m_cap > 0) {
+                bf[c][k] = cp.Brev[c][es];
+                gf[c][k] = cp.Grev[c][es];
+            }
+        }
+        if (m_cap > 0) jf[k] = has[k] ? (int64_t)jr : i;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) il_load<C>(R + jf[k] * C, rf[k]);
+    double acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            rf[k][c] = has[k] ? rf[k][c] : 0.0;
+            bf[c][k] = has[k] ? bf[c][k] : 0.0;
+            a = k == 0 ? (has[0] ? gf[c][0] * rf[k][c] : 0.0) : (has[k] ? fma(gf[c][k], rf[k][c], a) : a);
+        }
+        acc[c] = a;
+    }
+    for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) {
+        double rj[C];
+        il_load<C>(R + (int64_t)rev_j[e] * C, rj);
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = fma(cp.Grev[c][e], rj[c], acc[c]);
+    }
+    double wn[C], dw[C], rn[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        double a = acc[c];
+#if NNGP_GIBBS_DPP
+        a = group_sum<kGroup>(a);
+#else
+#pragma unroll
+        for (int o = kGroup / 2; o > 0; o >>= 1) a += __shfl_xor(a, o);
+#endif
+        const double it2 = cp.it2[c], is2 = cp.is2[c];
+        const double it2i = noise_w != nullptr ? it2 * hi : it2;
+        const double prec = fma(iF[c] + Pi[c], is2, it2i);
+        const double lin = fma(yi[c], it2i, is2 * fma(wi[c] - ri[c], iF[c], fma(wi[c], Pi[c], a)));
+        const double sd = nngp_rsqrt(prec);
+        wn[c] = fma(zl[c], sd, lin / prec);
+        dw[c] = wn[c] - wi[c];
+        rn[c] = ri[c] + dw[c];
+    }
+    if (live && l == 0) {
+        il_store<C>(W + i * C, wn);
+        il_store<C>(R + i * C, rn);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (has[k]) {
+            double v[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) v[c] = fma(-bf[c][k], dw[c], rf[k][c]);
+            il_store<C>(R + jf[k] * C, v);
+        }
+    }
+    for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) {
+        const int64_t j = rev_j[e];
+        double rj[C];
+        il_load<C>(R + j * C, rj);
+#pragma unroll
+        for (int c = 0; c < C; ++c) rj[c] = fma(-cp.Brev[c][e], dw[c], rj[c]);
+        il_store<C>(R + j * C, rj);
+    }
+}
+
 hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
                                        int chains, const void* const* preps, int64_t n, int m, const double* sigma2,
                                        const double* tau2, const double* const* yres, const double* noise_w,
@@ -826,7 +958,7 @@ hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors,
 #define NNGP_CHAINS_CASE(CC)                                                                                      \
     case CC:                                                                                                     \
         if (il)                                                                                                  \
-            hipLaunchKernelGGL((gibbs_w_color_chains<CC, true>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w,  \
+            hipLaunchKernelGGL((gibbs_w_color_chains_il<CC>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w,     \
                                rev_j, mc);                                                                       \
         else                                                                                                     \
             hipLaunchKernelGGL((gibbs_w_color_chains<CC, false>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w, \
