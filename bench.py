@@ -246,8 +246,13 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     # floors and its host synchronisations (tools/bench_gibbs_streams.py)
     cpg = 1 if single else max(1, args.chains_per_gpu)
     batched = cpg > 1 and args.chain_mode in ("batched", "batched-percopy")
+    # batched-streams: two batches of C / 2 chains, each on its own stream and host thread, so one batch's
+    # colour steps (memory-latency bound) overlap the other's phi-proposal sweeps (VALU bound)
+    groups = min(args.chain_groups, cpg) if cpg > 1 and args.chain_mode == "batched-streams" else 0
+    if groups and cpg % groups:
+        raise SystemExit("--chain-mode batched-streams needs --chains-per-gpu divisible by --chain-groups")
     streams = ([torch.cuda.current_stream(dev)] if cpg == 1 or batched
-               else [torch.cuda.Stream(dev) for _ in range(cpg)])
+               else [torch.cuda.Stream(dev) for _ in range(groups or cpg)])
     chains = []
     kw = dict(m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01, device=dev)
     if single:
@@ -257,6 +262,14 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
         multi = SeqNNGPChains(coords, y, X, seeds=[1 + rank * cpg + k for k in range(cpg)],
                               interleave=args.chain_mode == "batched", **kw)
         chains = list(multi.chains)
+    elif groups:
+        per = cpg // groups
+        batches = []
+        for k in range(groups):
+            with torch.cuda.stream(streams[k]):
+                batches.append(SeqNNGPChains(coords, y, X, seeds=[1 + rank * cpg + k * per + j for j in range(per)],
+                                             **kw))
+        chains = [c for b in batches for c in b.chains]
     else:
         for k in range(cpg):
             with torch.cuda.stream(streams[k]):
@@ -278,15 +291,17 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
 
         errors = []
 
+        units = batches if groups else chains
+
         def one(k):
             try:
                 with torch.cuda.stream(streams[k]):
                     for _ in range(iters):
-                        chains[k].step()
+                        units[k].step()
             except BaseException as e:  # re-raised below: a failed chain must fail the run
                 errors.append(e)
 
-        th = [threading.Thread(target=one, args=(k,)) for k in range(cpg)]
+        th = [threading.Thread(target=one, args=(k,)) for k in range(len(units))]
         for t in th:
             t.start()
         for t in th:
@@ -367,7 +382,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                                 if single else f"replicas x{world * cpg} ({cpg} independent chain(s) per GPU"
                                 + ("" if cpg == 1 else (", advanced together: one launch per colour for all"
                                                         if batched else ", each on its own stream")) + ")"),
-                "chain_mode": args.chain_mode if batched else ("streams" if cpg > 1 else "single"),
+                "chain_mode": args.chain_mode if (batched or groups) else ("streams" if cpg > 1 else "single"),
+                "chain_groups": groups or None,
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
@@ -437,10 +453,13 @@ def main():
                          "when not launched by torchrun): the N-rank all-gather + fold path on a one-GPU box")
     ap.add_argument("--chains-per-gpu", type=int, default=1,
                     help="config 5 replica mode: independent chains per GPU, one stream and host thread each")
-    ap.add_argument("--chain-mode", default="batched", choices=["batched", "batched-percopy", "streams"],
+    ap.add_argument("--chain-mode", default="batched-streams",
+                    choices=["batched", "batched-percopy", "batched-streams", "streams"],
                     help="--chains-per-gpu C > 1: advance the C chains together (SeqNNGPChains: one launch per colour "
-                         "for all, w / r interleaved; batched-percopy: per-chain w / r) or each on its own stream "
-                         "and host thread")
+                         "for all, w / r interleaved; batched-percopy: per-chain w / r; batched-streams: two such "
+                         "batches on their own streams and host threads) or each on its own stream and host thread")
+    ap.add_argument("--chain-groups", type=int, default=2,
+                    help="--chain-mode batched-streams: the number of batches (streams / host threads)")
     ap.add_argument("--single-chain", action="store_true",
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")

@@ -62,3 +62,11 @@ def test_bench_config5_two_chains_per_gpu(dev):
     d = _run("--config", "5", "--steps", "5", "--warmup", "2", "--n", "20000", "--cpu-seconds", "0",
              "--chains-per-gpu", "2")
     assert d["steps"] == 5 and d["value"] > 0 and d["config"]["chains"] == 2 and d["config"]["chains_per_gpu"] == 2
+
+
+@pytest.mark.parametrize("mode", ["batched-streams", "batched", "batched-percopy", "streams"])
+def test_bench_config5_chain_modes(dev, mode):
+    d = _run("--config", "5", "--steps", "4", "--warmup", "2", "--n", "20000", "--cpu-seconds", "0",
+             "--chains-per-gpu", "4", "--chain-mode", mode)
+    assert d["steps"] == 4 and d["value"] > 0 and d["config"]["chains_per_gpu"] == 4
+    assert d["config"]["chain_mode"] == mode
