@@ -5,34 +5,20 @@
 
 namespace nngp {
 
-// coefficients of f^k in the shifted Chebyshev polynomial T_j(2 f - 1) (exact integers; rows j, columns k)
-__constant__ double kShiftedCheb[NNGP_MT_NC][NNGP_MT_NC] = {
-    {1.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {-1.0, 2.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {1.0, -8.0, 8.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {-1.0, 18.0, -48.0, 32.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {1.0, -32.0, 160.0, -256.0, 128.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {-1.0, 50.0, -400.0, 1120.0, -1280.0, 512.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {1.0, -72.0, 840.0, -3584.0, 6912.0, -6144.0, 2048.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {-1.0, 98.0, -1568.0, 9408.0, -26880.0, 39424.0, -28672.0, 8192.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {1.0, -128.0, 2688.0, -21504.0, 84480.0, -180224.0, 212992.0, -131072.0, 32768.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-    {-1.0, 162.0, -4320.0, 44352.0, -228096.0, 658944.0, -1118208.0, 1105920.0, -589824.0, 131072.0, 0.0, 0.0, 0.0, 0.0},
-    {1.0, -200.0, 6600.0, -84480.0, 549120.0, -2050048.0, 4659200.0, -6553600.0, 5570560.0, -2621440.0, 524288.0, 0.0, 0.0, 0.0},
-    {-1.0, 242.0, -9680.0, 151008.0, -1208064.0, 5637632.0, -16400384.0, 30638080.0, -36765696.0, 27394048.0, -11534336.0, 2097152.0, 0.0, 0.0},
-    {1.0, -288.0, 13728.0, -256256.0, 2471040.0, -14057472.0, 50692096.0, -120324096.0, 190513152.0, -199229440.0, 132120576.0, -50331648.0, 8388608.0, 0.0},
-    {-1.0, 338.0, -18928.0, 416416.0, -4759040.0, 32361472.0, -141213696.0, 412778496.0, -825556992.0, 1133117440.0, -1049624576.0, 627048448.0, -218103808.0, 33554432.0},
-};
-
 // One block per octave of t: its NNGP_MT_K bins x NNGP_MT_NC nodes evaluate rho with the direct evaluation
 // (nngp_matern_rho; the Temme / continued-fraction loops are the kernel's critical path), then the fit of
 // nngp_matern_bin_fit in parallel -- one thread per (bin, Chebyshev coefficient) for the transform of the
 // deviations from the middle node's value, one per (bin, power of f) for the monomial coefficients --
 // with the same sums in the same order as the serial host version.
-__global__ __launch_bounds__(64) void matern_table_kernel(const CovParams P, double* __restrict__ tab) {
-    static_assert(NNGP_MT_K * NNGP_MT_NC <= 64, "one node per thread");
+constexpr int kMtThreads = (NNGP_MT_K * NNGP_MT_NC + 63) / 64 * 64;
+
+__global__ __launch_bounds__(kMtThreads) void matern_table_kernel(const CovParams P, double* __restrict__ tab) {
     __shared__ double rho[NNGP_MT_K][NNGP_MT_NC];
     __shared__ double cheb[NNGP_MT_K][NNGP_MT_NC];
     __shared__ double costab[NNGP_MT_NC * NNGP_MT_NC];
+    // coefficients of f^k in the shifted Chebyshev polynomial T_j(2 f - 1) (exact integers; rows j, columns
+    // k): T_0 = 1, T_1 = 2 f - 1, T_{j+1} = 2 (2 f - 1) T_j - T_{j-1}, the host fit's recurrence
+    __shared__ double scheb[NNGP_MT_NC][NNGP_MT_NC];
     const int o = blockIdx.x;
     const int tid = threadIdx.x;
     const int jb = tid / NNGP_MT_NC, k = tid % NNGP_MT_NC;
@@ -42,8 +28,18 @@ __global__ __launch_bounds__(64) void matern_table_kernel(const CovParams P, dou
         if (work) tab[(int64_t)b * NNGP_MT_NC + k] = (o == 0 && k == 0) ? 1.0 : 0.0;
         return;
     }
-    for (int i = tid; i < NNGP_MT_NC * NNGP_MT_NC; i += 64)
+    for (int i = tid; i < NNGP_MT_NC * NNGP_MT_NC; i += kMtThreads)
         costab[i] = cos(3.141592653589793 * (i / NNGP_MT_NC) * ((i % NNGP_MT_NC) + 0.5) / NNGP_MT_NC);
+    if (tid == 0) {  // row by row (a few hundred exact operations)
+        for (int j = 0; j < NNGP_MT_NC; ++j)
+            for (int k = 0; k < NNGP_MT_NC; ++k) {
+                double v;
+                if (j == 0) v = k == 0 ? 1.0 : 0.0;
+                else if (j == 1) v = k == 0 ? -1.0 : (k == 1 ? 2.0 : 0.0);
+                else v = (k > 0 ? 4.0 * scheb[j - 1][k - 1] : 0.0) - 2.0 * scheb[j - 1][k] - scheb[j - 2][k];
+                scheb[j][k] = v;
+            }
+    }
     if (work) rho[jb][k] = nngp_matern_rho(P, sqrt(nngp_matern_bin_t(P, b, nngp_matern_node(k))));
     __syncthreads();
     if (work) {  // Chebyshev coefficient c_k of bin jb (k plays j's role here)
@@ -57,14 +53,14 @@ __global__ __launch_bounds__(64) void matern_table_kernel(const CovParams P, dou
     if (work) {  // coefficient of f^k: sum_j c_j [f^k] T_j(2 f - 1), j ascending (then the middle value)
         double a = 0.0;
 #pragma unroll
-        for (int j = 0; j < NNGP_MT_NC; ++j) a = fma(cheb[jb][j], kShiftedCheb[j][k], a);
+        for (int j = 0; j < NNGP_MT_NC; ++j) a = fma(cheb[jb][j], scheb[j][k], a);
         if (k == 0) a += rho[jb][NNGP_MT_NC / 2];
         tab[(int64_t)b * NNGP_MT_NC + k] = a;
     }
 }
 
 hipError_t matern_table_launch(const CovParams& P, double* tab, hipStream_t s) {
-    hipLaunchKernelGGL(matern_table_kernel, dim3((unsigned)P.mt_noct), dim3(64), 0, s, P, tab);
+    hipLaunchKernelGGL(matern_table_kernel, dim3((unsigned)P.mt_noct), dim3(kMtThreads), 0, s, P, tab);
     return hipGetLastError();
 }
 

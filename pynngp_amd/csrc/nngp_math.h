@@ -285,13 +285,16 @@ NNGP_HD double nngp_matern_rho(const CovParams& P, double u) {
 // nodes (values from nngp_matern_rho), in monomial form.  Octave 0 holds rho = 1 (every t below it
 // has 1 - rho < NNGP_MT_EPS) and octave noct - 1 holds rho = 0 (rho < NNGP_MT_EPS beyond): coincident
 // points give exactly 1, far-away padding points exactly 0 (decoupled).  Interpolation error against
-// mpmath (nu = 0.5 .. 50, 4 bins per octave, degree 13): <= 1.2e-17 absolute; the table inherits the
+// mpmath (nu = 0.5 .. 50, 8 bins per octave of degree 9 since round 5: ~1e-16; 4 of degree 13: 1.2e-17)
+// absolute, well under what the table inherits from
 // accuracy of nngp_matern_rho (<= 1.3e-15 absolute).  Per covariance: 11 VALU for the index and the
-// local variable, 13 FMAs, NNGP_MT_NC / 2 LDS reads of 16 B.  The octaves from 1 - rho < eps to
+// local variable, NNGP_MT_NC - 1 FMAs, NNGP_MT_NC / 2 LDS reads of 16 B (8 x 10 measured 9-12 % faster
+// than 4 x 14 -- 5 reads and 9 FMAs against 7 and 13 -- and 16 x 8 slower: every block copies the table
+// into LDS, 77 KB, profiles/r05m).  The octaves from 1 - rho < eps to
 // rho < eps fit NNGP_MT_MAX_OCT for nu >= NNGP_MT_NU_MIN; smaller nu start the table at 2^-64 and take
 // the small-t expansion below it (NNGP_MT_SERIES_E): every nu in (0, 50] runs on the pair kernel.
-#define NNGP_MT_K 4
-#define NNGP_MT_NC 14
+#define NNGP_MT_K 8
+#define NNGP_MT_NC 10
 #define NNGP_MT_MAX_OCT 160
 #define NNGP_MT_EPS 1e-18
 #define NNGP_MT_NU_MIN 0.4

@@ -107,7 +107,7 @@ TABLE_NUS = tuple(NUS) + (0.45, 1.0000001, 1.97, 2.0, 3.0, 0.05, 0.2, 0.3, 0.44)
 
 
 def test_table_rho_vs_mpmath(table_rho):
-    """Table path (bins of t = u^2: 4 per octave, degree 13) against mpmath: the same 2e-15 absolute bound as
+    """Table path (bins of t = u^2: NNGP_MT_K per octave of degree NNGP_MT_NC - 1) against mpmath: the same 2e-15 absolute bound as
     the direct evaluation it is built from, over u from 1e-8 to 20 and at the clamps (u = 0, far)."""
     rng = np.random.default_rng(9)
     worst = 0.0
