@@ -195,7 +195,7 @@ class CallableCovariance:
     MODES = ("torch", "numpy", "loop", "loop_torch")
 
     def __init__(self, fn: Callable, tau2: float = 0.0, batch: Optional[str] = None, chunk_bytes: int = 1 << 28,
-                 cache: bool = False):
+                 cache: bool = False, pairs: bool = False):
         if not callable(fn):
             raise TypeError("cov must be callable as cov(a, b) on coordinate rows")
         if not tau2 >= 0:
@@ -204,6 +204,15 @@ class CallableCovariance:
             raise ValueError(f"batch must be one of {self.MODES} or None")
         self.fn, self.tau2, self.batch, self.chunk_bytes = fn, float(tau2), batch, int(chunk_bytes)
         self.mode = batch
+        # pairs=True: in "torch" mode, evaluate fn once per DISTINCT point pair of a sweep's joint blocks and
+        # gather the blocks from those values (N = 1e6, m = 15: 30.5 M pairs instead of 136 M block entries),
+        # when fn on single-row pairs reproduces its joint blocks bit for bit in both argument orders (probed
+        # once).  Opt-in: the pair index costs ~42 ms per neighbour set (then cached), and a cheap broadcasting
+        # plug-in evaluates (P, 1, 1)-shaped pairs at a lower per-element rate than whole blocks (17.2 against
+        # 19.0 ms per sweep's blocks, profiles/r05o) -- it pays for an expensive fn reused over many sweeps
+        self.pairs = pairs
+        self._pairs_ok = None
+        self._pidx = None  # (coords, nbr, order, i0, versions) -> the distinct pairs and the blocks' gather index
         # cache=True: NNGP keeps this covariance's evaluated joint blocks between sweeps (the caller promises
         # fn is a fixed function: no state it reads changes).  Default off, as the reference, which calls cov
         # on every evaluation (nngp.py:82,96): a mutable plug-in (an MLE loop over a closure's parameters)
@@ -262,6 +271,48 @@ class CallableCovariance:
         self.mode = ref_mode
         return ref_mode
 
+    def _pairs_probe(self, X: torch.Tensor, ta: torch.Tensor, tb: torch.Tensor) -> bool:
+        """fn on (P, 1, d) single-row pairs equals its joint blocks' entries bit for bit, in both argument
+        orders (the distinct pairs are keyed by (smaller, larger) point index)."""
+        if self._pairs_ok is None:
+            try:
+                C = self._eval(X, "torch")[:, ta, tb].reshape(-1)
+                xa, xb = X[:, ta].reshape(-1, 1, X.shape[2]), X[:, tb].reshape(-1, 1, X.shape[2])
+                ab = torch.as_tensor(self.fn(xa, xb), dtype=torch.float64, device=X.device).reshape(-1)
+                ba = torch.as_tensor(self.fn(xb, xa), dtype=torch.float64, device=X.device).reshape(-1)
+                self._pairs_ok = bool(torch.equal(ab, C) and torch.equal(ba, C))
+            except Exception:  # noqa: BLE001 -- the plug-in decides what it accepts
+                self._pairs_ok = False
+        return self._pairs_ok
+
+    def _pair_index(self, coords, nbr, i0, order, ta, tb):
+        """The sweep's distinct point pairs (pa, pb: point indices, pa <= pb) and the blocks' gather index
+        inv ((m+1)(m+2)/2, rows) into [0, values...] (0: an entry with a slot without a point -- unused by
+        the kernels); cached for the same coords / nbr / order tensors (held, and their versions checked)."""
+        key = (coords, nbr, order, int(i0), coords._version, nbr._version, None if order is None else order._version)
+        c = self._pidx
+        if c is not None and all(x is y for x, y in zip(c[0][:3], key[:3])) and c[0][3:] == key[3:]:
+            return c[1]
+        n = coords.shape[0]
+        rows = nbr.shape[0]
+        loc = (torch.arange(rows, device=nbr.device) if order is None else order.long()) + int(i0)
+        idx = nbr.long()
+        g = torch.cat([torch.where((idx >= 0) & (idx < n), idx, torch.full_like(idx, -1)), loc[:, None]], dim=1)
+        ga, gb = g[:, ta].t(), g[:, tb].t()  # entry-major (ne, rows)
+        keys = torch.where((ga >= 0) & (gb >= 0), torch.minimum(ga, gb) * n + torch.maximum(ga, gb),
+                           torch.full_like(ga, -1))
+        del g, ga, gb
+        uniq, inv = torch.unique(keys, return_inverse=True)
+        del keys
+        # slot 0 of the values is the unused entries' (a key of -1 sorts first when present)
+        if uniq.numel() and int(uniq[0]) < 0:
+            uniq = uniq[1:]
+        else:
+            inv += 1
+        res = (uniq // n, uniq % n, inv)
+        self._pidx = (key, res)
+        return res
+
     def blocks(self, coords: torch.Tensor, nbr: torch.Tensor, i0: int = 0, qcoords: Optional[torch.Tensor] = None,
                order: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Joint blocks in :func:`_lib.bf_sweep_blocks`'s layout ((m+1)(m+2)/2, rows): fn over
@@ -279,13 +330,32 @@ class CallableCovariance:
         tb = torch.cat([torch.arange(int(k) + 1, device=dev) for k in range(m + 1)])
         per_row = (m + 1) * (m + 1) * 8 * 3 + (m + 1) * coords.shape[1] * 8
         chunk = max(1, min(rows, self.chunk_bytes // per_row))
-        mode = self.resolve_mode(joint_points(coords, nbr[:min(rows, 4)], i0, qcoords, None if order is None else
-                                              order[:min(rows, 4)]))
+        X4 = joint_points(coords, nbr[:min(rows, 4)], i0, qcoords, None if order is None else order[:min(rows, 4)])
+        mode = self.resolve_mode(X4)
+        if (self.pairs and mode == "torch" and qcoords is None and dev.type == "cuda" and rows * ne < 2 ** 31
+                and coords.shape[0] < 2 ** 31 and self._pairs_probe(X4, ta, tb)):
+            pa, pb, inv = self._pair_index(coords, nbr, i0, order, ta, tb)
+            vals = torch.empty(pa.numel() + 1, dtype=torch.float64, device=dev)
+            vals[0] = 0.0
+            # (a pair is a few doubles of fn's temporaries: chunks of millions of pairs keep the launches few)
+            pchunk = max(1, 8 * self.chunk_bytes // (8 * (3 + 2 * coords.shape[1])))
+            for p0 in range(0, pa.numel(), pchunk):
+                p1 = min(pa.numel(), p0 + pchunk)
+                C = self.fn(coords[pa[p0:p1]][:, None, :], coords[pb[p0:p1]][:, None, :])
+                vals[1 + p0:1 + p1] = torch.as_tensor(C, dtype=torch.float64, device=dev).reshape(-1)
+            torch.index_select(vals, 0, inv.reshape(-1), out=out.view(-1))
+            if self.tau2 > 0:
+                out[_lib.joint_diagonal(m).to(dev)] += self.tau2
+            return out
         if mode.startswith("loop"):
             chunk = min(chunk, 4096)
         for r0 in range(0, rows, chunk):
             r1 = min(rows, r0 + chunk)
-            X = joint_points(coords, nbr[r0:r1], i0, qcoords, None if order is None else order[r0:r1])
+            # (rows r0.. of a sweep without a visiting order are the locations i0 + r0 ..: round 5 fix -- the
+            # chunks after the first took i0 .. again, wrong blocks once rows exceeded one chunk, e.g. m = 27
+            # beyond ~14 k rows; found by the distinct-pair evaluation's bit-identity test)
+            X = joint_points(coords, nbr[r0:r1], i0 + (r0 if order is None else 0), qcoords,
+                             None if order is None else order[r0:r1])
             C = self._eval(X, mode)
             if tuple(C.shape) != (r1 - r0, m + 1, m + 1):
                 raise ValueError(f"cov(a, b) returned {tuple(C.shape)} for {r1 - r0} joint blocks of {m + 1} rows")

@@ -303,3 +303,82 @@ def test_isotropic_and_callable_agree_at_m28(dev):
     np.testing.assert_allclose(F1.cpu().numpy(), F2.cpu().numpy(), rtol=1e-10)
     assert torch.all((B1 - B2).abs() <= 1e-9 * (1 + B2.abs()))
     assert abs(p1[1].item() - p2[1].item()) <= 1e-11 * abs(p2[1].item())
+
+
+@pytest.mark.parametrize("m", [10, 15, 27])
+def test_callable_distinct_pairs_equal_blocks(dev, m):
+    """Round 5: a broadcasting plug-in is evaluated once per DISTINCT point pair of the sweep's joint blocks
+    (the blocks gathered from those values) -- B, F and the partials bit-identical to one evaluation per
+    block entry (pairs=False), in index order and in a visiting order; the pair index is cached and rebuilt
+    when the neighbour tensor changes in place."""
+    from pynngp_amd import CallableCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    rng = np.random.default_rng(50 + m)
+    x = rng.uniform(size=(20_000, 2))
+    y = rng.standard_normal(20_000)
+    c, v = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    nb = _lib.knn_prior(c, m)
+    fn = _aniso(1.2, [[90.0, -20.0], [-20.0, 30.0]], 0.05)
+    cp, cb = CallableCovariance(fn, pairs=True), CallableCovariance(fn)
+    order, nbs = _lib.row_order(c, nbr=nb)
+    for kw in (dict(), dict(order=order)):
+        nbr = nbs if kw else nb
+        rp = _sweep_any(cp, c, nbr, 0, values=v, qvalues=v, **kw)
+        rb = _sweep_any(cb, c, nbr, 0, values=v, qvalues=v, **kw)
+        assert cp._pairs_ok is True and cp._pidx is not None
+        assert all(torch.equal(a, b) for a, b in zip(rp, rb))
+        pa = cp._pidx[1][0]
+        assert pa.numel() < 0.6 * nbr.shape[0] * (m + 1) * (m + 2) // 2  # shared pairs evaluated once
+    nb2 = nb.clone()
+    _sweep_any(cp, c, nb2, 0, values=v, qvalues=v)
+    nb2[m + 5:m + 500, 0] = -1  # in place: a dropped neighbour (the slot becomes padding)
+    rp = _sweep_any(cp, c, nb2, 0, values=v, qvalues=v)
+    rb = _sweep_any(cb, c, nb2, 0, values=v, qvalues=v)
+    assert all(torch.equal(a, b) for a, b in zip(rp, rb))
+
+
+def test_callable_pairs_probe_rejects_asymmetric(dev):
+    """A plug-in whose fn(a, b) and fn(b, a) differ in the last bits keeps one evaluation per block entry."""
+    from pynngp_amd import CallableCovariance, _lib
+    from pynngp_amd.nngp import _sweep_any
+
+    base = _aniso(1.0, [[60.0, 0.0], [0.0, 60.0]], 0.1)
+
+    def asym(a, b):  # a - b in a non-commutative form: (a0 - b0) + (a1 - b1) rounds differently from its negation
+        t = a[..., :, None, :] - b[..., None, :, :]
+        return base(a, b) * (1.0 + 1e-12 * torch.tanh(t[..., 0] * 3.0 + t[..., 1] * 7.0) ** 2 * torch.sign(t[..., 0]))
+
+    rng = np.random.default_rng(3)
+    c = torch.from_numpy(rng.uniform(size=(3_000, 2))).to(dev)
+    v = torch.from_numpy(rng.standard_normal(3_000)).to(dev)
+    nb = _lib.knn_prior(c, 10)
+    cp, cb = CallableCovariance(asym, pairs=True), CallableCovariance(asym)
+    rp = _sweep_any(cp, c, nb, 0, values=v, qvalues=v)
+    rb = _sweep_any(cb, c, nb, 0, values=v, qvalues=v)
+    assert cp._pairs_ok is False
+    assert all(torch.equal(a, b) for a, b in zip(rp, rb))
+
+
+@pytest.mark.parametrize("order_kind", ["none", "zorder"])
+def test_callable_blocks_chunked_rows(dev, order_kind):
+    """Round-5 regression: the per-entry evaluation in several row chunks gives the blocks of one chunk (the
+    chunks after the first took the locations i0.. again when the sweep had no visiting order)."""
+    from pynngp_amd import CallableCovariance, _lib
+
+    rng = np.random.default_rng(12)
+    c = torch.from_numpy(rng.uniform(size=(6_000, 2))).to(dev)
+    nb = _lib.knn_prior(c, 12)
+    order = None
+    if order_kind == "zorder":
+        order, nb = _lib.row_order(c, nbr=nb)
+    fn = _aniso(1.0, [[50.0, 5.0], [5.0, 40.0]], 0.1)
+    one = CallableCovariance(fn, pairs=False).blocks(c, nb, 0, order=order)
+    many = CallableCovariance(fn, pairs=False, chunk_bytes=200 * 13 * 13 * 24).blocks(c, nb, 0, order=order)
+    pairs = CallableCovariance(fn, pairs=True).blocks(c, nb, 0, order=order)
+    valid = torch.cat([nb >= 0, torch.ones(nb.shape[0], 1, dtype=torch.bool, device=dev)], 1)
+    a = torch.arange(13, device=dev)
+    ta, tb = torch.repeat_interleave(a, a + 1), torch.cat([torch.arange(int(k) + 1, device=dev) for k in range(13)])
+    ok = (valid[:, ta] & valid[:, tb]).t()
+    assert torch.equal(one, many)
+    assert torch.equal(one[ok], pairs[ok])

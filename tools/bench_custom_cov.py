@@ -65,10 +65,35 @@ def aniso(a, b):  # a reference-style plug-in: cross-covariance of two row sets,
     return 1.4 * torch.exp(-torch.sqrt(q))
 
 
-cc = CallableCovariance(aniso, tau2=0.05)
+cc = CallableCovariance(aniso, tau2=0.05, pairs=True)
 cblk = cc.blocks(c, srt, 0, order=order)
 out["callable_mode"] = cc.mode
 out["callable_blocks_ms"] = timed(lambda: cc.blocks(c, srt, 0, order=order), reps=5)
+out["callable_distinct_pairs"] = int(cc._pidx[1][0].numel()) if cc._pidx is not None else None
+out["callable_block_entries"] = int(srt.shape[0] * (srt.shape[1] + 1) * (srt.shape[1] + 2) // 2)
+cc_blocks = CallableCovariance(aniso, tau2=0.05, pairs=False)
+out["callable_blocks_per_entry_ms"] = timed(lambda: cc_blocks.blocks(c, srt, 0, order=order), reps=5)
+cc_fresh = CallableCovariance(aniso, tau2=0.05, pairs=True)
+import time as _t  # noqa: E402
+_ph = {}
+_x = c[cc._pidx[1][0][:1]] if cc._pidx is not None else None
+torch.cuda.synchronize()
+_t0 = _t.perf_counter()
+for _ in range(3):
+    pa_, pb_, inv_ = cc._pidx[1]
+    _v = aniso(c[pa_][:, None, :], c[pb_][:, None, :])
+torch.cuda.synchronize()
+out["callable_pairs_fn_ms"] = (_t.perf_counter() - _t0) / 3 * 1e3
+_vals = torch.zeros(pa_.numel() + 1, dtype=torch.float64, device=c.device)
+torch.cuda.synchronize()
+_t0 = _t.perf_counter()
+for _ in range(3):
+    _o = _vals[inv_.reshape(-1)]
+torch.cuda.synchronize()
+out["callable_pairs_gather_ms"] = (_t.perf_counter() - _t0) / 3 * 1e3
+del _o, _v, _vals
+out["callable_pair_index_build_ms"] = timed(lambda: (setattr(cc_fresh, "_pidx", None),
+                                                     cc_fresh.blocks(c, srt, 0, order=order)), reps=3)
 out["callable_sweep_ms"] = timed(lambda: _lib.bf_sweep_blocks(cblk, srt, n, 0, values=v, qvalues=v, order=order))
 del cblk
 nb28 = _lib.knn_prior(c, 28)
