@@ -691,25 +691,17 @@ struct ChainPtrs {
     const double* z[kMaxChains];
     double* w[kMaxChains];
     double* r[kMaxChains];
-    double* wil;  // IL: w and r interleaved, (n, C) row-major -- chain c of location i at [i C + c]
+    double* wil;  // gibbs_w_color_chains_il: w and r interleaved, (n, C) row-major (chain c of location i at [i C + c])
     double* ril;
     double it2[kMaxChains], is2[kMaxChains];
 };
 
-// IL (interleaved w and r): a child's r_j of all C chains sits in one 8C-byte run, so its gather and
-// scatter move one sector for every chain instead of one per chain -- the colour step is bound by those
-// scattered 8-byte accesses (54 MB of HBM per launch for 32 k members, profiles/r05g), not by the launch
-template <int C, bool IL>
-__device__ __forceinline__ double& chain_at(double* const* per, double* il, int c, int64_t idx) {
-    return IL ? il[idx * C + c] : per[c][idx];
-}
-
-template <int C, bool IL>
+template <int C>
 __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restrict__ member_rows, int64_t n_members,
                                                             const ChainPtrs cp, const double* __restrict__ noise_w,
                                                             const int32_t* __restrict__ rev_j, int64_t m_cap) {
-#define CW(c, idx) chain_at<C, IL>(cp.w, cp.wil, (c), (idx))
-#define CR(c, idx) chain_at<C, IL>(cp.r, cp.ril, (c), (idx))
+#define CW(c, idx) cp.w[c][idx]
+#define CR(c, idx) cp.r[c][idx]
     const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
     const int64_t g = t / kGroup;
     const int l = (int)(t % kGroup);
@@ -961,7 +953,7 @@ hipError_t gibbs_w_sweep_chains_launch(const int32_t* member_rows, int n_colors,
             hipLaunchKernelGGL((gibbs_w_color_chains_il<CC>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w,     \
                                rev_j, mc);                                                                       \
         else                                                                                                     \
-            hipLaunchKernelGGL((gibbs_w_color_chains<CC, false>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w, \
+            hipLaunchKernelGGL((gibbs_w_color_chains<CC>), grid, dim3(256), 0, s, mr, b - a, cp, noise_w,        \
                                rev_j, mc);                                                                       \
         break;
             NNGP_CHAINS_CASE(1) NNGP_CHAINS_CASE(2) NNGP_CHAINS_CASE(3) NNGP_CHAINS_CASE(4)
