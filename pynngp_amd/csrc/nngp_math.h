@@ -421,7 +421,13 @@ NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2)
     const double f = __builtin_amdgcn_fract(s);
 #endif
     const int j = (int)s - NNGP_MT_K;
-    if (P.mt_series && ex <= P.mt_e0) return nngp_matern_below(P.mt_A, t, P.nu);  // below the table (rare)
+    if (P.mt_series && ex <= P.mt_e0) {  // below the table (rare)
+        // coincident points (d2 at point_d2's floor) are exactly 1 -- 1 - A t^nu at the floor is not for a
+        // tiny nu (nu = 0.01: 1 - 1e-3) -- and skip the call: the four-lane kernel evaluates every row's
+        // self entry in its diagonal block, which took the call once per row group at small nu (+35 %)
+        if (d2 <= NNGP_D2_FLOOR) return 1.0;
+        return nngp_matern_below(P.mt_A, t, P.nu);
+    }
     int o = ex - P.mt_e0;
     o = o < 0 ? 0 : (o > P.mt_noct - 1 ? P.mt_noct - 1 : o);
     const double* c = tab + (o * NNGP_MT_K + j) * NNGP_MT_NC;

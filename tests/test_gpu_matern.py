@@ -151,7 +151,7 @@ def test_matern_m1_covariance_vs_mpmath(lib, dev, c_oracle):
             assert abs(cov[k] - float(ref)) <= 4e-15 * sigma2, (nu, k, cov[k], float(ref))
 
 
-@pytest.mark.parametrize("nu", [0.05, 0.2, 0.4])
+@pytest.mark.parametrize("nu", [0.01, 0.05, 0.2, 0.4])
 def test_matern_small_nu_near_coincident_points(lib, dev, nu):
     """Small nu below the table: points 1e-30 .. 1e-9 apart (t < 2^-64 with phi = 9) and exact duplicates
     take rho = 1 - A t^nu; the covariance against mpmath (m = 1), the pair and four-lane kernels."""

@@ -146,8 +146,9 @@ def test_table_small_nu_below_the_table(table_rho):
         us = [2.0 ** -e for e in (31, 32, 33, 40, 60, 100, 200, 400)] + [2.0 ** -31.9, 1e-12, 1e-100]
         got, noct = table_rho([(nu, u) for u in us] + [(nu, 0.0)])
         assert all(0 < k <= 160 for k in noct)
-        # u = 0 is the kernels' floor d^2 = 2^-1000 (coincident points): rho(2^-500), 1 - A 2^(-1000 nu)
-        assert abs(got[-1] - float(_ref(nu, 2.0 ** -500))) <= 2e-15
+        # u = 0 (the kernels' floor d^2 = 2^-1000, coincident points): exactly 1 (round 5; 1 - A 2^(-1000 nu)
+        # before, 1 - 1e-6 at nu = 0.02)
+        assert got[-1] == 1.0
         for u, g in zip(us, got):
             worst = max(worst, float(abs(g - _ref(nu, u))))
     assert worst <= 2e-15, worst
