@@ -190,7 +190,10 @@ __global__ __launch_bounds__(256) void bf_group(const double* __restrict__ coord
                 if (b < P * s) {
                     R[s][b] = cov(point_d2<DA>(o[s], X[b]));
                 } else if (b < P * s + P - 1) {  // diagonal block: lane-dependent
-                    const double c = cov(point_d2<DA>(o[s], X[b]));
+                    // (the self entry's value is not used: under the Matern table it would take the small-nu
+                    // branch's call for its zero distance, once per row group, so it evaluates d2 = 1 instead)
+                    const double d2 = point_d2<DA>(o[s], X[b]);
+                    const double c = cov(MT && b == a ? 1.0 : d2);
                     R[s][b] = b < a ? c : (b == a ? Pc.diag : 0.0);
                 } else {
                     R[s][b] = b == a ? Pc.diag : 0.0;

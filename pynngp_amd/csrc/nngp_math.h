@@ -321,11 +321,15 @@ NNGP_HD double nngp_matern_small_bound(double nu, double t) {
 // 1 - A t^nu below the table: a real call on the GPU (ocml's pow would otherwise be inlined at each of a
 // fully unrolled kernel's hundreds of covariance sites -- 4x the code -- for a branch that near-coincident
 // points alone take)
+// points, and coincident points -- t at point_d2's floor times phi^2 -- are exactly 1 (1 - A t^nu there is
+// not for a tiny nu: 1 - 1e-3 at nu = 0.01)
 #ifdef NNGP_MATH_HOST
-static inline double nngp_matern_below(double A, double t, double nu) { return fma(-A, pow(t, nu), 1.0); }
+static inline double nngp_matern_below(double A, double t, double nu, double mphi2) {
+    return t <= NNGP_D2_FLOOR * mphi2 ? 1.0 : fma(-A, pow(t, nu), 1.0);
+}
 #else
-__device__ __attribute__((noinline)) static double nngp_matern_below(double A, double t, double nu) {
-    return fma(-A, pow(t, nu), 1.0);
+__device__ __attribute__((noinline)) static double nngp_matern_below(double A, double t, double nu, double mphi2) {
+    return t <= NNGP_D2_FLOOR * mphi2 ? 1.0 : fma(-A, pow(t, nu), 1.0);
 }
 #endif
 
@@ -421,13 +425,7 @@ NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2)
     const double f = __builtin_amdgcn_fract(s);
 #endif
     const int j = (int)s - NNGP_MT_K;
-    if (P.mt_series && ex <= P.mt_e0) {  // below the table (rare)
-        // coincident points (d2 at point_d2's floor) are exactly 1 -- 1 - A t^nu at the floor is not for a
-        // tiny nu (nu = 0.01: 1 - 1e-3) -- and skip the call: the four-lane kernel evaluates every row's
-        // self entry in its diagonal block, which took the call once per row group at small nu (+35 %)
-        if (d2 <= NNGP_D2_FLOOR) return 1.0;
-        return nngp_matern_below(P.mt_A, t, P.nu);
-    }
+    if (P.mt_series && ex <= P.mt_e0) return nngp_matern_below(P.mt_A, t, P.nu, P.mphi2);  // below the table (rare)
     int o = ex - P.mt_e0;
     o = o < 0 ? 0 : (o > P.mt_noct - 1 ? P.mt_noct - 1 : o);
     const double* c = tab + (o * NNGP_MT_K + j) * NNGP_MT_NC;
