@@ -89,6 +89,9 @@ namespace nngp {
 // NNGP_PAIRB_ZLDS_MIN: from this m the neighbour values wait in LDS between the gathers and the
 // residual (they are read only there): NP doubles of registers per lane less where the two-wave
 // register budget is tight.
+#ifndef NNGP_MT_GLOBAL  // 1: the Matern-nu table from global memory instead of a per-block LDS copy (A/B)
+#define NNGP_MT_GLOBAL 0
+#endif
 #ifndef NNGP_PAIRB_ZLDS_MIN
 #define NNGP_PAIRB_ZLDS_MIN 99
 #endif
@@ -479,7 +482,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     __shared__ double etab_own[MT || LEFT ? 1 : NNGP_EXP_TAB_N];
     double* const etab = LEFT ? lbuf : etab_own;
     extern __shared__ double4 pairb_mtab[];  // MT: the Matern table (dynamic LDS, NNGP_MT_BYTES(noct))
-    const double* ctab = MT ? (const double*)pairb_mtab : etab;  // the covariance evaluation's table
+    // (NNGP_MT_GLOBAL: the Matern table read in place from global memory -- no per-block copy)
+    const double* ctab = MT ? (NNGP_MT_GLOBAL ? cblk : (const double*)pairb_mtab) : etab;
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)
     constexpr int kTabPer = kPairbThreads >= NNGP_EXP_TAB_N ? 1 : NNGP_EXP_TAB_N / kPairbThreads;
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
-        if constexpr (MT) {
+        if constexpr (MT && !NNGP_MT_GLOBAL) {
             const int n4 = Pc.mt_noct * (NNGP_MT_K * NNGP_MT_NC / 4);
             const double4* g = (const double4*)cblk;
             for (int k = (int)threadIdx.x; k < n4; k += kPairbThreads) pairb_mtab[k] = g[k];
@@ -1176,7 +1180,7 @@ inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
 // being the whole sweep's count; the records are then the caller's to fold (never fused)
 template <int M, int KIND, int D, bool PL = false>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s, const PairPlanArgs* ppl = nullptr) {
-    const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
+    const size_t lds = KIND == NNGP_KIND_MATERN && !NNGP_MT_GLOBAL ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
     const PairbTiling tl = pairb_tiling(a.n_rows, M, KIND);
     PairPlanArgs pp = ppl != nullptr ? *ppl : PairPlanArgs{};
     if (!PL && a.tiles != nullptr) {

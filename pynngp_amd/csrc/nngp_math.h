@@ -429,9 +429,23 @@ NNGP_HD double nngp_matern_tab(const CovParams& P, const double* tab, double d2)
     int o = ex - P.mt_e0;
     o = o < 0 ? 0 : (o > P.mt_noct - 1 ? P.mt_noct - 1 : o);
     const double* c = tab + (o * NNGP_MT_K + j) * NNGP_MT_NC;
+#ifdef NNGP_MATH_HOST
     double r = c[NNGP_MT_NC - 1];
 #pragma unroll
     for (int k = NNGP_MT_NC - 2; k >= 0; --k) r = fma(r, f, c[k]);
+#else
+    // the same Horner order from 16-byte pairs (a bin's NC coefficients start 16-byte aligned: one load
+    // each from LDS or global memory)
+    static_assert(NNGP_MT_NC % 2 == 0, "coefficient pairs");
+    const double2* c2 = (const double2*)c;
+    double2 v = c2[NNGP_MT_NC / 2 - 1];
+    double r = fma(v.y, f, v.x);
+#pragma unroll
+    for (int h = NNGP_MT_NC / 2 - 2; h >= 0; --h) {
+        v = c2[h];
+        r = fma(fma(r, f, v.y), f, v.x);
+    }
+#endif
     return r;
 }
 
