@@ -337,7 +337,7 @@ int nngp_combine_partials_batch(const double *gathered, int32_t world, int64_t n
  *   (host arrays of device pointers) -- in ONE launch per colour; chain c's result is bit-identical
  *   to nngp_gibbs_w_sweep on its own arguments (with z given).
  * nngp_gibbs_w_sweep_chains_il: the same with every chain's w and r interleaved in two (n, chains)
- *   row-major arrays (chain c of location i at [i * chains + c]): a child's r_j of all chains is one
+ *   row-major, 16-byte aligned arrays (chain c of location i at [i * chains + c]): a child's r_j of all chains is one
  *   contiguous run, so the colour steps' scattered accesses move one sector for all chains; the
  *   results are the per-chain call's, bit for bit.
  * nngp_gibbs_stats: out[0] = sum r_i^2 / Ft_i, out[1] = sum h_i (yres_i - w_i)^2,

@@ -569,7 +569,8 @@ int nngp_gibbs_w_sweep_chains_il(const int32_t* member_rows, const int32_t* colo
         (m > 0 && rev_j == nullptr))
         return fail(NNGP_EINVAL, "null pointer argument");
     if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
-    if (((uintptr_t)w_il & 7) != 0 || ((uintptr_t)r_il & 7) != 0) return fail(NNGP_EINVAL, "w_il / r_il misaligned");
+    if (((uintptr_t)w_il & 15) != 0 || ((uintptr_t)r_il & 15) != 0)  // (read and written as 16-byte pairs)
+        return fail(NNGP_EINVAL, "w_il / r_il must be 16-byte aligned");
     if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
     for (int c = 0; c < chains; ++c) {

@@ -244,3 +244,21 @@ def test_sharded_gibbs_entries_reject(lib):
     assert lib.nngp_gibbs_w_apply(P(4), 3, P(8), P(8), 10, 3, P(8), P(8), P(8), P(8), None) == -1
     assert lib.nngp_gibbs_w_apply(P(16), 3, None, P(8), 10, 3, P(8), P(8), P(8), P(8), None) == -1
     assert lib.nngp_gibbs_w_apply(P(16), 0, None, None, 10, 3, None, None, None, None, None) == 0
+
+
+def test_gibbs_chains_entry_points_reject(lib):
+    """nngp_gibbs_w_sweep_chains / _il argument checks without a GPU: chain count, null and misaligned pointers."""
+    import ctypes
+
+    P = ctypes.c_void_p
+    C = 2
+    arr = (P * C)(P(256), P(512))
+    dbl = (ctypes.c_double * C)(1.0, 1.0)
+    off = (ctypes.c_int32 * 2)(0, 10)
+    args = lambda chains, w, r: (P(256), off, 1, chains, arr, 10, 5, dbl, dbl, arr, None, w, r, P(256), arr, None)
+    assert lib.nngp_gibbs_w_sweep_chains_il(*args(9, P(1024), P(2048))) == -1
+    assert "chains" in lib.nngp_last_error().decode()
+    assert lib.nngp_gibbs_w_sweep_chains_il(*args(C, None, P(2048))) == -1
+    assert lib.nngp_gibbs_w_sweep_chains_il(*args(C, P(1032), P(2048))) == -1
+    assert "16-byte" in lib.nngp_last_error().decode()
+    assert lib.nngp_gibbs_w_sweep_chains(*args(0, arr, arr)) == -1
