@@ -38,8 +38,8 @@ for m in range(lo, hi + 1):
     B = torch.empty((args.n, m), dtype=torch.float64, device=dev)
     F = torch.empty((args.n,), dtype=torch.float64, device=dev)
     algos = ["lane"] if m <= 16 else []
-    algos += ["quad"] if 25 <= m <= 32 and args.kind in ("exponential", "matern32") else []
-    algos += ["pairb"] if 1 <= m <= 32 else []
+    algos += ["quad"] if 25 <= m <= 32 else []
+    algos += ["pairb"] if 1 <= m <= 24 else []
     algos += ["wave"]
     if args.algos:
         algos = [a for a in algos if a in args.algos.split(",")]
