@@ -99,12 +99,13 @@ namespace nngp {
 // column's covariances evaluated when it is reached and updated from the finished columns, so the
 // trailing block and every coordinate are never live at once; the finished factor rows
 // 0..KL-1 wait in LDS for the back-substitution.  The register peak is the factor's later rows
-// instead of the whole joint block plus coordinates: m = 19, 20, 22 run at two waves per SIMD
-// (right-looking: one; 0.352 / 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows,
-// profiles/r03e); from m = NNGP_PAIRB_LEFT_ONE_WAVE_MIN the left-looking kernel runs at one wave
-// with more rows in LDS (its peak no longer fits 256 registers).
+// instead of the whole joint block plus coordinates: m = 19..22 run at two waves per SIMD
+// (right-looking: one; 0.352 / 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows at m = 19 /
+// 20 / 22, profiles/r03e; m = 21 0.416 vs 0.552, profiles/r05z2); from m = NNGP_PAIRB_LEFT_ONE_WAVE_MIN
+// the left-looking kernel runs at one wave with more rows in LDS (its peak no longer fits 256
+// registers): m = 23 / 24 0.604 / 0.696 vs 0.659 / 0.732 right-looking (profiles/r05z2).
 #ifndef NNGP_PAIRB_LEFT_MASK
-#define NNGP_PAIRB_LEFT_MASK ((1ull << 19) | (1ull << 20) | (1ull << 22))
+#define NNGP_PAIRB_LEFT_MASK ((1ull << 19) | (1ull << 20) | (1ull << 21) | (1ull << 22) | (1ull << 23) | (1ull << 24))
 #endif
 #ifndef NNGP_PAIRB_LEFT_ONE_WAVE_MIN
 #define NNGP_PAIRB_LEFT_ONE_WAVE_MIN 23
@@ -112,8 +113,8 @@ namespace nngp {
 #ifndef NNGP_PAIRB_LEFT_LDS_ROWS  // factor rows in LDS at two waves per SIMD (5: 123 KB of 160 per CU)
 #define NNGP_PAIRB_LEFT_LDS_ROWS 5
 #endif
-#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_1W  // ... and at one wave per SIMD (8: 147 KB)
-#define NNGP_PAIRB_LEFT_LDS_ROWS_1W 8
+#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_1W  // ... and at one wave per SIMD (7, with the late state in LDS)
+#define NNGP_PAIRB_LEFT_LDS_ROWS_1W 7
 #endif
 // Left-looking at three waves per SIMD (<= 168 VGPRs; bit m of NNGP_PAIRB_LEFT_3W_MASK, which
 // must also be set in NNGP_PAIRB_LEFT_MASK): NNGP_PAIRB_LEFT_LDS_ROWS_3W factor rows in LDS.

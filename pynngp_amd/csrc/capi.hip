@@ -28,7 +28,7 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py):
-// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking at m = 19, 20, 22) for 1 <= m <= 24
+// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking at m = 19..24) for 1 <= m <= 24
 // (profiles/r02ap, r03e: since its round-2 cuts it ties the one-lane kernel at m = 1, 2 and is
 // faster from m = 3), four lanes per location for 25..32 (profiles/r03e: 1.08-2.78 ms per 1e6 rows,
 // 1.15-1.9x faster than the blocked pair kernel spilling at one wave), one wavefront per location
