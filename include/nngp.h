@@ -54,9 +54,9 @@ extern "C" {
 
 /* kernels (NNGP_ALGO_AUTO picks the fastest measured one for m, kind and dim); LANE serves 2-D
  * exponential / Matern-3/2 only, QUAD kinds 0..4 in every dimension, PAIRB and WAVE every kind
- * (PAIRB and QUAD: NNGP_COV_MATERN through its table).  (3 and 7 were comparison-only kernels of earlier
+ * (PAIRB and QUAD: NNGP_COV_MATERN through its table; PAIRB at 25 <= m <= 32: kinds 0..4).  (3 and 7 were comparison-only kernels of earlier
  * builds; they are rejected as unknown.) */
-#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 24, quad for 25..32, wave above (matern: see kind 5) */
+#define NNGP_ALGO_AUTO 0  /* pairb for 1 <= m <= 32 except quad at 31, wave above (matern: see kind 5) */
 #define NNGP_ALGO_LANE 1  /* one lane per location (m <= 16)                                 */
 #define NNGP_ALGO_WAVE 2  /* one wavefront per location (m <= 63)                            */
 #define NNGP_ALGO_QUAD 4  /* four lanes per location (25 <= m <= 32)                         */

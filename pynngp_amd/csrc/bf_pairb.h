@@ -105,7 +105,7 @@ namespace nngp {
 // the left-looking kernel runs at one wave with more rows in LDS (its peak no longer fits 256
 // registers): m = 23 / 24 0.604 / 0.696 vs 0.659 / 0.732 right-looking (profiles/r05z2).
 #ifndef NNGP_PAIRB_LEFT_MASK
-#define NNGP_PAIRB_LEFT_MASK ((1ull << 19) | (1ull << 20) | (1ull << 21) | (1ull << 22) | (1ull << 23) | (1ull << 24))
+#define NNGP_PAIRB_LEFT_MASK (((1ull << 33) - 1) & ~((1ull << 19) - 1))  // m = 19..32
 #endif
 #ifndef NNGP_PAIRB_LEFT_ONE_WAVE_MIN
 #define NNGP_PAIRB_LEFT_ONE_WAVE_MIN 23
@@ -1252,7 +1252,13 @@ static bool launch_pairb_if(const BfArgs& a, const CovParams& Pc, hipStream_t s)
         case 2: launch_pairb_mkd<M, 2, D>(a, Pc, s); return true;
         case 3: launch_pairb_mkd<M, 3, D>(a, Pc, s); return true;
         case 4: launch_pairb_mkd<M, 4, D>(a, Pc, s); return true;
-        case NNGP_KIND_MATERN: launch_pairb_mkd<M, NNGP_KIND_MATERN, D>(a, Pc, s); return true;
+        case NNGP_KIND_MATERN:  // right-looking (the table path); above m = 24 the four-lane kernel serves it
+            if constexpr (M <= 24) {
+                launch_pairb_mkd<M, NNGP_KIND_MATERN, D>(a, Pc, s);
+                return true;
+            } else {
+                return false;
+            }
         default: return false;
     }
 }

@@ -28,12 +28,12 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py):
-// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking at m = 19..24) for 1 <= m <= 24
-// (profiles/r02ap, r03e: since its round-2 cuts it ties the one-lane kernel at m = 1, 2 and is
-// faster from m = 3), four lanes per location for 25..32 (profiles/r03e: 1.08-2.78 ms per 1e6 rows,
-// 1.15-1.9x faster than the blocked pair kernel spilling at one wave), one wavefront per location
-// above; every kind and dimension (the four-lane kernel has a runtime-kind, runtime-dimension
-// instantiation beside its 2-D exponential / Matern-3/2 ones).
+// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking from m = 19, at one wave with 7 factor
+// rows in LDS from m = 23) for 1 <= m <= 30 and m = 32 (profiles/r02ap, r03e; m = 25..32 since round 5,
+// profiles/r05z3: 0.72 / 1.05 / 2.05 ms per 1e6 rows at m = 25 / 28 / 32 against the four-lane kernel's
+// 1.07 / 1.42 / 2.77), four lanes per location at m = 31 (1.68 vs 1.83 ms), one wavefront per location
+// above; every kind and dimension.  The general-smoothness Matern kind keeps the four-lane kernel for
+// m = 25..32 (its pair-kernel form is right-looking: the table path is not instantiated above 24).
 int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     (void)dim;
     if (algo != NNGP_ALGO_AUTO) return algo;
@@ -44,8 +44,7 @@ int resolve_algo(int32_t algo, int32_t m, int32_t kind, int32_t dim) {
     // many rows.)
     if (kind == NNGP_COV_MATERN)
         return m >= 1 && m <= 24 ? nngp::kAlgoPairB : (m >= 25 && m <= 32 ? nngp::kAlgoQuad : nngp::kAlgoWave);
-    if (m >= 1 && m <= 24) return nngp::kAlgoPairB;
-    if (m >= 25 && m <= 32) return nngp::kAlgoQuad;
+    if (m >= 1 && m <= 32) return m == 31 ? nngp::kAlgoQuad : nngp::kAlgoPairB;
     return nngp::kAlgoWave;
 }
 

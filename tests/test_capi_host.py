@@ -89,7 +89,7 @@ def _sweep(lib, **kw):
     (dict(algo=4, m=20), -4, "4-lane kernel"),
     (dict(algo=3, m=15), -1, "unknown algo"),  # the removed comparison kernels
     (dict(algo=7, m=15), -1, "unknown algo"),
-    (dict(algo=5, m=25), -4, "blocked pair kernel"),
+    (dict(algo=5, m=33), -4, "blocked pair kernel"),
     (dict(sigma2=0.0), -1, "theta"),
     (dict(phi=float("nan")), -1, "theta"),
     (dict(tau2=-1.0), -1, "theta"),
@@ -166,14 +166,16 @@ def test_check_partials_codes(lib):
 
 
 def test_resolve_algo_table(lib):
-    """auto: the blocked pair kernel for 1 <= m <= 24 and the four-lane kernel for 25..32 at kinds
-    0..4 and every dimension, the wavefront kernel above; the general-smoothness Matern kind (5) the same
-    for every nu in (0, 50] (since round 5 the launch's table serves small nu too: below t = 2^-64 the
-    small-t expansion 1 - A t^nu); explicit codes pass through."""
-    for m in (1, 15, 20, 24, 25, 32):
+    """auto: the blocked pair kernel for 1 <= m <= 32 except m = 31 (the four-lane kernel) at kinds
+    0..4 and every dimension, the wavefront kernel above; the general-smoothness Matern kind (5): the pair
+    kernel for m <= 24 and the four-lane kernel for 25..32, for every nu in (0, 50] (since round 5 the
+    launch's table serves small nu too: below t = 2^-64 the small-t expansion 1 - A t^nu); explicit codes
+    pass through."""
+    for m in (1, 15, 20, 24, 25, 28, 30, 31, 32):
         for kind in range(6):
             for dim in (1, 2, 3):
-                assert lib.nngp_resolve_algo(0, m, kind, dim) == (5 if m <= 24 else 4)
+                want = (5 if m <= 24 else 4) if kind == 5 else (4 if m == 31 else 5)
+                assert lib.nngp_resolve_algo(0, m, kind, dim) == want, (m, kind, dim)
     assert lib.nngp_resolve_algo(0, 33, 0, 2) == 2
     assert lib.nngp_resolve_algo(0, 63, 4, 3) == 2
     assert lib.nngp_resolve_algo(1, 15, 0, 2) == 1

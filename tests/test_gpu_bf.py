@@ -74,7 +74,7 @@ ALL_KINDS = ("exponential", "matern32", "matern52", "gaussian", "spherical")
 
 
 QUAD_M = tuple(range(25, 33))  # instantiated for the 4-lane kernel
-PAIRB_M = tuple(range(1, 25))  # and for the 2x2-blocked 2-lane kernel
+PAIRB_M = tuple(range(1, 33))  # and for the 2x2-blocked 2-lane kernel (m = 25..32: left-looking, kinds 0..4)
 
 
 @pytest.mark.parametrize("algo", ["lane", "wave", "pairb"])
@@ -116,22 +116,39 @@ def test_bf_quad_all_m(lib, dev, c_oracle, m):
                                         ("spherical", (1.0, 8.0, 0.05))])
 @pytest.mark.parametrize("dim", [1, 2, 3])
 def test_bf_quad_generic_m25_32(lib, dev, c_oracle, m, kind, theta, dim):
-    """m = 25..32 (the four-lane kernel: 2-D exponential / Matern-3/2 instantiations, one
-    runtime-kind, runtime-dimension instantiation per m for the rest), every kind and dimension,
-    under algo "auto" (which must pick it, never the wavefront kernel)."""
+    """m = 25..32 on the four-lane kernel (2-D exponential / Matern-3/2 instantiations, one
+    runtime-kind, runtime-dimension instantiation per m for the rest), every kind and dimension; and
+    the same sweep under algo "auto" (the pair kernel except at m = 31, never the wavefront kernel)."""
     rng = np.random.default_rng(500 + m + 7 * dim)
     coords = rng.uniform(0.0, 1.0, (1500, dim))
     coords[700:705] = coords[300]
     y = rng.standard_normal(1500)
     nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, "quad")
     _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, "auto")
+
+
+@pytest.mark.parametrize("m", list(range(25, 33)))
+@pytest.mark.parametrize("kind,theta", [("exponential", (1.0, 20.0, 0.3)), ("matern32", (1.3, 15.0, 0.2)),
+                                        ("matern52", (1.0, 12.0, 0.1)), ("gaussian", (1.0, 6.0, 0.2)),
+                                        ("spherical", (1.0, 8.0, 0.05))])
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_bf_pairb_m25_32_kinds_dims(lib, dev, c_oracle, m, kind, theta, dim):
+    """The left-looking pair kernel at m = 25..32 (one wave per SIMD, 7 factor rows in LDS), every
+    fused kind and dimension, duplicates included."""
+    rng = np.random.default_rng(900 + m + 7 * dim)
+    coords = rng.uniform(0.0, 1.0, (1500, dim))
+    coords[700:705] = coords[300]
+    y = rng.standard_normal(1500)
+    nbr = c_oracle.c_knn_prior(coords, m)
+    _check(dev, lib, c_oracle, coords, nbr, kind, theta, y, "pairb")
 
 
 def test_auto_never_wave_below_33(lib):
     for m in range(1, 33):
         for kind in ALL_KINDS:
             for dim in (1, 2, 3):
-                assert lib.resolve_algo("auto", m, kind, dim) == ("pairb" if m <= 24 else "quad"), (m, kind, dim)
+                assert lib.resolve_algo("auto", m, kind, dim) == ("quad" if m == 31 else "pairb"), (m, kind, dim)
     assert lib.resolve_algo("auto", 33, "exponential", 2) == "wave"
 
 

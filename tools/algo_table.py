@@ -39,7 +39,7 @@ for m in range(lo, hi + 1):
     F = torch.empty((args.n,), dtype=torch.float64, device=dev)
     algos = ["lane"] if m <= 16 else []
     algos += ["quad"] if 25 <= m <= 32 else []
-    algos += ["pairb"] if 1 <= m <= 24 else []
+    algos += ["pairb"] if 1 <= m <= 32 else []
     algos += ["wave"]
     if args.algos:
         algos = [a for a in algos if a in args.algos.split(",")]
