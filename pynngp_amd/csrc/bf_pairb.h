@@ -99,13 +99,15 @@ namespace nngp {
 // column's covariances evaluated when it is reached and updated from the finished columns, so the
 // trailing block and every coordinate are never live at once; the finished factor rows
 // 0..KL-1 wait in LDS for the back-substitution.  The register peak is the factor's later rows
-// instead of the whole joint block plus coordinates: m = 19..22 run at two waves per SIMD
+// instead of the whole joint block plus coordinates: m = 18..22 run at two waves per SIMD (m = 18:
+// 0.273 vs 0.413 ms per 1e6 rows right-looking with 224 B of scratch, profiles/r05z5; m = 16 / 17
+// tie and stay right-looking)
 // (right-looking: one; 0.352 / 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows at m = 19 /
 // 20 / 22, profiles/r03e; m = 21 0.416 vs 0.552, profiles/r05z2); from m = NNGP_PAIRB_LEFT_ONE_WAVE_MIN
 // the left-looking kernel runs at one wave with more rows in LDS (its peak no longer fits 256
 // registers): m = 23 / 24 0.604 / 0.696 vs 0.659 / 0.732 right-looking (profiles/r05z2).
 #ifndef NNGP_PAIRB_LEFT_MASK
-#define NNGP_PAIRB_LEFT_MASK (((1ull << 33) - 1) & ~((1ull << 19) - 1))  // m = 19..32
+#define NNGP_PAIRB_LEFT_MASK (((1ull << 33) - 1) & ~((1ull << 18) - 1))  // m = 18..32
 #endif
 #ifndef NNGP_PAIRB_LEFT_ONE_WAVE_MIN
 #define NNGP_PAIRB_LEFT_ONE_WAVE_MIN 23
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr int NR = M + 1;         // joint rows 0..M (row M = the location)
     constexpr int NP = (NR + 1) / 2;  // row pairs
     constexpr int T = M / 2;          // pairs made of two neighbour rows: full 2x2 block steps
-    constexpr bool LEFT = pairb_lk(M, KIND);
+    constexpr bool LEFT = !PL && pairb_lk(M, KIND);  // (the planned kernel is right-looking)
     static_assert(!PL || (!CM && !MT && !LEFT && D >= 1 && M >= kPlanMinM && M <= kPlanMaxM),
                   "pair plans: the right-looking fused kinds, 1 <= D <= 3");
     // the planned kernel's LDS: the tile's points (coordinates, values) and its distinct covariances

@@ -28,7 +28,7 @@ int hip_fail(hipError_t e, const char* what) {
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // NNGP_ALGO_AUTO: fastest kernel per m, measured on MI355X at N = 1e6 in Z-order (tools/algo_table.py):
-// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking from m = 19, at one wave with 7 factor
+// the 2x2-blocked two-lane kernel (bf_pairb.h; left-looking from m = 18, at one wave with 7 factor
 // rows in LDS from m = 23) for 1 <= m <= 30 and m = 32 (profiles/r02ap, r03e; m = 25..32 since round 5,
 // profiles/r05z3: 0.72 / 1.05 / 2.05 ms per 1e6 rows at m = 25 / 28 / 32 against the four-lane kernel's
 // 1.07 / 1.42 / 2.77), four lanes per location at m = 31 (1.68 vs 1.83 ms), one wavefront per location
