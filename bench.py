@@ -444,8 +444,9 @@ def main():
                     help="testing only: every rank on cuda:0 with gloo collectives (the N-rank flow on one GPU)")
     ap.add_argument("--sweep-api", default="ops", choices=["ops", "ctypes"],
                     help="ops: torch.ops.nngp.bf_sweep_out (default); ctypes: the same C ABI via ctypes (A/B)")
-    ap.add_argument("--event-stride", type=int, default=10,
-                    help="bracket every S-th timed sweep with HIP events for kernel_ms (1 = every sweep)")
+    ap.add_argument("--event-stride", type=int, default=None,
+                    help="bracket every S-th timed sweep with HIP events for kernel_ms (1 = every sweep; default "
+                         "min(10, steps // 5): at least 5 samples from 5 steps on)")
     ap.add_argument("--exchange-batch", type=int, default=16,
                     help="sweeps whose (4,) partials share one all-gather (PipelinedCombine batch)")
     ap.add_argument("--force-collective", action="store_true",
@@ -464,7 +465,7 @@ def main():
                     help="config 5: ONE chain sharded over the GPUs (ShardedSeqNNGP, n locations per GPU) instead "
                          "of one chain per GPU")
     ap.add_argument("--plan", default="auto", choices=["auto", "on", "off"],
-                    help="tile pair plans (shared covariances evaluated once per tile; built with the neighbour "
+                    help="wave pair plans (shared covariances evaluated once per wavefront; built with the neighbour "
                          "sets, outside the timed region): auto = sweep.PLAN_DEFAULT (off: measured slower, DESIGN.md 4.1b)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
@@ -542,15 +543,19 @@ def main():
     # queue drain around the op it brackets (~6-8 us of idle GPU per bracketed sweep, measured:
     # config 2 runs 29.0 us per sweep without events and 36.8 us with a pair around every sweep,
     # profiles/r02am), so only a sample of the steps is bracketed; kernel_ms is their mean.
-    stride = max(1, args.event_stride)
+    # With few steps (the driver's 20) the stride shrinks so that >= 5 sweeps are sampled; one more event
+    # pair around the whole timed loop gives the GPU time per step over every step (kernel_ms_loop).
+    stride = max(1, args.event_stride if args.event_stride is not None else min(10, args.steps // 5))
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for k in range(min(stride // 2, args.steps - 1), args.steps, stride)}  # the middle step of each window
+    ev_loop = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     # independent sweeps: the all-gather of sweep k overlaps sweep k+1 (RCCL stream + side
     # stream for the fold); every sweep's global partials are complete when the clock stops.
     # (Deferring the block-record fold to the side stream as well, nngp_bf_finalize, issued
     # 9x the host work per step and measured 0.35 vs 0.25 ms per step: the in-line fold stays.)
     pipe = PipelinedCombine(sweep, args.steps, batch=args.exchange_batch)
     t0 = time.perf_counter()
+    ev_loop[0].record(stream)
     for k in range(args.steps):
         if k in ev:
             ev[k][0].record(stream)
@@ -558,6 +563,7 @@ def main():
         if k in ev:
             ev[k][1].record(stream)
         pipe.exchange(k)
+    ev_loop[1].record(stream)
     per_sweep = pipe.finish()
     torch.cuda.synchronize()
     if distributed:
@@ -568,6 +574,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
+    loop_ms = ev_loop[0].elapsed_time(ev_loop[1]) / args.steps
     p = per_sweep[-1].cpu().numpy()
     assert all(np.array_equal(q, p, equal_nan=True) for q in per_sweep.cpu().numpy()), \
         "sweeps of the same field must give identical partials"
@@ -575,7 +582,9 @@ def main():
 
     if rank == 0:
         bpl = bytes_per_location(args.m) if want_bf else bytes_per_location(args.m) - 8 * args.m - 8
-        achieved = bpl * rows / (kern_ms * 1e-3)
+        # a planned sweep also streams its wave pair plan: those bytes count as the sweep's input
+        plan_bpl = (sweep.plan_read_bytes / rows if sweep._plan_for(args.kind) is not None and rows > 0 else 0.0)
+        achieved = (bpl + plan_bpl) * rows / (kern_ms * 1e-3)
         fpl = flops_per_location(args.m)
         traffic, traffic_src = args.pmc_traffic, "--pmc-traffic" if args.pmc_traffic is not None else None
         if traffic is None:
@@ -628,10 +637,14 @@ def main():
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_location": bpl,
+                "algorithmic_bytes_per_location": bpl + plan_bpl,
+                "plan_bytes_per_location": plan_bpl,
+                "frac_without_plan_bytes": bpl * rows / (kern_ms * 1e-3) / HBM_PEAK,
                 "kernel_ms": kern_ms,
                 "kernel_ms_samples": len(ev),
                 "event_stride": stride,
+                "kernel_ms_loop": loop_ms,
+                "kernel_ms_loop_samples": args.steps,
                 "kernel_rows": rows,
             },
             "roofline_valu": valu_roofline(committed_profile(args, want_bf), rows, kern_ms),

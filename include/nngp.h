@@ -81,8 +81,10 @@ const char *nngp_version(void);
  * nngp_bf_cross take `nu` after tau2; nngp_bf_sweep_blocks serves 1 <= m <= 32.  Revision 3
  * (library 0.3.0) adds the tile pair plans (nngp_pair_plan_*, nngp_bf_sweep_plan), the batched
  * chains' sweeps (nngp_gibbs_w_sweep_chains, _il) and the device colouring (nngp_color_moral_graph_dev);
- * NNGP_ALGO_AUTO / PAIRB / QUAD take the general Matern kind for every nu; nothing earlier moved. */
-#define NNGP_ABI_VERSION 3
+ * NNGP_ALGO_AUTO / PAIRB / QUAD take the general Matern kind for every nu; nothing earlier moved.
+ * Revision 4 (library 0.4.0): the pair plans are per wave (a new plan format, m <= 17) and their info
+ * array holds 10 words (NNGP_PLAN_INFO_LEN: + the nbr / order pointers, checked by nngp_bf_sweep_plan). */
+#define NNGP_ABI_VERSION 4
 int32_t nngp_abi_version(void);
 
 /* Message for the last error returned on the calling thread. */
@@ -171,28 +173,30 @@ int nngp_bf_finalize(const void *workspace, size_t workspace_bytes, int64_t n_ro
                      int32_t dim, int32_t algo, double *partials, void *stream);
 
 /* ---------------------------------------------------------------------------
- * Tile pair plans: the same sweep with every covariance a tile shares evaluated once.
- * The pair kernel (NNGP_ALGO_PAIRB) sweeps tiles of ~128 consecutive rows; in a spatial visiting
- * order neighbouring locations share most of their neighbours, so only ~36 % of a tile's joint-block
+ * Wave pair plans: the same sweep with every covariance a wavefront's locations share evaluated once.
+ * The pair kernel (NNGP_ALGO_PAIRB) sweeps 32 consecutive rows per wavefront; in a spatial visiting
+ * order neighbouring locations share most of their neighbours, so only ~46 % of a wave's joint-block
  * entries are distinct point pairs (N = 1e6, m = 15).  A plan -- built once per (nbr, order, i0,
- * n_points), like the neighbour sets -- lists per tile its distinct points and pairs and, per
- * location, where each of its entries lives; nngp_bf_sweep_plan then evaluates each pair once into
- * LDS and factors every location's block from there.  Same reference methods as nngp_bf_sweep
- * (_CNs / _Ccross / _Cs / _Bsi / _Fsi, nngp.py:73-96); its B, F, R are bit-identical to
+ * n_points), like the neighbour sets -- lists per wave its distinct points and pairs and, per lane,
+ * where each of its joint-block entries lives; nngp_bf_sweep_plan then evaluates each pair once into
+ * the wave's LDS slice and factors every location's block from there.  Same reference methods as
+ * nngp_bf_sweep (_CNs / _Ccross / _Cs / _Bsi / _Fsi, nngp.py:73-96); its B, F, R are bit-identical to
  * nngp_bf_sweep's with NNGP_ALGO_PAIRB on the same arguments, and so are its partials (tiles whose
- * points or pairs exceed the LDS budget are swept by the unplanned kernel into the same records).
- * nngp_pair_plan_supported: 1 when plans serve (m, kind, dim): 2 <= m <= 18, kinds 0..4, dim 1..3.
+ * waves exceed the LDS budget are swept by the unplanned kernel into the same records).
+ * nngp_pair_plan_supported: 1 when plans serve (m, kind, dim): 2 <= m <= 17, kinds 0..4, dim 1..3.
  * nngp_pair_plan_bytes: the plan buffer's size (0: unsupported m).
  * nngp_pair_plan_build: builds the plan for the sweep's nbr / order / i0 / n_points (device
  * pointers as nngp_bf_sweep; 256-B aligned plan) on `stream`, then SYNCHRONISES the stream (a setup
  * call, the one exception to the no-synchronisation rule above) to fill the host array
- * info[NNGP_PLAN_INFO_LEN]: tiles swept through the plan, tiles swept directly, then the geometry the
- * plan was built for (n_rows, m, dim, i0, n_points) and a tag.  The plan stays valid while nbr and
- * order are unchanged (the caller's responsibility, as for any cached factorisation).
+ * info[NNGP_PLAN_INFO_LEN]: tiles swept through the plan, tiles swept directly, the geometry the
+ * plan was built for (n_rows, m, dim, i0, n_points), a tag, and the nbr and order pointers.
  * nngp_bf_sweep_plan: nngp_bf_sweep's arguments (algo PAIRB implied; kinds 0..4, no nu) plus the
- * plan and its info; n_rows, m, dim, i0 and n_points must be those in info (checked).
+ * plan and its info; n_rows, m, dim, i0, n_points and the nbr / order pointers must be those in info
+ * (checked: NNGP_EINVAL).  The plan is stale once the contents of nbr or order change: the kernel
+ * re-derives a per-location checksum of the words it reads and flags a mismatching location in
+ * partials[3] with B = F = R = NaN, so a stale plan never returns the old neighbour sets' results.
  * ------------------------------------------------------------------------- */
-#define NNGP_PLAN_INFO_LEN 8
+#define NNGP_PLAN_INFO_LEN 10
 int nngp_pair_plan_supported(int32_t m, int32_t kind, int32_t dim);
 size_t nngp_pair_plan_bytes(int64_t n_rows, int32_t m, int32_t dim);
 int nngp_pair_plan_build(const int32_t *nbr, const int32_t *order, int64_t n_rows, int32_t m, int64_t i0,

@@ -69,8 +69,8 @@ MATERN_NU_MAX = 50.0
 ALGO_CODES = {"auto": 0, "lane": 1, "wave": 2, "quad": 4, "pairb": 5}
 MAX_M = 63
 MAX_DIM = 3
-ABI_VERSION = 3  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
-PLAN_INFO_LEN = 8  # NNGP_PLAN_INFO_LEN
+ABI_VERSION = 4  # NNGP_ABI_VERSION of include/nngp.h this binding's signatures follow
+PLAN_INFO_LEN = 10  # NNGP_PLAN_INFO_LEN
 BLOCKS_MAX_M = 32  # nngp_bf_sweep_blocks: 1 <= m <= 32
 
 
@@ -343,11 +343,12 @@ def _check_kind(kind: str, nu: Optional[float]) -> float:
 
 
 class PairPlan:
-    """A tile pair plan (``nngp_pair_plan_build``, include/nngp.h): the distinct covariance pairs of
-    every sweep tile and each location's map into them, for one (nbr, order, i0, n_points).  Passed to
-    :func:`bf_sweep` (``plan=``), it evaluates each shared covariance once per tile; B / F / R and the
+    """A wave pair plan (``nngp_pair_plan_build``, include/nngp.h): the distinct covariance pairs of
+    every sweep wavefront and each lane's map into them, for one (nbr, order, i0, n_points).  Passed to
+    :func:`bf_sweep` (``plan=``), it evaluates each shared covariance once per wave; B / F / R and the
     partials are bit-identical to the unplanned pair kernel's.  The plan is stale once nbr or order
-    change (rebuild it, as the neighbour sets themselves)."""
+    change (rebuild it, as the neighbour sets themselves): :meth:`matches` compares the buffers and
+    torch's in-place version counters, the C ABI the buffers, the kernel a per-location checksum."""
 
     def __init__(self, buf: torch.Tensor, info, nbr: torch.Tensor, order: Optional[torch.Tensor]):
         self.buf = buf
@@ -355,22 +356,43 @@ class PairPlan:
         self.n_planned, self.n_direct = int(info[0]), int(info[1])
         self.n_rows, self.m, self.dim, self.i0, self.n_points = (int(v) for v in info[2:7])
         self._nbr_ptr, self._order_ptr = nbr.data_ptr(), (order.data_ptr() if order is not None else 0)
+        self._versions = (nbr._version, order._version if order is not None else 0)
 
     def matches(self, nbr: torch.Tensor, order: Optional[torch.Tensor], i0: int, n_points: int, dim: int) -> bool:
-        """True when this plan was built for these (same storage) nbr / order and geometry."""
+        """True when this plan was built for these nbr / order tensors (same storage, not modified in place
+        since) and this geometry."""
         return (nbr.data_ptr() == self._nbr_ptr and (order.data_ptr() if order is not None else 0) == self._order_ptr
+                and (nbr._version, order._version if order is not None else 0) == self._versions
                 and tuple(nbr.shape) == (self.n_rows, self.m) and i0 == self.i0 and n_points == self.n_points
                 and dim == self.dim)
 
 
+def pair_plan_read_bytes(buf: torch.Tensor, m: int) -> int:
+    """Bytes a planned sweep streams from its plan (pair_plan.h: per planned wave the three header words,
+    the map chunks, the checksums, the U list and the pair words, in whole rounds) -- the plan's share of
+    the sweep's input traffic.  Reads the wave headers back (a setup-time helper: one synchronisation)."""
+    hdr = buf[:256].view(torch.int64).cpu()
+    nreg, sb = int(hdr[6]), int(hdr[9])
+    if nreg == 0:
+        return 0
+    wsb = sb // 4
+    w = buf[256:256 + nreg * sb].view(nreg * 4, wsb)[:, :12].contiguous().view(torch.int32).long().cpu()
+    nU, nE, st = w[:, 0], w[:, 1].clamp(min=0), w[:, 2]
+    planned = (st.view(nreg, 4) == 0).all(1).repeat_interleave(4)
+    np_ = (m + 2) // 2
+    che = (np_ * np_ + 7) // 8
+    per = 12 + che * 1024 + 256 + 256 * ((nU + 63) // 64) + 1024 * ((nE + 255) // 256)
+    return int(per[planned].sum())
+
+
 def pair_plan_supported(m: int, kind: str, dim: int) -> bool:
-    """Whether tile pair plans serve (m, kind, dim) (2 <= m <= 18, kinds exponential .. spherical, dim 1..3)."""
+    """Whether wave pair plans serve (m, kind, dim) (2 <= m <= 17, kinds exponential .. spherical, dim 1..3)."""
     return kind in KIND_CODES and bool(load().nngp_pair_plan_supported(int(m), KIND_CODES[kind], int(dim)))
 
 
 def pair_plan(nbr: torch.Tensor, n_points: int, dim: int, i0: int = 0,
               order: Optional[torch.Tensor] = None) -> PairPlan:
-    """Build the tile pair plan of a sweep over ``nbr`` (int32 (rows, m) on the GPU; rows are locations
+    """Build the wave pair plan of a sweep over ``nbr`` (int32 (rows, m) on the GPU; rows are locations
     ``i0 + (order[t] if order else t)`` of an ``n_points``-point field of dimension ``dim``).  A setup
     call: it synchronises torch's current stream once (the plan's tile counts come back to the host)."""
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
@@ -383,7 +405,7 @@ def pair_plan(nbr: torch.Tensor, n_points: int, dim: int, i0: int = 0,
     lib = load()
     nbytes = lib.nngp_pair_plan_bytes(rows, m, dim)
     if nbytes == 0:
-        raise NNGPExtensionError(f"no pair plans for m={m}, dim={dim} (2 <= m <= 18, dim 1..3)")
+        raise NNGPExtensionError(f"no pair plans for m={m}, dim={dim} (2 <= m <= 17, dim 1..3)")
     buf = _workspace(nbytes, dev)
     info = (ctypes.c_int64 * PLAN_INFO_LEN)()
     _check(lib.nngp_pair_plan_build(_ptr(nbr), _ptr(order), rows, m, int(i0), int(n_points), int(dim), _ptr(buf),
@@ -457,6 +479,9 @@ def bf_sweep(coords: torch.Tensor, nbr: torch.Tensor, i0: int, kind: str, sigma2
             raise ValueError(f"a pair plan runs the pair kernel, not algo {algo!r}")
         if not isinstance(plan, PairPlan) or plan.buf.device != dev:
             raise ValueError("plan must be a PairPlan on the sweep's device")
+        if not plan.matches(nbr, order, i0, coords.shape[0], d):
+            raise ValueError("stale pair plan: it was built for other nbr / order tensors (or they were modified in "
+                             "place since) or another geometry; rebuild it with pair_plan")
         _check(lib.nngp_bf_sweep_plan(_ptr(coords), coords.shape[0], d, _ptr(nbr), _ptr(order), rows, m, i0,
                                       KIND_CODES[kind], float(sigma2), float(phi), float(tau2), _ptr(values), _ptr(B),
                                       _ptr(F), _ptr(R), _ptr(partials), _ptr(workspace), workspace.numel(),

@@ -419,8 +419,8 @@ __device__ __forceinline__ double pr_rcp(double x) {
 // cblk[(a (a + 1) / 2 + b) * n_rows + t] (entry-major: one load instruction reads 32 consecutive
 // rows).  Slots with an invalid neighbour index are decoupled exactly (0 off the diagonal, 1 on it)
 // whatever the caller's values there; sigma2 = 1 (the blocks are the covariances themselves).
-// Tile pair plans (pair_plan.h): PL = true reads the tile's distinct covariance pairs and its entry map from
-// the plan instead of gathering coordinates per location; tiles != null lists the tiles (regions) this
+// Wave pair plans (pair_plan.h): PL = true reads each wave's distinct covariance pairs and its lanes' entry maps
+// from the plan instead of gathering coordinates per location; tiles != null lists the tiles (regions) this
 // launch sweeps (the planned and the direct launches of a planned sweep), n_tiles = all regions.
 struct PairPlanArgs {
     const uint8_t* slots = nullptr;   // region slots (pair_plan.h), region r at slots + r * slot_bytes
@@ -452,16 +452,10 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     constexpr bool LEFT = !PL && pairb_lk(M, KIND);  // (the planned kernel is right-looking)
     static_assert(!PL || (!CM && !MT && !LEFT && D >= 1 && M >= kPlanMinM && M <= kPlanMaxM),
                   "pair plans: the right-looking fused kinds, 1 <= D <= 3");
-    // the planned kernel's LDS: the tile's points (coordinates, values) and its distinct covariances
-    constexpr int PCS = plan_cs(D >= 1 ? D : 1);
-    constexpr int PE = PL ? plan_ecap(M, D >= 1 ? D : 1) + 1 : 1;  // covariance slots (slot 0: exact zero)
-    constexpr int PU = PL ? kPlanUMax : 1;
-    constexpr int KE = (PE - 1 + kPairbThreads - 1) / kPairbThreads;  // pair words per thread (max)
-    // points first (LDS address 0: a pair word's byte offsets are their addresses), then the covariances
-    // (sized for every lane of the last pair group: lanes past nE store into slots no entry reads)
-    __shared__ double ucrd[PU * PCS];
-    __shared__ double uval[PU];
-    __shared__ double ptab[PL ? KE * kPairbThreads + 1 : 1];
+    // the planned kernel's LDS (pair_plan.h): one slice per wave -- the wave's distinct covariances from its
+    // head (slot 0: the exact zero), the wave's points at its end
+    constexpr int PSL = PL ? plan_slice_bytes(M) : 16;
+    __shared__ __attribute__((aligned(16))) double wsl[PL ? kPairbWaves * PSL / 8 : 1];
     constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
     constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
                           (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
@@ -524,7 +518,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 #pragma unroll
         for (int s = 0; s < NP; ++s) {
             const int a = 2 * s + q;
-            jn[s] = PL ? -1 : nbr[rl * M + (a < M ? a : M - 1)];
+            jn[s] = nbr[rl * M + (a < M ? a : M - 1)];
         }
         double o[NP][DA], z[NP];
         // one unsigned compare per slot (a negative index is out of range as a huge unsigned);
@@ -550,7 +544,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             } else {
                 load_point<D>(pc, o[s]);
             }
-            if constexpr (!LEFT && !PL) z[s] = *pv;  // (the left-looking kernel gathers the values late)
+            if constexpr (!LEFT) z[s] = *pv;  // (the left-looking kernel gathers the values late)
         }
         if constexpr (ZLDS) {
 #pragma unroll
@@ -564,8 +558,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             lidx[NP + 1][threadIdx.x] = (int32_t)(uint32_t)((uint64_t)rr >> 32);
             lidx[NP + 2][threadIdx.x] = bad_index ? 1 : 0;
         }
-        const uint8_t* pslot = PL ? pp.slots + tile * pp.slot_bytes : nullptr;
-        double badi_plan = INFINITY;
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
@@ -584,108 +576,154 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         double R[NP][NP][2];
         bool bad = false;
+        bool stale_plan = false;  // PL: the plan was built for other neighbour sets (flagged as a bad index)
         double Fu, res;
         if constexpr (PL) {
-            // ---- the tile's plan (pair_plan.h): this lane's entry map and row indices first (their loads
-            // overlap the staging below), then the points, the distinct pairs, the joint block from LDS
-            constexpr int CHE = plan_map_chunks(M), CHL = plan_loc_chunks(M);
-            // (block-uniform: scalar loads and branches)
-            const int nU0 = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[0]);
-            const int nE0 = __builtin_amdgcn_readfirstlane(((const int32_t*)pslot)[1]);
-            // a region past this kernel's caps (a foreign or damaged plan) stays inside LDS and comes out NaN
-            const bool over = nU0 < 0 || nU0 > PU - 1 || nE0 < 0 || nE0 > PE - 1;
+            // ---- the wave's plan (pair_plan.h), wave-private after the table barrier: the map, the U list and
+            // the pair words are streamed in at once (fixed offsets in the wave's slot, no dependent header
+            // read), the U points' coordinates are the one dependent gather, staged at the end of the wave's
+            // LDS slice; each distinct pair is evaluated once by one lane into the slice's head; the joint
+            // block is read through the lane's map.  No block barrier after the table's.
+            constexpr int CHE = plan_map_chunks(M);
+            constexpr int PS = plan_ps(DA);
+            constexpr int UK = plan_ucap(M) / 64;  // U-list rounds (max)
+            constexpr int64_t WSB = plan_wave_slot_bytes(M);
+            const int wv = (int)(threadIdx.x >> 6), L = (int)(threadIdx.x & 63);
+            const uint8_t* wsp = pp.slots + tile * pp.slot_bytes + (int64_t)__builtin_amdgcn_readfirstlane(wv) * WSB;
+            // (wave-uniform: scalar loads and branches)
+            const int nU0 = __builtin_amdgcn_readfirstlane(((const int32_t*)wsp)[0]);
+            const int nE0 = __builtin_amdgcn_readfirstlane(((const int32_t*)wsp)[1]);
+            const int st0 = __builtin_amdgcn_readfirstlane(((const int32_t*)wsp)[2]);
+            // a foreign or damaged plan stays inside the slice and comes out NaN
+            const bool over = st0 != 0 || nU0 < 0 || nU0 > plan_ucap(M) || nE0 < 0 || nE0 > plan_ecap(M) ||
+                              !plan_fits(nU0, nE0, PS, PSL);
             const int nU = over ? 0 : nU0, nE = over ? 0 : nE0;
             bad = over;
-            // the region's first bad location
-            badi_plan = threadIdx.x == 0 ? *(const double*)(pslot + kPlanHdrBadOff) : INFINITY;
-            // the slot through a buffer descriptor (uniform base, per-lane voffset, per-load soffset: no
-            // 64-bit address arithmetic per load)
             const __amdgpu_buffer_rsrc_t srd =
-                __builtin_amdgcn_make_buffer_rsrc((void*)pslot, (short)0, (int)pp.slot_bytes, 0x00020000);
-            uint32_t mw[4 * (CHE + CHL)];
+                __builtin_amdgcn_make_buffer_rsrc((void*)wsp, (short)0, (int)WSB, 0x00020000);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            uint32_t mw[4 * CHE];
 #pragma unroll
-            for (int c = 0; c < CHE + CHL; ++c) {
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srd, kPlanMapOff + 16 * (int)threadIdx.x,
-                                                                      c * kPairbThreads * 16, 0);
+            for (int c = 0; c < CHE; ++c) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srd, plan_map_off(M) + 16 * L, c * 64 * 16, 0);
                 mw[4 * c] = v.x;
                 mw[4 * c + 1] = v.y;
                 mw[4 * c + 2] = v.z;
                 mw[4 * c + 3] = v.w;
             }
-            const int32_t* ul = (const int32_t*)(pslot + kPlanUOff);
-            for (int u = (int)threadIdx.x; u < nU; u += kPairbThreads) {
-                const int64_t g = ul[u];
-                double x[DA];
-                load_point<DA>(coords + g * ds, x);
+            const uint32_t ck = __builtin_amdgcn_raw_buffer_load_b32(srd, plan_chk_off(M) + 4 * L, 0, 0);
+            // (every round, without waiting for the header: the builder zero-fills the list)
+            int32_t ug[UK];
 #pragma unroll
-                for (int k = 0; k < DA; ++k) ucrd[(u + 1) * PCS + k] = x[k];
-                uval[u + 1] = values != nullptr ? values[g] : 0.0;
-            }
-            const int nit = (nE + kPairbThreads - 1) / kPairbThreads;  // block-uniform
-            uint32_t pwd[KE];
+            for (int k = 0; k < UK; ++k)
+                ug[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(srd, plan_u_off() + 4 * L, 256 * k, 0);
+            // pair rounds in groups of PG = 4 (the builder zero-fills the words of the last group and keeps its
+            // slots below the points): a group's words are one 16-byte load per lane (lane-major in the slot)
+            static_assert(kPlanPairGroup == 4, "one 16-byte word load per lane and group");
+            constexpr int PG = kPlanPairGroup;
+            constexpr int KG = plan_pair_groups(M);  // groups (max)
+            const int ngr = (nE + 64 * PG - 1) / (64 * PG);                 // wave-uniform
+            // (the first two groups without waiting for the header: the loop starts from them)
+            u32x4 wg[KG];
 #pragma unroll
-            for (int it = 0; it < KE; ++it)  // (words past nE inside the slot's pair area: unused)
-                pwd[it] = it < nit ? __builtin_amdgcn_raw_buffer_load_b32(srd, kPlanPairOff + 4 * (int)threadIdx.x,
-                                                                          it * kPairbThreads * 4, 0)
-                                   : 0u;
+            for (int g = 0; g < KG; ++g)
+                wg[g] = (g < 2 || g < ngr) ? __builtin_amdgcn_raw_buffer_load_b128(srd, plan_pair_off(M) + 16 * L, 1024 * g, 0)
+                                           : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
             for (int e = 0; e < kTabPer; ++e)
                 if (kPairbThreads <= NNGP_EXP_TAB_N || threadIdx.x < NNGP_EXP_TAB_N)
                     etab[threadIdx.x + e * kPairbThreads] = etab_entry[e];
-            if (threadIdx.x == 0) {
-                ptab[0] = 0.0;
-                uval[0] = 0.0;
-#pragma unroll
-                for (int c = 0; c < PCS; ++c) ucrd[c] = 0.0;  // (read by a group's unused tail)
-            }
             __syncthreads();
-            NNGP_PHASE(plan_pairs);
-            // each distinct pair once, block-cooperatively (the unplanned kernel's nngp_cov_unit on the same
-            // operands: (a - b)^2 == (b - a)^2 bit for bit)
-            // in groups of PG pairs per thread: all of a group's point reads are issued before its
-            // arithmetic, so the LDS latency overlaps (a group past nE reads slot 0 and stores nothing)
-            constexpr int PG = 4;
+            NNGP_PHASE(plan_points);
+            char* const sl = (char*)wsl + wv * PSL;  // this wave's slice
+            const int cb = PSL - nU * PS;            // its points' base
 #pragma unroll
-            for (int g = 0; g < (KE + PG - 1) / PG; ++g) {
-                if (PG * g < nit) {  // block-uniform
-                    double xa[PG][DA], xb[PG][DA];
-#pragma unroll
-                    for (int j = 0; j < PG; ++j) {
-                        const int it = PG * g + j;
-                        const uint32_t w = it < KE ? pwd[it < KE ? it : 0] : 0u;  // LDS byte offsets of both points
-                        const double* pa = (const double*)((const char*)ucrd + (w & 0xffffu));
-                        const double* pb = (const double*)((const char*)ucrd + (w >> 16));
+            for (int k = 0; k < UK; ++k) {
+                if (64 * k < nU) {  // wave-uniform
+                    const uint32_t g = (uint32_t)ug[k] < (uint32_t)n_points ? (uint32_t)ug[k] : 0u;
+                    double x[DA];
+                    load_point<DA>(coords + (int64_t)g * ds, x);
+                    if (L + 64 * k < nU) {
+                        double* pd = (double*)(sl + cb + (L + 64 * k) * PS);
                         if constexpr (DA == 2) {
-                            const double2 va = *(const double2*)pa, vb = *(const double2*)pb;
-                            xa[j][0] = va.x;
-                            xa[j][1] = va.y;
-                            xb[j][0] = vb.x;
-                            xb[j][1] = vb.y;
+                            *(double2*)pd = make_double2(x[0], x[1]);
                         } else {
 #pragma unroll
-                            for (int c = 0; c < DA; ++c) {
-                                xa[j][c] = pa[c];
-                                xb[j][c] = pb[c];
-                            }
+                            for (int c = 0; c < DA; ++c) pd[c] = x[c];
                         }
-                    }
-#pragma unroll
-                    for (int j = 0; j < PG; ++j) {
-                        const int it = PG * g + j;
-                        const int k = (int)threadIdx.x + it * kPairbThreads;
-                        if (it < KE)  // branch-free: lanes past nE store into slots past nE (no entry reads them)
-                            ptab[k + 1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(xa[j], xb[j]));
                     }
                 }
             }
-            __syncthreads();
+            // group g's words (g >= 2) wait in the covariance slots of group g - 2, [8 + 2048 (g - 2), + 1024):
+            // the loop reads them at the start of half g - 2, before that half's stores
+#pragma unroll
+            for (int g = 2; g < KG; ++g)
+                if (g < ngr) *(u32x4*)(sl + 8 + 2048 * (g - 2) + 16 * L) = wg[g];
+            // (a wave's LDS operations complete in order; the barrier keeps the compiler's order)
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            NNGP_PHASE(plan_pairs);
+            // the wave's distinct pairs: a loop over groups, software-pipelined -- group g + 1's words and point
+            // reads are in flight while group g is evaluated (the unplanned kernel's nngp_cov_unit on the same
+            // operands: (a - b)^2 == (b - a)^2 bit for bit)
+            auto pair_points = [&](const u32x4 w4, double (*xa)[DA], double (*xb)[DA]) {
+                const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (int j = 0; j < PG; ++j) {
+                    const double* pa = (const double*)(sl + (w[j] & 0xffffu));
+                    const double* pb = (const double*)(sl + (w[j] >> 16));
+                    if constexpr (DA == 2) {
+                        const double2 va = *(const double2*)pa, vb = *(const double2*)pb;
+                        xa[j][0] = va.x;
+                        xa[j][1] = va.y;
+                        xb[j][0] = vb.x;
+                        xb[j][1] = vb.y;
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < DA; ++c) {
+                            xa[j][c] = pa[c];
+                            xb[j][c] = pb[c];
+                        }
+                    }
+                }
+            };
+            // one group's covariances from its points into its slots
+            auto pair_covs = [&](int g, double (*xa)[DA], double (*xb)[DA]) {
+#pragma unroll
+                for (int j = 0; j < PG; ++j)
+                    *(double*)(sl + 8 * (1 + L + 64 * (PG * g + j))) =
+                        nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(xa[j], xb[j]));
+            };
+            // (past the last group: group 0's words, valid point offsets, read for nothing)
+            const u32x4 w0g = wg[0];
+            auto group_words = [&](int g) -> u32x4 {
+                return g < ngr ? *(const u32x4*)(sl + 8 + 2048 * (g - 2) + 16 * L) : w0g;
+            };
+            double xa0[PG][DA], xb0[PG][DA], xa1[PG][DA], xb1[PG][DA];
+            pair_points(wg[0], xa0, xb0);
+            // two groups per trip, the point registers and the word registers alternating (no copies): at a
+            // trip's start x0 holds group g's points and wA group g + 1's words; each half reads the words two
+            // groups ahead and the points one group ahead of the group it evaluates
+            u32x4 wA = wg[KG > 1 ? 1 : 0], wB;
+#pragma unroll 1
+            for (int g = 0; g < ngr; g += 2) {
+                wB = group_words(g + 2);
+                pair_points(wA, xa1, xb1);
+                pair_covs(g, xa0, xb0);
+                if (g + 1 >= ngr) break;  // wave-uniform
+                wA = group_words(g + 3);
+                pair_points(wB, xa0, xb0);
+                pair_covs(g + 1, xa1, xb1);
+            }
+            if (L == 0) *(double*)sl = 0.0;  // the exact-zero slot
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
             NNGP_PHASE(plan_fill);
             // the joint block in the unplanned kernel's register order (pair_plan.h plan_entry): entry e's
-            // LDS byte offset is u16 half e & 1 of map word e >> 1
+            // slice byte offset is u16 half e & 1 of map word e >> 1
             auto rd = [&](int e) -> double {
                 const uint32_t off = (e & 1) ? (mw[e >> 1] >> 16) : (mw[e >> 1] & 0xffffu);
-                return *(const double*)((const char*)ptab + off);
+                return *(const double*)(sl + off);
             };
             int e = 0;
 #pragma unroll
@@ -698,12 +736,12 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 R[s][s][0] = Pc.diag;
                 R[s][s][1] = rd(e++);
             }
+            // the plan belongs to this nbr / order: the lane's checksum (pair_plan.h plan_chk_*)
+            uint32_t h = plan_chk_init((uint32_t)(uint64_t)rr);
 #pragma unroll
-            for (int s = 0; s < NP; ++s) {
-                const int h = 4 * CHE + (s >> 1);
-                const uint32_t u = (s & 1) ? (mw[h] >> 16) : (mw[h] & 0xffffu);
-                z[s] = uval[u];
-            }
+            for (int s = 0; s < NP; ++s) h = plan_chk_step(h, jn[s], s);
+            const int stale = h != ck ? 1 : 0;
+            stale_plan = (stale | __builtin_amdgcn_mov_dpp(stale, 0xB1, 0xf, 0xf, true)) != 0;  // either lane of the pair
         }
         if constexpr (CM) {
             // ---- covariances from the caller's blocks, own-parity-first order.  vm: bit a set when
@@ -1008,7 +1046,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         bad |= !(Fu > 0.0);
         const double F = Fu * sigma2;  // the unit-variance pivot scaled back
         int64_t rrl = rr, il = i;
-        bool bidx = bad_index;
+        bool bidx = bad_index || stale_plan;
         if constexpr (LEFT) {
             // (the fence keeps the compiler from forwarding the stores' registers past the factorisation)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1093,7 +1131,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             NNGP_PHASE(stores);
             if (Bout != nullptr && live) {
                 // padded slots hold exact zeros (far-away points decouple exactly, nngp_math.h)
-                const double bscale = bad ? NAN : 1.0;
+                const double bscale = (bad || stale_plan) ? NAN : 1.0;
 #pragma unroll
                 for (int s = 0; s < NP; ++s) {
                     const int a = 2 * s + q;
@@ -1103,13 +1141,13 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
         }
         NNGP_PHASE(tail);
         const bool lead = live && lead0;
-        if (Fout != nullptr && lead) Fout[rrl] = bad ? NAN : F;
-        if (Rout != nullptr && lead) Rout[rrl] = bad ? NAN : res;
+        if (Fout != nullptr && lead) Fout[rrl] = (bad || stale_plan) ? NAN : F;
+        if (Rout != nullptr && lead) Rout[rrl] = (bad || stale_plan) ? NAN : res;
         // this lane's terms of the tile record (lead lanes; a NaN F -- a bad pivot -- propagates
         // into the mantissa product as log(NaN) would; the flag is what callers check)
         pairb_tile_store(lead ? __builtin_amdgcn_frexp_mant(F) : 1.0, lead ? __builtin_amdgcn_frexp_exp(F) : 0,
                          lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)il : INFINITY,
-                         PL ? badi_plan : ((live && bidx) ? (double)il : INFINITY), sh, 0, rec, lexp, tile);
+                         (live && bidx) ? (double)il : INFINITY, sh, 0, rec, lexp, tile);
         __syncthreads();
         if (fused == nullptr) {
             if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);

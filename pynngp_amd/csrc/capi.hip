@@ -62,7 +62,7 @@ int64_t bf_blocks(int64_t n_rows, int algo, int m) { return nngp::bf_record_coun
 
 extern "C" {
 
-const char* nngp_version(void) { return "pynngp_amd 0.3.0 gfx950"; }
+const char* nngp_version(void) { return "pynngp_amd 0.4.0 gfx950"; }
 
 int32_t nngp_abi_version(void) { return NNGP_ABI_VERSION; }
 
@@ -152,6 +152,9 @@ static int bf_common(const double* coords, int64_t n_points, int32_t dim, const 
         return fail(NNGP_EUNSUP, "no 4-lane kernel instantiated for m=%d (25..32)", m);
     if (a == nngp::kAlgoPairB && !nngp::bf_pairb_supported(m))
         return fail(NNGP_EUNSUP, "no blocked pair kernel instantiated for m=%d", m);
+    if (a == nngp::kAlgoPairB && kind == NNGP_COV_MATERN && m > 24)
+        return fail(NNGP_EUNSUP, "the matern kind runs on the pair kernel for m <= 24 (m=%d): use NNGP_ALGO_AUTO or "
+                                 "QUAD", m);
     const size_t need = nngp_bf_sweep_workspace_bytes(n_rows, m, kind, dim, algo);
     if (workspace_bytes < need)
         return fail(NNGP_EINVAL, "workspace too small: %zu < %zu bytes", workspace_bytes, need);
@@ -197,7 +200,7 @@ int nngp_pair_plan_build(const int32_t* nbr, const int32_t* order, int64_t n_row
     if (plan == nullptr || info == nullptr || (n_rows > 0 && nbr == nullptr))
         return fail(NNGP_EINVAL, "plan, info (and nbr for n_rows > 0) must be non-null");
     if (!nngp::bf_pairb_planned_supported(m, 0, dim))
-        return fail(NNGP_EUNSUP, "pair plans serve 2 <= m <= 18, dim 1..3 (m=%d, dim=%d)", m, dim);
+        return fail(NNGP_EUNSUP, "pair plans serve 2 <= m <= 17, dim 1..3 (m=%d, dim=%d)", m, dim);
     if (n_rows < 0 || n_rows > INT32_MAX || i0 < 0 || n_points < 1 || i0 + n_rows > n_points || n_points > INT32_MAX)
         return fail(NNGP_EINVAL, "rows [%lld, %lld) outside [0, %lld) (or n_rows / n_points >= 2^31)", (long long)i0,
                     (long long)(i0 + n_rows), (long long)n_points);
@@ -207,8 +210,7 @@ int nngp_pair_plan_build(const int32_t* nbr, const int32_t* order, int64_t n_row
     hipStream_t s = (hipStream_t)stream;
     const nngp::PairbTiling tl = nngp::pairb_tiling(n_rows, m, 0);
     if (tl.tiles != nngp::plan_regions(n_rows)) return fail(NNGP_EUNSUP, "plan regions differ from the pair tiling");
-    hipError_t e = nngp::pair_plan_build_launch(nbr, order, n_rows, m, dim, i0, n_points, tl.q, tl.rem,
-                                                nngp::plan_ecap(m, dim), plan, s);
+    hipError_t e = nngp::pair_plan_build_launch(nbr, order, n_rows, m, dim, i0, n_points, tl.q, tl.rem, plan, s);
     if (e != hipSuccess) return hip_fail(e, "pair_plan build");
     nngp::PlanHeader h;
     e = hipMemcpyAsync(&h, plan, sizeof h, hipMemcpyDeviceToHost, s);
@@ -222,6 +224,8 @@ int nngp_pair_plan_build(const int32_t* nbr, const int32_t* order, int64_t n_row
     info[5] = i0;
     info[6] = n_points;
     info[7] = nngp::kPlanMagic;
+    info[8] = (int64_t)(uintptr_t)nbr;
+    info[9] = (int64_t)(uintptr_t)order;
     return NNGP_OK;
 }
 
@@ -238,8 +242,11 @@ int nngp_bf_sweep_plan(const double* coords, int64_t n_points, int32_t dim, cons
                                  "this sweep's (%lld, %d, %d, %lld, %lld)", (long long)info[2], (long long)info[3],
                     (long long)info[4], (long long)info[5], (long long)info[6], (long long)n_rows, m, dim,
                     (long long)i0, (long long)n_points);
+    if (info[8] != (int64_t)(uintptr_t)nbr || info[9] != (int64_t)(uintptr_t)order)
+        return fail(NNGP_EINVAL, "stale plan: it was built for other nbr / order buffers (rebuild it with the "
+                                 "sweep's neighbour sets)");
     if (!nngp::bf_pairb_planned_supported(m, kind, dim))
-        return fail(NNGP_EUNSUP, "planned sweeps serve kinds 0..4, 2 <= m <= 18, dim 1..3 (kind=%d)", kind);
+        return fail(NNGP_EUNSUP, "planned sweeps serve kinds 0..4, 2 <= m <= 17, dim 1..3 (kind=%d)", kind);
     if (plan_bytes < (size_t)nngp::plan_total_bytes(n_rows, m)) return fail(NNGP_EINVAL, "plan too small");
     const int64_t nreg = nngp::plan_regions(n_rows);
     if (info[0] < 0 || info[1] < 0 || info[0] + info[1] != nreg)

@@ -207,12 +207,14 @@ __global__ __launch_bounds__(256) void color_round_kernel(const int32_t* __restr
                                                           int32_t* __restrict__ overflow, int32_t* __restrict__ maxc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    if (color[i] >= 0) return;
+    // (colours are written by other workgroups of the same launch: relaxed agent-scope atomics make the
+    // "final once written, read once" argument well defined -- no re-load or speculation of a plain load)
+    if (__hip_atomic_load(&color[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) return;
     uint64_t used[4] = {0, 0, 0, 0};
     // true when k is a lower neighbour that is still uncoloured (not ready); marks its colour otherwise
     auto lower = [&](int64_t k) -> bool {
         if (k < 0 || k >= i) return false;
-        const int32_t c = color[k];
+        const int32_t c = __hip_atomic_load(&color[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (c < 0) return true;
         used[(c >> 6) & 3] |= c < 256 ? (1ull << (c & 63)) : 0ull;
         return false;
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void color_round_kernel(const int32_t* __restr
         *overflow = 1;
         return;
     }
-    color[i] = c;
+    __hip_atomic_store(&color[i], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     atomicAdd(done, 1ull);
     atomicMax(maxc, c);
 }
@@ -791,21 +793,30 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
 // each chain's operations and their order are gibbs_w_color's (its sums, then its draw, then its
 // scatter), so chain c is still bit-identical; across chains only the interleaving of independent
 // operations changes.
+// (rows of an odd chain count are only 8-byte aligned: scalar accesses there, the same values)
 template <int C>
 __device__ __forceinline__ void il_load(const double* p, double (&v)[C]) {
+    if constexpr (C % 2 == 0) {
 #pragma unroll
-    for (int q = 0; q + 1 < C; q += 2) {
-        const double2 t = *(const double2*)(p + q);
-        v[q] = t.x;
-        v[q + 1] = t.y;
+        for (int q = 0; q < C; q += 2) {
+            const double2 t = *(const double2*)(p + q);
+            v[q] = t.x;
+            v[q + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < C; ++q) v[q] = p[q];
     }
-    if (C % 2 == 1) v[C - 1] = p[C - 1];
 }
 template <int C>
 __device__ __forceinline__ void il_store(double* p, const double (&v)[C]) {
+    if constexpr (C % 2 == 0) {
 #pragma unroll
-    for (int q = 0; q + 1 < C; q += 2) *(double2*)(p + q) = make_double2(v[q], v[q + 1]);
-    if (C % 2 == 1) p[C - 1] = v[C - 1];
+        for (int q = 0; q < C; q += 2) *(double2*)(p + q) = make_double2(v[q], v[q + 1]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < C; ++q) p[q] = v[q];
+    }
 }
 
 template <int C>

@@ -116,13 +116,13 @@ bool bf_group_supported(int m, int lanes);
 bool bf_pairb_launch(const BfArgs& a, const CovParams& P, hipStream_t s);
 bool bf_pairb_supported(int m);
 bool bf_pairb_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS (bf_pairb.h)
-// tile pair plans (pair_plan.h, pair_plan.hip)
+// wave pair plans (pair_plan.h, pair_plan.hip)
 bool bf_pairb_planned_supported(int m, int kind, int dim);
 bool bf_pairb_planned_launch(const BfArgs& a, const CovParams& P, const PlanLaunch& pl, hipStream_t s);
 hipError_t bf_launch_planned(const BfArgs& a, const PlanLaunch& pl, hipStream_t s);
 size_t pair_plan_build_lds(int m);
 hipError_t pair_plan_build_launch(const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int dim, int64_t i0,
-                                  int64_t n_points, int64_t tq, int64_t trem, int ecap, void* plan, hipStream_t s);
+                                  int64_t n_points, int64_t tq, int64_t trem, void* plan, hipStream_t s);
 bool bf_pairb_blocks_supported(int m);
 bool bf_group_blocks_launch(const BfArgs& a, hipStream_t s);  // NNGP_KIND_BLOCKS at m = 25..32 (bf_group.h)
 bool bf_group_blocks_supported(int m);

@@ -1,20 +1,22 @@
-// Tile pair plans (pair_plan.h): built once per neighbour set and visiting order, on the GPU.
+// Wave pair plans (pair_plan.h): built once per neighbour set and visiting order, on the GPU.
 //
-// One 256-thread block per region (= the pair kernel's tile: the same q / q + 1 rows of
-// pairb_tiling).  Per region:
+// One 256-thread block per wave (4 per region = the pair kernel's tile: the same q / q + 1 rows of
+// pairb_tiling; wave w of a region holds its local rows 32 w .. 32 w + 31, lanes 2 l + q).  Per wave:
 //   1. the joint points of its rows (each row's neighbours nbr[r, :] and the location i0 + order[r]
 //      itself) are sorted as (global index, position) keys in LDS (bitonic); the first of each run
-//      gets the next local index u = 1, 2, ... (ascending global index), invalid slots (-1, or out of
-//      range) keep u = 0, and rows with an index out of range are noted (the first bad location);
-//   2. every used entry (u_a, u_b) of every lane marks a bit of a 2^18-bit LDS bitmap (u <= 511: key
-//      (min - 1) << 9 | (max - 1)); popcount prefix sums over the bitmap give each distinct pair its
-//      rank in key order, i.e. the pair list sorted by (u_a, u_b) and an O(1) lookup per entry;
-//   3. the pair words, the U list and, per lane in the kernel's fill order, the entries' LDS byte
-//      offsets (8 (rank + 1); 0: exact-zero slot) and the rows' local indices are written to the
-//      region's fixed-size slot.
-// Regions past the caps (nU > plan_ucap or nE > plan_ecap(m, dim)) are marked direct.  A last
-// single-block kernel lists planned and direct regions in order; the host reads the two counts once
-// (nngp_pair_plan_build synchronises: a setup call, like the neighbour build).
+//      gets the next local index u = 0, 1, ... (ascending global index); invalid slots (-1, or out of
+//      range) get none and read the exact-zero covariance;
+//   2. every used entry (u_a, u_b) of every lane marks a bit of a 2^16-bit LDS bitmap (u < 256: key
+//      min << 8 | max); popcount prefix sums over the bitmap give each distinct pair its rank k in key
+//      order -- pair k is evaluated by lane k % 64 in round k / 64 into slice byte 8 (k + 1);
+//   3. the U list (zero-filled to whole rounds of 64), the pair words (the points' slice byte offsets,
+//      zero-filled to whole groups of kPlanPairGroup rounds; plan_pair_word's lane-major order), per
+//      lane in the kernel's fill order the entries' slice byte offsets, and per lane the checksum of the
+//      nbr / order words the kernel will read (pair_plan.h) are written to the wave's fixed-size slot.
+// Waves past the caps (nU > plan_ucap, or the covariances and the points not fitting the slice) are
+// marked; a region is planned only when all its waves are.  A last single-block kernel lists planned and
+// direct regions in order; the host reads the two counts once (nngp_pair_plan_build synchronises: a
+// setup call, like the neighbour build).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,7 +27,7 @@ namespace nngp {
 
 namespace {
 
-constexpr int kBitWords = (1 << 18) / 32;  // 8192 words: keys (u_a - 1) << 9 | (u_b - 1), u <= 511
+constexpr int kBitWords = (1 << 16) / 32;  // 2048 words: keys u_a << 8 | u_b, u < 256
 
 // exclusive prefix sum over the block's 256 threads (every thread calls it); returns the total in *tot
 __device__ int block_scan_excl(int v, int* sh, int* tot) {
@@ -49,50 +51,46 @@ __device__ int block_scan_excl(int v, int* sh, int* tot) {
     return base + x - v;
 }
 
-__global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
+__global__ __launch_bounds__(kPlanThreads) void wave_plan_build_kernel(
     const int32_t* __restrict__ nbr, const int32_t* __restrict__ order, int64_t n_rows, int m, int64_t i0,
-    int64_t n_points, int64_t tq, int64_t trem, uint8_t* __restrict__ plan, int64_t slot_bytes, int ucap, int ecap,
-    int ps) {
+    int64_t n_points, int64_t tq, int64_t trem, uint8_t* __restrict__ slots, int ps) {
     extern __shared__ uint64_t pp_lds[];
     __shared__ int scan_sh[kPlanThreads / 64];
-    __shared__ double bad_sh[kPlanThreads / 64];
     const int t = threadIdx.x;
-    const int64_t region = blockIdx.x;
+    const int64_t region = blockIdx.x / kPlanWaves;
+    const int wv = (int)(blockIdx.x % kPlanWaves);
     const int nr = (int)(tq + (region < trem ? 1 : 0));
     const int64_t r0 = region * tq + (region < trem ? region : trem);
     const int NR = m + 1, NP = plan_np(m), NE = plan_entries(m);
-    const int npos = kPlanThreads / 2 * NR;  // (local row, joint row) positions
+    const int npos = kPlanWaveRows * NR;  // (wave row, joint row) positions
     int nsort = 1;
     while (nsort < npos) nsort <<= 1;
     uint64_t* key = pp_lds;                                      // nsort
-    uint16_t* loc = (uint16_t*)(key + nsort);                    // npos (+ pad)
+    int16_t* loc = (int16_t*)(key + nsort);                      // npos (+ pad): local index or -1
     uint32_t* bits = (uint32_t*)(loc + ((npos + 7) & ~7));       // kBitWords
     uint32_t* pref = bits + kBitWords;                           // kBitWords
-    uint8_t* slot = plan + kPlanGlobalHdr + region * slot_bytes;
+    const int64_t wsb = plan_wave_slot_bytes(m);
+    uint8_t* slot = slots + (region * kPlanWaves + wv) * wsb;
+    int32_t* hdr = (int32_t*)slot;
+    const int slice = plan_slice_bytes(m), ecap = plan_ecap(m), ucap = plan_ucap(m);
 
     // ---- 1. the joint points, sorted by (global index, position)
-    double bad = INFINITY;
     for (int p = t; p < nsort; p += kPlanThreads) {
         uint64_t k = ~0ull;
         if (p < npos) {
-            const int lr = p / NR, a = p % NR;
+            const int l = p / NR, a = p % NR;
+            const int lr = kPlanWaveRows * wv + l;
             if (lr < nr) {
                 const int64_t r = r0 + lr;
                 const int64_t rr = order != nullptr ? (int64_t)order[r] : r;
-                const int64_t i = i0 + rr;
-                int64_t j = i;
-                if (a < m) {
-                    j = nbr[r * m + a];
-                    if (j >= n_points || j < -1) bad = fmin(bad, (double)i);
-                }
+                int64_t j = i0 + rr;
+                if (a < m) j = nbr[r * m + a];
                 if (j >= 0 && j < n_points) k = ((uint64_t)j << 32) | (uint64_t)p;
             }
-            loc[p] = 0;
+            loc[p] = -1;
         }
         key[p] = k;
     }
-    bad = wave_min(bad);
-    if ((t & 63) == 0) bad_sh[t >> 6] = bad;
     __syncthreads();
     for (int k = 2; k <= nsort; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -109,92 +107,90 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
             __syncthreads();
         }
     }
-    // local indices: u = inclusive count of run starts (a thread scans a contiguous chunk)
-    const int per = nsort / kPlanThreads;  // nsort >= 512 (m >= 2)
-    const int c0 = t * per, c1 = c0 + per;
-    int cnt = 0;
-    for (int p = c0; p < c1; ++p) {
+    // local indices: u = count of run starts before (a thread scans a contiguous chunk)
+    const int per = (nsort + kPlanThreads - 1) / kPlanThreads;
+    const int c0 = t * per < nsort ? t * per : nsort, c1 = c0 + per < nsort ? c0 + per : nsort;
+    auto run_start = [&](int p) -> bool {
         const uint64_t k = key[p];
-        const bool start = k != ~0ull && (p == 0 || (key[p - 1] >> 32) != (k >> 32));
-        cnt += start ? 1 : 0;
-    }
+        return k != ~0ull && (p == 0 || (key[p - 1] >> 32) != (k >> 32));
+    };
+    int cnt = 0;
+    for (int p = c0; p < c1; ++p) cnt += run_start(p) ? 1 : 0;
     int nU;
-    int u = block_scan_excl(cnt, scan_sh, &nU);
-    int32_t* ulist = (int32_t*)(slot + kPlanUOff);
+    int u = block_scan_excl(cnt, scan_sh, &nU) - 1;
+    int32_t* ulist = (int32_t*)(slot + plan_u_off());
     for (int p = c0; p < c1; ++p) {
         const uint64_t k = key[p];
         if (k == ~0ull) break;
-        if (p == 0 || (key[p - 1] >> 32) != (k >> 32)) {
+        if (run_start(p)) {
             ++u;
-            if (u <= ucap) ulist[u - 1] = (int32_t)(k >> 32);
+            if (u < ucap) ulist[u] = (int32_t)(k >> 32);
         }
-        loc[k & 0xffffffffu] = (uint16_t)(u <= ucap ? u : 0);
+        if (u < ucap) loc[k & 0xffffffffu] = (int16_t)u;
     }
-    double badr = INFINITY;
-#pragma unroll
-    for (int w = 0; w < kPlanThreads / 64; ++w) badr = fmin(badr, bad_sh[w]);
-    int32_t* hdr = (int32_t*)slot;
     if (nU > ucap) {
         if (t == 0) {
             hdr[0] = nU;
             hdr[1] = -1;
             hdr[2] = 1;
-            *(double*)(slot + kPlanHdrBadOff) = badr;
         }
         return;
     }
+    for (int x = nU + t; x < ucap; x += kPlanThreads) ulist[x] = 0;  // (the kernel loads every round: point 0)
     for (int w = t; w < kBitWords; w += kPlanThreads) bits[w] = 0;
     __syncthreads();
 
-    // ---- 2. mark the used pairs: thread t is lane q = t & 1 of local row t >> 1
-    const int lr = t >> 1, q = t & 1;
-    const bool live = lr < nr;
-    auto pair_key = [&](int e, int* key_out) -> bool {
+    // ---- 2. mark the used pairs: threads 0..63 are the wave's lanes (lane L: wave row L >> 1, q = L & 1)
+    auto pair_key = [&](int L, int e, int* key_out) -> bool {
+        const int l = L >> 1, q = L & 1;
+        if (kPlanWaveRows * wv + l >= nr) return false;
         int a, b;
         plan_entry(NP, q, e, &a, &b);
-        if (!live || a < 0 || a > m || b > m) return false;
-        const int ua = loc[lr * NR + a], ub = loc[lr * NR + b];
-        if (ua == 0 || ub == 0) return false;
-        const int lo = ua < ub ? ua : ub, hi = ua < ub ? ub : ua;
-        *key_out = ((lo - 1) << 9) | (hi - 1);
+        if (a < 0 || a > m || b > m) return false;
+        const int ua = loc[l * NR + a], ub = loc[l * NR + b];
+        if (ua < 0 || ub < 0) return false;
+        *key_out = ua < ub ? (ua << 8) | ub : (ub << 8) | ua;
         return true;
     };
-    for (int e = 0; e < NE; ++e) {
+    for (int x = t; x < 64 * NE; x += kPlanThreads) {
         int k;
-        if (pair_key(e, &k)) atomicOr(&bits[k >> 5], 1u << (k & 31));
+        if (pair_key(x / NE, x % NE, &k)) atomicOr(&bits[k >> 5], 1u << (k & 31));
     }
     __syncthreads();
-    // ---- 3. ranks: popcount prefix over the bitmap (thread t: words [32 t, 32 t + 32))
+    // ---- 3. ranks: popcount prefix over the bitmap (thread t: words [8 t, 8 t + 8))
+    constexpr int WPT = kBitWords / kPlanThreads;
     int pc = 0;
-    for (int w = 32 * t; w < 32 * t + 32; ++w) pc += __popc(bits[w]);
+    for (int w = WPT * t; w < WPT * t + WPT; ++w) pc += __popc(bits[w]);
     int nE;
     int base = block_scan_excl(pc, scan_sh, &nE);
-    if (nE > ecap) {
+    const int cb = slice - nU * ps;  // the points' base in the slice
+    if (nE > ecap || !plan_fits(nU, nE, ps, slice)) {
         if (t == 0) {
             hdr[0] = nU;
             hdr[1] = nE;
             hdr[2] = 1;
-            *(double*)(slot + kPlanHdrBadOff) = badr;
         }
         return;
     }
-    uint32_t* pw = (uint32_t*)(slot + kPlanPairOff);
-    for (int w = 32 * t; w < 32 * t + 32; ++w) {
+    uint32_t* pw = (uint32_t*)(slot + plan_pair_off(m));
+    for (int w = WPT * t; w < WPT * t + WPT; ++w) {
         pref[w] = (uint32_t)base;
         uint32_t x = bits[w];
         while (x != 0u) {
             const int bit = __ffs(x) - 1;
             x &= x - 1u;
             const int k = (w << 5) | bit;
-            // the planned kernel's LDS byte offsets of the two points (u * ps, u <= 511: < 2^16)
-            pw[base++] = (uint32_t)(((k >> 9) + 1) * ps) | ((uint32_t)(((k & 511) + 1) * ps) << 16);
+            // the slice byte offsets of the two points (< slice <= 2^16)
+            pw[plan_pair_word(base++)] = (uint32_t)(cb + (k >> 8) * ps) | ((uint32_t)(cb + (k & 255) * ps) << 16);
         }
     }
+    for (int x = nE + t; x < plan_pair_slots(nE) - 1; x += kPlanThreads) pw[plan_pair_word(x)] = 0u;  // whole groups
     __syncthreads();
-    // ---- 4. this lane's map: entry offsets (u16 pairs in dwords, 4 dwords per chunk), then row indices
-    uint32_t* mp = (uint32_t*)(slot + kPlanMapOff);
-    const int CHE = plan_map_chunks(m), CHL = plan_loc_chunks(m);
-    for (int c = 0; c < CHE; ++c) {
+    // ---- 4. the lanes' maps (slice byte offsets 8 (rank + 1); 0: the exact-zero slot) and checksums
+    uint32_t* mp = (uint32_t*)(slot + plan_map_off(m));
+    const int CHE = plan_map_chunks(m);
+    for (int x = t; x < 64 * CHE; x += kPlanThreads) {
+        const int L = x & 63, c = x >> 6;
         uint32_t d[4];
         for (int k = 0; k < 4; ++k) {
             uint32_t v = 0;
@@ -202,7 +198,7 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
                 const int e = 8 * c + 2 * k + h;
                 int key2;
                 uint32_t off = 0;
-                if (e < NE && pair_key(e, &key2)) {
+                if (e < NE && pair_key(L, e, &key2)) {
                     const uint32_t wd = bits[key2 >> 5];
                     const uint32_t rank = pref[key2 >> 5] + __popc(wd & ((1u << (key2 & 31)) - 1u));
                     off = (rank + 1u) * 8u;
@@ -211,33 +207,33 @@ __global__ __launch_bounds__(kPlanThreads) void pair_plan_build_kernel(
             }
             d[k] = v;
         }
-        *(uint4*)(mp + 4 * ((int64_t)c * kPlanThreads + t)) = make_uint4(d[0], d[1], d[2], d[3]);
+        *(uint4*)(mp + 4 * ((int64_t)c * 64 + L)) = make_uint4(d[0], d[1], d[2], d[3]);
     }
-    for (int c = 0; c < CHL; ++c) {
-        uint32_t d[4];
-        for (int k = 0; k < 4; ++k) {
-            uint32_t v = 0;
-            for (int h = 0; h < 2; ++h) {
-                const int s = 8 * c + 2 * k + h, a = 2 * s + q;
-                const uint32_t ua = (live && s < NP && a <= m) ? loc[lr * NR + a] : 0u;
-                v |= ua << (16 * h);
-            }
-            d[k] = v;
+    if (t < 64) {
+        // the words the kernel reads for lane t (bf_pairb.h: dead lanes read the last row)
+        const int lr = kPlanWaveRows * wv + (t >> 1), q = t & 1;
+        const int64_t rl = lr < nr ? r0 + lr : n_rows - 1;
+        const int32_t ov = (order != nullptr ? order : nbr)[rl];
+        const int64_t rr = order != nullptr ? (int64_t)ov : rl;
+        uint32_t h = plan_chk_init((uint32_t)(uint64_t)rr);
+        for (int s = 0; s < NP; ++s) {
+            const int a = 2 * s + q;
+            h = plan_chk_step(h, nbr[rl * m + (a < m ? a : m - 1)], s);
         }
-        *(uint4*)(mp + 4 * ((int64_t)(CHE + c) * kPlanThreads + t)) = make_uint4(d[0], d[1], d[2], d[3]);
+        ((uint32_t*)(slot + plan_chk_off(m)))[t] = h;
     }
     if (t == 0) {
         hdr[0] = nU;
         hdr[1] = nE;
         hdr[2] = 0;
-        *(double*)(slot + kPlanHdrBadOff) = badr;
     }
 }
 
-// planned / direct region lists in region order, and the counts into the global header
-// (status: word 2 of each region slot's header, written by pair_plan_build_kernel)
+// planned / direct region lists in region order, and the counts into the global header (a region is
+// planned when all its waves are: status word 2 of each wave slot, written by wave_plan_build_kernel)
 __global__ __launch_bounds__(1024) void pair_plan_lists_kernel(const uint8_t* __restrict__ slots, int64_t slot_bytes,
-                                                               int64_t n_regions, int32_t* __restrict__ planned,
+                                                               int64_t wave_slot_bytes, int64_t n_regions,
+                                                               int32_t* __restrict__ planned,
                                                                int32_t* __restrict__ direct, PlanHeader* hdr) {
     __shared__ int sh[16];
     __shared__ int64_t carry[2];
@@ -246,7 +242,12 @@ __global__ __launch_bounds__(1024) void pair_plan_lists_kernel(const uint8_t* __
     __syncthreads();
     for (int64_t b = 0; b < n_regions; b += 1024) {
         const int64_t r = b + t;
-        const int st = r < n_regions ? ((const int32_t*)(slots + r * slot_bytes))[2] : -1;
+        int st = -1;
+        if (r < n_regions) {
+            st = 0;
+            for (int k = 0; k < kPlanWaves; ++k)
+                st |= ((const int32_t*)(slots + r * slot_bytes + k * wave_slot_bytes))[2] != 0 ? 1 : 0;
+        }
         const int isp = st == 0 ? 1 : 0;
         int x = isp;
 #pragma unroll
@@ -282,14 +283,14 @@ __global__ __launch_bounds__(1024) void pair_plan_lists_kernel(const uint8_t* __
 }  // namespace
 
 size_t pair_plan_build_lds(int m) {
-    const int npos = kPlanThreads / 2 * (m + 1);
+    const int npos = kPlanWaveRows * (m + 1);
     int nsort = 1;
     while (nsort < npos) nsort <<= 1;
     return (size_t)nsort * 8 + (size_t)((npos + 7) & ~7) * 2 + (size_t)kBitWords * 8;
 }
 
 hipError_t pair_plan_build_launch(const int32_t* nbr, const int32_t* order, int64_t n_rows, int m, int dim, int64_t i0,
-                                  int64_t n_points, int64_t tq, int64_t trem, int ecap, void* plan, hipStream_t s) {
+                                  int64_t n_points, int64_t tq, int64_t trem, void* plan, hipStream_t s) {
     const int64_t nreg = plan_regions(n_rows);
     const int64_t sb = plan_slot_bytes(m);
     uint8_t* p = (uint8_t*)plan;
@@ -300,12 +301,12 @@ hipError_t pair_plan_build_launch(const int32_t* nbr, const int32_t* order, int6
     if (e != hipSuccess) return e;
     if (nreg == 0) return hipSuccess;
     const size_t lds = pair_plan_build_lds(m);
-    hipLaunchKernelGGL(pair_plan_build_kernel, dim3((unsigned)nreg), dim3(kPlanThreads), lds, s, nbr, order, n_rows, m,
-                       i0, n_points, tq, trem, p, sb, plan_ucap(), ecap, 8 * plan_cs(dim));
+    hipLaunchKernelGGL(wave_plan_build_kernel, dim3((unsigned)(nreg * kPlanWaves)), dim3(kPlanThreads), lds, s, nbr,
+                       order, n_rows, m, i0, n_points, tq, trem, p + kPlanGlobalHdr, plan_ps(dim));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pair_plan_lists_kernel, dim3(1), dim3(1024), 0, s, (const uint8_t*)(p + kPlanGlobalHdr), sb, nreg,
-                       planned, direct, (PlanHeader*)p);
+    hipLaunchKernelGGL(pair_plan_lists_kernel, dim3(1), dim3(1024), 0, s, (const uint8_t*)(p + kPlanGlobalHdr), sb,
+                       plan_wave_slot_bytes(m), nreg, planned, direct, (PlanHeader*)p);
     return hipGetLastError();
 }
 

@@ -134,7 +134,7 @@ void bf_sweep_out(const at::Tensor& coords, const at::Tensor& nbr, const c10::op
     TORCH_CHECK(ws.is_contiguous(), "workspace must be contiguous");
     check_same_device(coords, ws, "workspace");
     if (plan.has_value()) {
-        // a tile pair plan (pair_plan op): the pair kernel with every shared covariance evaluated once per tile
+        // a wave pair plan (pair_plan op): the pair kernel with every shared covariance evaluated once per wave
         TORCH_CHECK(plan_info.has_value() && plan_info->device().is_cpu() && plan_info->scalar_type() == at::kLong &&
                         plan_info->numel() == NNGP_PLAN_INFO_LEN && plan_info->is_contiguous(),
                     "plan_info must be the pair_plan op's CPU int64 (", NNGP_PLAN_INFO_LEN, ",) tensor");
@@ -206,7 +206,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bf_cross(const at::Tensor& ref, c
     return {B, F, mean};
 }
 
-// the tile pair plan of a sweep over nbr (include/nngp.h nngp_pair_plan_build): (plan bytes on the GPU,
+// the wave pair plan of a sweep over nbr (include/nngp.h nngp_pair_plan_build): (plan bytes on the GPU,
 // CPU int64 info).  A setup call: it synchronises the tensors' stream once.
 std::tuple<at::Tensor, at::Tensor> pair_plan(const at::Tensor& nbr, const c10::optional<at::Tensor>& order, int64_t i0,
                                              int64_t n_points, int64_t dim) {
@@ -220,7 +220,7 @@ std::tuple<at::Tensor, at::Tensor> pair_plan(const at::Tensor& nbr, const c10::o
         check_same_device(nbr, *order, "order");
     }
     const size_t bytes = nngp_pair_plan_bytes(rows, (int32_t)m, (int32_t)dim);
-    TORCH_CHECK(bytes > 0, "no pair plans for m=", m, ", dim=", dim, " (2 <= m <= 18, dim 1..3)");
+    TORCH_CHECK(bytes > 0, "no pair plans for m=", m, ", dim=", dim, " (2 <= m <= 17, dim 1..3)");
     auto plan = workspace((int64_t)bytes, nbr);
     auto info = at::empty({NNGP_PLAN_INFO_LEN}, at::TensorOptions().dtype(at::kLong));
     check_rc(nngp_pair_plan_build(nbr.data_ptr<int32_t>(), ptr<int32_t>(order), rows, (int32_t)m, i0, n_points,

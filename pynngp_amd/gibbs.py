@@ -106,8 +106,8 @@ class SeqNNGP:
     nngp.py:45-47: the uniform 5-NN mean of the observed responses at every node).
     """
 
-    # the whole-field phi sweeps through a tile pair plan?  Off: slower than the unplanned kernel
-    # (sweep.PLAN_DEFAULT, profiles/r05f); set True on an instance's class to opt in
+    # the whole-field phi sweeps through a wave pair plan?  Off: slower than the unplanned kernel
+    # (sweep.PLAN_DEFAULT, profiles/r06c); set True on an instance's class to opt in
     _use_plan = False
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
@@ -337,8 +337,8 @@ class SeqNNGP:
         else:
             self._ws = _lib.bf_workspace(n, self.m, algo, dev, kind=kind, dim=self.coords.shape[1])
             self._kind_code, self._algo_code = ops.kind_code(kind), ops.algo_code(algo)
-        # tile pair plan for the phi-proposal sweeps (pair_plan.h; the same B / F / r bits, each shared
-        # covariance of a tile evaluated once): built once, the DAG never changes
+        # wave pair plan for the phi-proposal sweeps (pair_plan.h; the same B / F / r bits, each shared
+        # covariance of a wavefront evaluated once): built once, the DAG never changes
         self._plan = (None, None)
         if (self._use_plan and self._custom is None and algo in ("auto", "pairb")
                 and _lib.pair_plan_supported(self.m, kind, self.coords.shape[1])):

@@ -16,7 +16,7 @@ for tracing.
     torch.ops.nngp.bf_sweep_out(coords, nbr, order, i0, kind, sigma2, phi, tau2, values, B, F, R, partials,
                                 workspace, algo, nu=-1.0, plan=None, plan_info=None) -> ()
                                                                       # the hot path: caller-owned buffers
-    torch.ops.nngp.pair_plan(nbr, order, i0, n_points, dim) -> (plan, plan_info)   # tile pair plan (setup)
+    torch.ops.nngp.pair_plan(nbr, order, i0, n_points, dim) -> (plan, plan_info)   # wave pair plan (setup)
     torch.ops.nngp.bf_cross(ref, query, nbr, kind, sigma2, phi, tau2, ref_values, algo, nu=-1.0) -> (B, F, mean)
     torch.ops.nngp.row_order(coords, i0, rows, nbr) -> (order, nbr_sorted)
     torch.ops.nngp.combine_partials_out(gathered, out) -> ()
@@ -132,7 +132,7 @@ def bf_sweep_out(coords, nbr, order, i0, kind: str, theta, values, B, F, R, part
 
 
 def pair_plan(nbr, order, i0: int, n_points: int, dim: int):
-    """The tile pair plan of a sweep over ``nbr`` (``torch.ops.nngp.pair_plan``): ``(plan, plan_info)``.
+    """The wave pair plan of a sweep over ``nbr`` (``torch.ops.nngp.pair_plan``): ``(plan, plan_info)``.
     A setup call (one host synchronisation); stale once nbr or order change."""
     load()
     return torch.ops.nngp.pair_plan(nbr, order, int(i0), int(n_points), int(dim))

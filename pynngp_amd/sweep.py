@@ -27,10 +27,11 @@ from . import _lib, ops
 from .nngp import Covariance, LOG_2PI, _raise_on_bad
 
 
-# ShardedLogLik(plan=None): sweep through a tile pair plan (pair_plan.h)?  Off by default: measured on the
-# same box (profiles/r05f), the planned kernel executes 28 % fewer VALU instructions at m = 15 but runs 20 %
-# longer (176.8 -> 212.2 us at N = 1e6; config 2 28.1 -> 30.2 us): its plan loads and the two barriers
-# around the shared evaluation leave the memory latency exposed at two blocks per CU.  plan=True opts in.
+# ShardedLogLik(plan=None): sweep through a wave pair plan (pair_plan.h)?  Off by default: measured on the
+# same box (profiles/r06a, r06c), the planned kernel executes 19.5 % fewer VALU instructions
+# at m = 15 but the sweep takes 0.230 against 0.172 ms at N = 1e6 -- the plan's ~420 B per location are a
+# dependent HBM stream at every wave's start, and the shared covariances' LDS round trips cost what the saved
+# instructions buy (a cache-resident plan: 0.180 ms).  plan=True opts in.
 PLAN_DEFAULT = False
 
 
@@ -145,10 +146,11 @@ class ShardedLogLik:
             self._partials = torch.empty(4, dtype=torch.float64, device=coords.device)
             self._B = torch.empty((self.hi - self.lo, self.m), dtype=torch.float64, device=coords.device)
             self._F = torch.empty((self.hi - self.lo,), dtype=torch.float64, device=coords.device)
-        # tile pair plan (pair_plan.h): every covariance a sweep tile shares evaluated once; built once here
+        # wave pair plan (pair_plan.h): every covariance a wavefront shares evaluated once; built once here
         # (one host synchronisation), used by every sweep of a kind it serves.  plan=None: when supported.
         self._plan = self._plan_ctypes = None
         self.plan_build_s = 0.0
+        self.plan_read_bytes = 0  # bytes a planned sweep streams from the plan (_lib.pair_plan_read_bytes)
         want = plan if plan is not None else PLAN_DEFAULT
         d = coords.shape[1]
         if (compute is None and want and self.hi > self.lo and algo in ("auto", "pairb")
@@ -157,8 +159,9 @@ class ShardedLogLik:
             self._plan = ops.pair_plan(self._nbr_sweep, self.order, self.lo, self.n, d)
             self.plan_build_s = time.perf_counter() - t0
             self._plan_ctypes = _lib.PairPlan(self._plan[0], self._plan[1].tolist(), self._nbr_sweep, self.order)
+            self.plan_read_bytes = _lib.pair_plan_read_bytes(self._plan[0], self.m)
         elif plan:
-            raise ValueError(f"pair plans serve algo auto / pairb, 2 <= m <= 18, dim 1..3 (m={self.m}, dim={d})")
+            raise ValueError(f"pair plans serve algo auto / pairb, 2 <= m <= 17, dim 1..3 (m={self.m}, dim={d})")
 
     @property
     def planned(self) -> bool:

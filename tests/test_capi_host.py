@@ -105,6 +105,8 @@ def _sweep(lib, **kw):
     (dict(kind=5, nu=float("nan")), -1, "nu"),
     (dict(kind=5, nu=1.2, algo=1, m=8), -4, "pair (m <= 24), four-lane (25..32) or wavefront kernel"),
     (dict(kind=5, nu=0.3, algo=1, m=8), -4, "pair (m <= 24), four-lane (25..32) or wavefront kernel"),
+    (dict(kind=5, nu=1.5, algo=5, m=25), -4, "matern kind runs on the pair kernel for m <= 24"),  # (advice r05)
+    (dict(kind=5, nu=1.5, algo=5, m=32), -4, "matern kind runs on the pair kernel for m <= 24"),
 ])
 def test_bf_sweep_rejects(lib, kw, code, msg):
     assert _sweep(lib, **kw) == code
@@ -214,7 +216,7 @@ def test_blocks_entry_points_reject(lib):
     assert lib.nngp_bf_sweep_blocks(*args(m=33)) == -4
     assert "m <= 32" in lib.nngp_last_error().decode()
     assert lib.nngp_bf_sweep_blocks(*args(m=0)) == -4
-    assert lib.nngp_abi_version() == 3 and b"0.3.0" in lib.nngp_version()
+    assert lib.nngp_abi_version() == 4 and b"0.4.0" in lib.nngp_version()
     assert lib.nngp_bf_sweep_blocks(*args(cov=None)) == -1
     assert lib.nngp_joint_dist(P(256), 10, 4, P(256), 10, P(256), None, 10, 5, 0, P(256), None) == -4
     assert lib.nngp_joint_dist(P(256), 10, 2, P(256), 10, P(256), None, 11, 5, 0, P(256), None) == -1

@@ -1,12 +1,12 @@
-"""GPU parity: tile pair plans (nngp_pair_plan_build / nngp_bf_sweep_plan, pair_plan.h).
+"""GPU parity: wave pair plans (nngp_pair_plan_build / nngp_bf_sweep_plan, pair_plan.h).
 
-A planned sweep evaluates every covariance a tile's locations share once, into LDS, and factors
-each location's joint block from there.  Covariances are symmetric bit for bit ((a - b)^2 == (b - a)^2
+A planned sweep evaluates every covariance a wavefront's locations share once, into the wave's LDS
+slice, and factors each location's joint block from there.  Covariances are symmetric bit for bit ((a - b)^2 == (b - a)^2
 in IEEE arithmetic) and everything after them is the unplanned pair kernel's code, so the bar is
 EXACT equality with the unplanned sweep (NNGP_ALGO_PAIRB) on the same arguments: B, F, the residuals
-R and the four partials, for every kind the plans serve, m = 2..18, dimensions 1..3, with and without
+R and the four partials, for every kind the plans serve, m = 2..17, dimensions 1..3, with and without
 a visiting order, shards (i0 > 0), padded first rows, invalid neighbour indices, and tiles that
-exceed the LDS budget (swept by the unplanned kernel into the same records).  The unplanned kernel
+exceed the LDS budget (swept by the unplanned kernel into the same records), and stale plans.  The unplanned kernel
 itself is held to the C oracle by tests/test_gpu_bf.py and tests/test_gpu_fullsize.py; one case here
 also checks the planned sweep against the oracle directly.
 """
@@ -67,7 +67,7 @@ def test_plan_equals_unplanned_every_kind(dev, lib, kind):
     assert float(a[3][2]) == -1.0 and float(a[3][3]) == -1.0
 
 
-@pytest.mark.parametrize("m", list(range(2, 19)))
+@pytest.mark.parametrize("m", list(range(2, 18)))
 def test_plan_equals_unplanned_every_m(dev, lib, m):
     c, v = _field(dev, 9_000, 2, m)
     nbr = lib.knn_prior(c, m)
@@ -79,14 +79,16 @@ def test_plan_equals_unplanned_every_m(dev, lib, m):
 
 
 @pytest.mark.parametrize("dim", [1, 3])
-@pytest.mark.parametrize("m", [5, 10, 15, 18])
+@pytest.mark.parametrize("m", [5, 10, 15, 17])
 def test_plan_equals_unplanned_dims(dev, lib, dim, m):
     c, v = _field(dev, 12_000, dim, 10 * dim + m)
     nbr = lib.knn_prior(c, m)
     order, nbr_s = lib.row_order(c, 0, c.shape[0], nbr)
     for kind in ("exponential", "gaussian"):
         (a, b), plan = _both(lib, c, nbr_s, kind, THETA[kind], v, order=order)
-        assert plan.n_planned > 0
+        # (3-D points take 32 bytes of LDS each and a sparse 3-D field shares fewer pairs: at m >= 15 the
+        # waves of this 12,000-point field overflow their slices and every tile is direct -- still exact)
+        assert plan.n_planned > 0 or (dim == 3 and m >= 15)
         _assert_same(a, b)
 
 
@@ -125,7 +127,7 @@ def test_plan_shard_rows_i0(dev, lib):
 
 def test_plan_padding_rows_small_fields(dev, lib):
     """rows i < m (padded slots, exact zeros), fields smaller than one tile, one row"""
-    for n, m in ((1, 5), (2, 5), (17, 15), (127, 15), (128, 15), (129, 15), (300, 18)):
+    for n, m in ((1, 5), (2, 5), (17, 15), (127, 15), (128, 15), (129, 15), (300, 17)):
         c, v = _field(dev, n, 2, n)
         nbr = lib.knn_prior(c, m)
         (a, b), plan = _both(lib, c, nbr, "exponential", THETA["exponential"], v)
@@ -188,12 +190,55 @@ def test_plan_geometry_mismatch_rejected(dev, lib):
     c, v = _field(dev, 5_000, 2, 17)
     nbr = lib.knn_prior(c, 10, 1_000, 3_000)
     plan = lib.pair_plan(nbr, c.shape[0], 2, i0=1_000)
-    with pytest.raises(lib.NNGPExtensionError):
+    # (PairPlan.matches refuses these in Python; the C ABI checks the same geometry)
+    with pytest.raises((ValueError, lib.NNGPExtensionError)):
         lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 30.0, 0.0, values=v, plan=plan)  # i0 differs
-    with pytest.raises(lib.NNGPExtensionError):
+    with pytest.raises((ValueError, lib.NNGPExtensionError)):
         lib.bf_sweep(c, nbr[:1_500], 1_000, "exponential", 1.0, 30.0, 0.0, values=v, plan=plan)  # rows differ
     with pytest.raises(lib.NNGPExtensionError):
         lib.bf_sweep(c, nbr, 1_000, "matern", 1.0, 30.0, 0.0, values=v, plan=plan, nu=1.3)  # kind not served
+
+
+def test_plan_stale_rejected_or_flagged(dev, lib):
+    """a plan of other neighbour sets: another buffer is refused (Python and the C ABI); the same buffer
+    changed in place is refused by PairPlan.matches (torch's version counter) and, reached through the C
+    ABI anyway, flagged by the kernel's per-location checksum with NaN B / F"""
+    import ctypes
+
+    c, v = _field(dev, 20_000, 2, 19)
+    order, nbr = lib.row_order(c, 0, c.shape[0], lib.knn_prior(c, 15))  # (Z-order: planned waves)
+    plan = lib.pair_plan(nbr, c.shape[0], 2, order=order)
+    assert plan.n_planned > 0.8 * (plan.n_planned + plan.n_direct)
+    other = nbr.clone()
+    with pytest.raises(ValueError, match="stale"):
+        lib.bf_sweep(c, other, 0, "exponential", 1.0, 30.0, 0.0, values=v, plan=plan, order=order)
+    rows_changed = list(range(500, 20_000, 500))
+    for t in rows_changed:  # swap two neighbours in place
+        nbr[t, 3], nbr[t, 4] = int(nbr[t, 4]), int(nbr[t, 3])
+    with pytest.raises(ValueError, match="stale"):
+        lib.bf_sweep(c, nbr, 0, "exponential", 1.0, 30.0, 0.0, values=v, plan=plan, order=order)
+    # the C ABI directly (its pointer check passes: same buffer): the kernel flags the changed location
+    L = lib.load()
+    rows, m = nbr.shape
+    B = torch.empty((rows, m), dtype=torch.float64, device=dev)
+    F = torch.empty(rows, dtype=torch.float64, device=dev)
+    p = torch.empty(4, dtype=torch.float64, device=dev)
+    ws = lib.bf_workspace(rows, m, "pairb", dev)
+    P = ctypes.c_void_p
+    rc = L.nngp_bf_sweep_plan(P(c.data_ptr()), c.shape[0], 2, P(nbr.data_ptr()), P(order.data_ptr()), rows, m, 0, 0,
+                              1.0, 30.0, 0.0,
+                              P(v.data_ptr()), P(B.data_ptr()), P(F.data_ptr()), None, P(p.data_ptr()),
+                              P(ws.data_ptr()), ws.numel(), P(plan.buf.data_ptr()), plan.buf.numel(), plan.info,
+                              P(torch.cuda.current_stream(dev).cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize(dev)
+    # (B / F are written at their natural rows; a changed row in a direct tile -- swept by the unplanned
+    # kernel from nbr itself -- is simply right)
+    changed = {int(order[t]) for t in rows_changed}
+    nan_at = set(torch.nonzero(torch.isnan(F)).flatten().tolist())
+    assert nan_at and nan_at <= changed, (len(nan_at), sorted(nan_at - changed)[:5])
+    assert float(p[3]) == float(min(nan_at))
+    assert all(torch.isnan(B[i]).all() for i in nan_at)
 
 
 def test_plan_vs_oracle(dev, lib, c_oracle):
