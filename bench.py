@@ -255,6 +255,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                else [torch.cuda.Stream(dev) for _ in range(groups or cpg)])
     chains = []
     kw = dict(m=m, priors=Priors(), sigma2=sigma2, tau2=tau2, phi=phi, phi_tuning=0.01, device=dev)
+    # the w sweep of a single chain per GPU: one launch per colour, or the tiled sweep (gibbs_tiles.py)
+    tiled = args.gibbs_sweep == "tiled" and not single and cpg == 1
     if single:
         chains.append(ShardedSeqNNGP(coords, y, X, seed=1, collective=distributed, **kw))
     elif batched:
@@ -273,7 +275,8 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     else:
         for k in range(cpg):
             with torch.cuda.stream(streams[k]):
-                chains.append(SeqNNGP(coords, y, X, seed=1 + rank * cpg + k, **kw))
+                chains.append(SeqNNGP(coords, y, X, seed=1 + rank * cpg + k, sweep="tiled" if tiled else "colour",
+                                      **kw))
     g = chains[0]
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
@@ -340,8 +343,11 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
     w_save, r_save = g.w.clone(), g.r.clone()
     e0.record(stream)
     for _ in range(reps):
-        g.update_wt()
-        g.update_ws()
+        if tiled:
+            g._sweep_tiles()
+        else:
+            g.update_wt()
+            g.update_ws()
     e1.record(stream)
     torch.cuda.synchronize()
     wsweep_ms = e0.elapsed_time(e1) / reps
@@ -384,10 +390,13 @@ def run_gibbs(args, dev, rank, world, distributed, json_fd):
                                                         if batched else ", each on its own stream")) + ")"),
                 "chain_mode": args.chain_mode if (batched or groups) else ("streams" if cpg > 1 else "single"),
                 "chain_groups": groups or None,
+                "w_sweep": "tiled" if tiled else "colour",
             },
             "breakdown": {
                 "bf_sweep_ms": sweep_ms, "bf_sweep_share": sweep_ms / ms_iter,
                 "w_sweep_ms": wsweep_ms, "w_sweep_share": wsweep_ms / ms_iter, "n_colors": int(g.n_colors),
+                "w_sweep": ("tiled: one launch per phase of spatial tiles, r in LDS (%d tiles, %d launches)"
+                            % (g._tiles.tinfo.shape[0], len(g._tiles.phases))) if tiled else "one launch per colour",
                 "phi_accept_rate": g.n_accept / max(1, g.iteration), "setup_s": setup_s,
             },
             "roofline": {
@@ -420,6 +429,9 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gibbs-sweep", default="colour", choices=["colour", "tiled"],
+                    help="config 5, one chain per GPU: the w sweep as one launch per colour, or tiled (one launch "
+                         "per phase of spatial tiles holding r in LDS, pynngp_amd/gibbs_tiles.py)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
                     help="BASELINE.json config preset: 2 = N=1e5, m=15, Matern-3/2 (tau2=0.1); 3 = the headline "
                          "(default flags); 4 = N=1e7 / world per GPU, m=20, exponential; 5 = the Gibbs sampler "

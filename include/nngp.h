@@ -385,6 +385,24 @@ int nngp_gibbs_w_sweep(const int32_t *member_rows, const int32_t *color_off_host
                        int64_t n, int32_t m, double sigma2, double tau2, const double *yres, const double *noise_w,
                        double *w, double *r, const int32_t *rev_j, const double *z, uint64_t seed, uint64_t sweep,
                        void *stream);
+/* nngp_gibbs_w_sweep_tiles: the same w sweep, tiled (pynngp_amd/gibbs_tiles.py builds the plan): one launch
+ *   per phase, one workgroup per tile of the phase holding its footprint's r and its rows' new w in LDS and
+ *   running every colour of its rows in order, in steps; the tiles of a phase have disjoint footprints (each
+ *   node and its children), so the sweep is a valid colour sweep in the plan's (level, phase, colour) order.
+ *   The plan is contiguous: the storage order is the plan's node order.
+ *   tiles: the tile ids of every phase, phase p's at [phase_off_host[p], phase_off_host[p + 1]) (host
+ *   offsets); phase_lds_host[p]: its dynamic LDS bytes (gibbs_tiles.tile_lds_bytes of its largest tile);
+ *   tinfo (n_tiles, 8) int32, 16-byte aligned: the tile's rows [n0, n1), its footprint range [f0, f1) in
+ *   tfp, its step range [s0, s1) in tstep, two zeros; tstep: each step's first row (tile-local), a step
+ *   being <= 64 rows of one colour with <= ecap reverse entries (ecap <= 2048); tfp: each tile's footprint
+ *   (its rows first, then the halo); rev_loc (n_entries): the footprint-local index of reverse entry e's
+ *   child; off: the reverse lists' offsets, n_entries = off[n]; z: the normals (nngp_gibbs_normals).
+ *   Round 6. */
+int nngp_gibbs_w_sweep_tiles(const int32_t *tiles, const int32_t *phase_off_host, const int32_t *phase_lds_host,
+                             int32_t n_phases, const int32_t *tinfo, const int32_t *tstep, int32_t ecap,
+                             const int32_t *tfp, const int32_t *off, const int32_t *rev_loc, const void *prep,
+                             int64_t n, int32_t m, int64_t n_entries, double sigma2, double tau2, const double *yres,
+                             const double *noise_w, double *w, double *r, const double *z, void *stream);
 int nngp_gibbs_w_sweep_chains(const int32_t *member_rows, const int32_t *color_off_host, int32_t n_colors,
                               int32_t chains, const void *const *prep, int64_t n, int32_t m, const double *sigma2,
                               const double *tau2, const double *const *yres, const double *noise_w, double *const *w,

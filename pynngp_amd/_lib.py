@@ -57,6 +57,7 @@ SYMBOLS = (
     "nngp_gibbs_stats",
     "nngp_gibbs_w_sweep_chains",
     "nngp_gibbs_w_sweep_chains_il",
+    "nngp_gibbs_w_sweep_tiles",
     "nngp_color_moral_graph_dev",
     "nngp_pair_plan_supported",
     "nngp_pair_plan_bytes",
@@ -169,6 +170,9 @@ def load() -> ctypes.CDLL:
     lib.nngp_bf_sweep.restype = ctypes.c_int
     lib.nngp_color_moral_graph_dev.argtypes = [P, P, P, I64, I32, P, P, SZ, P]
     lib.nngp_color_moral_graph_dev.restype = I64
+    lib.nngp_gibbs_w_sweep_tiles.argtypes = [P, P, P, I32, P, P, I32, P, P, P, P, I64, I32, I64, D, D, P, P, P, P,
+                                             P, P]
+    lib.nngp_gibbs_w_sweep_tiles.restype = ctypes.c_int
     lib.nngp_gibbs_w_sweep_chains.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
     lib.nngp_gibbs_w_sweep_chains.restype = ctypes.c_int
     lib.nngp_gibbs_w_sweep_chains_il.argtypes = [P, P, I32, I32, P, I64, I32, P, P, P, P, P, P, P, P, P]
@@ -871,6 +875,30 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
                                      _ptr(rev_j),
                                      _ptr(z), int(seed) & (2 ** 64 - 1), int(sweep), _stream(dev)),
            "nngp_gibbs_w_sweep")
+
+
+def gibbs_w_sweep_tiles(plan, prep: torch.Tensor, m: int, sigma2: float, tau2: float, yres: torch.Tensor,
+                        w: torch.Tensor, r: torch.Tensor, off: torch.Tensor, z: torch.Tensor,
+                        noise_w: Optional[torch.Tensor] = None) -> None:
+    """The tiled colour sweep (nngp_gibbs_w_sweep_tiles) over a :class:`pynngp_amd.gibbs_tiles.TilePlan`: one
+    launch per phase, each tile's footprint of r in LDS; in place on w and r; ``z`` the normals
+    (:func:`gibbs_normals`).  The order is the plan's (level, phase, colour) -- its ``effective_colors`` as a
+    colouring.  The plan must be contiguous (its node order is the storage order: ``plan.contiguous``;
+    :func:`pynngp_amd.gibbs_tiles.contiguous_plan` / SeqNNGP(sweep="tiled") arrange it)."""
+    dev = _require_gpu(prep, yres, w, r, off, z, noise_w, plan.tinfo)
+    _check_noise_w(noise_w, w.shape[0])
+    if not plan.contiguous:
+        raise ValueError("the tiled sweep needs a contiguous tile plan (tile t's nodes = storage rows [n0, n1)): "
+                         "store the field in plan.tnodes order and rebuild the plan there")
+    if plan.tnodes.numel() != w.shape[0]:
+        raise ValueError(f"the tile plan covers {plan.tnodes.numel()} nodes, the field has {w.shape[0]}")
+    tiles, poff, plds = plan.launch_arrays()
+    _check(load().nngp_gibbs_w_sweep_tiles(_ptr(tiles), poff.ctypes.data, plds.ctypes.data, len(plds),
+                                           _ptr(plan.tinfo), _ptr(plan.tstep), int(plan.ecap), _ptr(plan.tfp),
+                                           _ptr(off), _ptr(plan.rev_loc), _ptr(prep), w.shape[0], int(m),
+                                           int(plan.rev_loc.numel()), float(sigma2), float(tau2), _ptr(yres),
+                                           _ptr(noise_w), _ptr(w), _ptr(r), _ptr(z), _stream(dev)),
+           "nngp_gibbs_w_sweep_tiles")
 
 
 def gibbs_w_sweep_chains(member_rows: torch.Tensor, color_off_host, preps, m: int, sigma2s, tau2s, yres, w, r,

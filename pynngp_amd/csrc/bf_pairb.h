@@ -52,113 +52,51 @@
 
 namespace nngp {
 
-// Pair exchanges.  NNGP_PAIRB_SWZ bit 0: the partner swaps go through ds_swizzle (quad-perm
-// mode) on the LDS pipe instead of two v_mov_dpp on the VALU; bit 1: the lane-0 / lane-1
-// broadcasts too.  The kernel is VALU-issue bound, so an exchange issued on the LDS pipe
-// co-issues with the other wave's VALU work.
-#ifndef NNGP_PAIRB_SWZ
-#define NNGP_PAIRB_SWZ 0
-#endif
-// The within-pair covariance split (below) up to m = NNGP_PAIRB_DEDUP_MAX: it keeps the partner
-// coordinates live longer (+20 VGPRs at m = 15), which costs spills past m = 17.
-#ifndef NNGP_PAIRB_DEDUP_MAX
-#define NNGP_PAIRB_DEDUP_MAX 17
-#endif
-// NNGP_PAIRB_NOZ: no value column in the elimination; the residual is r = v_i - B v_N after
-// the back-substitution (B is then always computed): 5 % fewer VALU at m = 15.  Not at m = 19
-// with two waves per SIMD, where it moved the register peak (100 -> 220 B of scratch, 0.394 ->
-// 0.499 ms per 10^6 rows).
-#ifndef NNGP_PAIRB_NOZ
-#define NNGP_PAIRB_NOZ 1
-#endif
-// (A 2x2-block LDL^T -- one reciprocal of det D_t per block step instead of two pivot square
-// roots, -4.3 % VALU -- was measured and rejected: L = X D_t^{-1} multiplies by entries ~1/delta
-// for a nearly singular pair block where the Cholesky factor's are ~1/sqrt(delta), and F lost
-// accuracy: 2e-9 relative vs the oracle at Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
-// NNGP_PAIRB_SLDL: scalar-pivot LDL^T in the 2x2-blocked layout (reciprocals, unit factor)
-// instead of the Cholesky factor (inverse square roots): -44 VALU per wave at m = 15 (-1.7 %),
-// -0.6 % time (same-box A/B), every GPU parity test unchanged.  Not at m = 19 (no value column
-// path there, NOZ).
-#ifndef NNGP_PAIRB_SLDL
-#define NNGP_PAIRB_SLDL 1
-#endif
-// ... except where the two-wave register budget is tight (m = 18: 80 -> 216 B of scratch)
-#ifndef NNGP_PAIRB_SLDL_MAX
-#define NNGP_PAIRB_SLDL_MAX 17
-#endif
-// NNGP_PAIRB_ZLDS_MIN: from this m the neighbour values wait in LDS between the gathers and the
-// residual (they are read only there): NP doubles of registers per lane less where the two-wave
-// register budget is tight.
-#ifndef NNGP_MT_GLOBAL  // 1: the Matern-nu table from global memory instead of a per-block LDS copy (A/B)
-#define NNGP_MT_GLOBAL 0
-#endif
-#ifndef NNGP_PAIRB_ZLDS_MIN
-#define NNGP_PAIRB_ZLDS_MIN 99
-#endif
-// Left-looking elimination (bit m of NNGP_PAIRB_LEFT_MASK): column pair by column pair, each
-// column's covariances evaluated when it is reached and updated from the finished columns, so the
-// trailing block and every coordinate are never live at once; the finished factor rows
-// 0..KL-1 wait in LDS for the back-substitution.  The register peak is the factor's later rows
-// instead of the whole joint block plus coordinates: m = 18..22 run at two waves per SIMD (m = 18:
-// 0.273 vs 0.413 ms per 1e6 rows right-looking with 224 B of scratch, profiles/r05z5; m = 16 / 17
-// tie and stay right-looking)
-// (right-looking: one; 0.352 / 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows at m = 19 /
-// 20 / 22, profiles/r03e; m = 21 0.416 vs 0.552, profiles/r05z2); from m = NNGP_PAIRB_LEFT_ONE_WAVE_MIN
-// the left-looking kernel runs at one wave with more rows in LDS (its peak no longer fits 256
-// registers): m = 23 / 24 0.604 / 0.696 vs 0.659 / 0.732 right-looking (profiles/r05z2).
-#ifndef NNGP_PAIRB_LEFT_MASK
-#define NNGP_PAIRB_LEFT_MASK (((1ull << 33) - 1) & ~((1ull << 18) - 1))  // m = 18..32
-#endif
-#ifndef NNGP_PAIRB_LEFT_ONE_WAVE_MIN
-#define NNGP_PAIRB_LEFT_ONE_WAVE_MIN 23
-#endif
-#ifndef NNGP_PAIRB_LEFT_LDS_ROWS  // factor rows in LDS at two waves per SIMD (5: 123 KB of 160 per CU)
-#define NNGP_PAIRB_LEFT_LDS_ROWS 5
-#endif
-#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_1W  // ... and at one wave per SIMD (7, with the late state in LDS)
-#define NNGP_PAIRB_LEFT_LDS_ROWS_1W 7
-#endif
-// Left-looking at three waves per SIMD (<= 168 VGPRs; bit m of NNGP_PAIRB_LEFT_3W_MASK, which
-// must also be set in NNGP_PAIRB_LEFT_MASK): NNGP_PAIRB_LEFT_LDS_ROWS_3W factor rows in LDS.
-#ifndef NNGP_PAIRB_LEFT_3W_MASK
-#define NNGP_PAIRB_LEFT_3W_MASK 0ull
-#endif
-#ifndef NNGP_PAIRB_LEFT_LDS_ROWS_3W  // (4: 40 KB per block, 123 KB per CU at three blocks)
-#define NNGP_PAIRB_LEFT_LDS_ROWS_3W 4
-#endif
-constexpr bool pairb_left(int m) { return ((unsigned long long)(NNGP_PAIRB_LEFT_MASK) >> m) & 1ull; }
-constexpr bool pairb_left3(int m) {
-    return pairb_left(m) && (((unsigned long long)(NNGP_PAIRB_LEFT_3W_MASK) >> m) & 1ull);
-}
-// the same for a kernel of covariance kind `kind` (the covariance-blocks kernels are right-looking)
+// Design constants (each measured; the rejected alternatives -- partner exchanges through ds_swizzle, the
+// Matern table read from global memory, values parked in LDS, left-looking at three waves per SIMD, balanced
+// tilings, the fused record fold -- are described in DESIGN.md 4.1 / 4.2a / 5 and live as patches under
+// tools/variants/ for tools/build_variant.sh, not as switches here).
+//
+// The within-pair covariance split (below) up to m = kPairbDedupMax: it keeps the partner coordinates live
+// longer (+20 VGPRs at m = 15), which costs spills past m = 17.
+constexpr int kPairbDedupMax = 17;
+// (A 2x2-block LDL^T -- one reciprocal of det D_t per block step instead of two pivot square roots, -4.3 %
+// VALU -- was measured and rejected: L = X D_t^{-1} multiplies by entries ~1/delta for a nearly singular pair
+// block where the Cholesky factor's are ~1/sqrt(delta), and F lost accuracy: 2e-9 relative vs the oracle at
+// Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
+// Scalar-pivot LDL^T in the 2x2-blocked layout (reciprocals, unit factor) instead of the Cholesky factor
+// (inverse square roots) for the right-looking kernels: -44 VALU per wave at m = 15 (-1.7 %), -0.6 % time
+// (same-box A/B), every GPU parity test unchanged; except at m = 18 (the Matern-nu / blocks kinds there),
+// where the two-wave register budget is tight (80 -> 216 B of scratch).
+constexpr int kPairbSldlSkipM = 18;
+// Left-looking elimination (m in [kPairbLeftMin, 32], the fused kinds): column pair by column pair, each
+// column's covariances evaluated when it is reached and updated from the finished columns, so the trailing
+// block and every coordinate are never live at once; the finished factor rows 0..KL-1 wait in LDS for the
+// back-substitution.  The register peak is the factor's later rows instead of the whole joint block plus
+// coordinates: m = 18..22 run at two waves per SIMD (m = 18: 0.273 vs 0.413 ms per 1e6 rows right-looking
+// with 224 B of scratch, profiles/r05z5; m = 16 / 17 tie and stay right-looking) (right-looking: one; 0.352 /
+// 0.392 / 0.566 vs 0.457 / 0.544 / 0.639 ms per 1e6 rows at m = 19 / 20 / 22, profiles/r03e; m = 21 0.416 vs
+// 0.552, profiles/r05z2); from m = kPairbLeftOneWaveMin the left-looking kernel runs at one wave with more
+// rows in LDS (its peak no longer fits 256 registers): m = 23 / 24 0.604 / 0.696 vs 0.659 / 0.732
+// right-looking (profiles/r05z2).
+constexpr int kPairbLeftMin = 18;
+constexpr int kPairbLeftOneWaveMin = 23;
+constexpr int kPairbLeftLdsRows = 5;    // factor rows in LDS at two waves per SIMD (123 KB of 160 per CU)
+constexpr int kPairbLeftLdsRows1W = 7;  // ... and at one wave per SIMD (with the late state in LDS)
+constexpr bool pairb_left(int m) { return m >= kPairbLeftMin && m <= 32; }
+// the same for a kernel of covariance kind `kind` (the covariance-blocks and Matern-table kernels are
+// right-looking)
 constexpr bool pairb_lk(int m, int kind) {
     return pairb_left(m) && kind != NNGP_KIND_BLOCKS && kind != NNGP_KIND_MATERN;
 }
-constexpr bool pairb_left3_k(int m, int kind) { return pairb_left3(m) && kind != NNGP_KIND_BLOCKS; }
-// static per-phase budgets (tools/isa_phases.py): -DNNGP_PAIRB_PHASES fences the phases
-#ifdef NNGP_PAIRB_PHASES
-#define NNGP_PHASE(name)                        \
-    __builtin_amdgcn_sched_barrier(0);          \
-    asm volatile("; PHASE_" #name ::: "memory"); \
-    __builtin_amdgcn_sched_barrier(0)
-#else
+// static per-phase budgets (tools/isa_phases.py): tools/variants/phases.h defines NNGP_PHASE to fence the
+// phases with named markers (hipcc -include tools/variants/phases.h); a product build leaves them empty
+#ifndef NNGP_PHASE
 #define NNGP_PHASE(name)
 #endif
-template <int CTRL>
-__device__ __forceinline__ double swz_f64(double v) {
-    const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)(u & 0xffffffffll), 0x8000 | CTRL);
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(u >> 32), 0x8000 | CTRL);
-    return __hiloint2double(hi, lo);
-}
-template <int CTRL, bool SWZ>
-__device__ __forceinline__ double pr_xchg(double v) {
-    if constexpr (SWZ) return swz_f64<CTRL>(v);
-    return dpp_f64<CTRL>(v);
-}
-__device__ __forceinline__ double pr_swap(double v) { return pr_xchg<0xB1, (NNGP_PAIRB_SWZ & 1) != 0>(v); }   // partner lane's v
-__device__ __forceinline__ double pr_from0(double v) { return pr_xchg<0xA0, (NNGP_PAIRB_SWZ & 2) != 0>(v); }  // lane 0's v
-__device__ __forceinline__ double pr_from1(double v) { return pr_xchg<0xF5, (NNGP_PAIRB_SWZ & 2) != 0>(v); }  // lane 1's v
+__device__ __forceinline__ double pr_swap(double v) { return dpp_f64<0xB1>(v); }   // partner lane's v
+__device__ __forceinline__ double pr_from0(double v) { return dpp_f64<0xA0>(v); }  // lane 0's v
+__device__ __forceinline__ double pr_from1(double v) { return dpp_f64<0xF5>(v); }  // lane 1's v
 __device__ __forceinline__ double pr_sel(bool q1, double v1, double v0) { return q1 ? v1 : v0; }
 // the same select as a bit-field insert under an opaque lane mask: a plain select of two entries
 // of one register array becomes an array access at a lane-dependent index, which LLVM lowers
@@ -170,73 +108,47 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
     return __hiloint2double((int)hi, (int)lo);
 }
 
-// Occupancy: up to m = NNGP_PAIRB_TWO_WAVES_MAX the compiler is asked for two waves per SIMD
-// (<= 256 VGPRs): m = 16 / 17 fit without spills; m = 18 spills 20 dwords to scratch and still
-// runs ~30 % faster than at one wave per SIMD (0.314 vs 0.435 ms per 10^6 rows, profiles/r02ap);
-// m = 19 spilled 60 dwords in the final build and runs faster at one wave (0.476 vs 0.546 ms;
-// it was 23 dwords and 22 % faster at two waves in profiles/r02p).  From m = 20 (342 VGPRs) the
-// forced spills (91 dwords) cost more than the second wave gains (+52 % at m = 20, 2-3x at
-// m = 22 / 24).
-#ifndef NNGP_PAIRB_TWO_WAVES_MAX
-#define NNGP_PAIRB_TWO_WAVES_MAX 18
-#endif
-// Three waves per SIMD (<= 168 VGPRs) up to m = NNGP_PAIRB_THREE_WAVES_MAX: m = 12 / 13 fit
-// in 162 / 164 VGPRs (-3.7 % cycles at m = 13); forced at m = 14 / 15 the 31 / 35 spilled
+// Occupancy: up to m = kPairbTwoWavesMax the compiler is asked for two waves per SIMD (<= 256 VGPRs):
+// m = 16 / 17 fit without spills; m = 18 (the right-looking Matern-nu / blocks kinds) spills 20 dwords and
+// still runs ~30 % faster than at one wave per SIMD (0.314 vs 0.435 ms per 10^6 rows, profiles/r02ap).  From
+// m = 20 (342 VGPRs) the right-looking kernels' forced spills (91 dwords) cost more than the second wave gains
+// (+52 % at m = 20, 2-3x at m = 22 / 24).  Three waves per SIMD (<= 168 VGPRs) up to m = kPairbThreeWavesMax:
+// m = 12 / 13 fit in 162 / 164 VGPRs (-3.7 % cycles at m = 13); forced at m = 14 / 15 the 31 / 35 spilled
 // dwords cost more (+10 % / +37 %, profiles/r02y).
-#ifndef NNGP_PAIRB_THREE_WAVES_MAX
-#define NNGP_PAIRB_THREE_WAVES_MAX 13
-#endif
-// (KIND == NNGP_KIND_BLOCKS: covariances read from memory; NNGP_KIND_MATERN: the Matern table in LDS
-// -- both always right-looking, pairb_lk)
-#define NNGP_PAIRB_ATTR                                                                              \
-    __attribute__((amdgpu_waves_per_eu(                                                                 \
-        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3                                 \
-         : (M <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_lk(M, KIND) && M < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2 : 1), \
-        ((M <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(M, KIND)) ? 3 : 2))))
-
-// waves per SIMD the kernel for (m, kind) is built for (NNGP_PAIRB_ATTR's minimum): blocks per CU
+constexpr int kPairbTwoWavesMax = 18;
+constexpr int kPairbThreeWavesMax = 13;
+// waves per SIMD the kernel for (m, kind) is built for: blocks per CU
 constexpr int pairb_waves_per_simd(int m, int kind) {
-    return (m <= NNGP_PAIRB_THREE_WAVES_MAX || pairb_left3_k(m, kind)) ? 3
-           : (m <= NNGP_PAIRB_TWO_WAVES_MAX || (pairb_lk(m, kind) && m < NNGP_PAIRB_LEFT_ONE_WAVE_MIN)) ? 2
-                                                                                                     : 1;
+    return m <= kPairbThreeWavesMax ? 3
+           : (m <= kPairbTwoWavesMax || (pairb_lk(m, kind) && m < kPairbLeftOneWaveMin)) ? 2
+                                                                                          : 1;
 }
+#define NNGP_PAIRB_ATTR \
+    __attribute__((amdgpu_waves_per_eu(pairb_waves_per_simd(M, KIND), M <= kPairbThreeWavesMax ? 3 : 2)))
 
 // Threads per block (one tile of up to kPairbThreads / 2 locations per block).  256 measured fastest:
 // 128 / 64 threads (table fill per block, 2x / 4x the tile records) took +0.9 % / +2.6 % at
 // config 3 and +5 % / +1 % at config 2 (same-box A/B).
-#ifndef NNGP_PAIRB_THREADS
-#define NNGP_PAIRB_THREADS 256
-#endif
-constexpr int kPairbThreads = NNGP_PAIRB_THREADS;
+constexpr int kPairbThreads = 256;
 constexpr int kPairbWaves = kPairbThreads / 64;
 constexpr int kPairbTile = kPairbThreads / 2;  // locations per tile (at most)
 constexpr int kDeviceCUs = 256;                 // MI355X (gfx950): 8 XCDs x 32 CUs
 
-// Tiling of n_rows locations: q or q + 1 rows per tile (the sweep writes the tile count into the
-// workspace header, where the record fold reads it).  NNGP_PAIRB_BALANCE (round 4, measured and not
-// kept): make the tiles a whole number of rounds of the device's block slots (256 CUs x blocks per
-// CU), each holding q or q + 1 rows as long as every wave keeps a live row (q > 96) -- meant to avoid
-// a last, partly filled round of lone waves (config 2: 782 tiles on 512 two-wave slots, 1.53 rounds).
-// Same-box A/B (profiles/r04d): config 3 186.3 vs 178.8 us (+4 %: 32,768 instead of 31,252 waves, each
-// with the full instruction count), config 2 29.2 vs 28.1 us -- the partly filled round costs less
-// than the extra waves.  Default: the plain tiling (ceil(n / 128) tiles).
+// Tiling of n_rows locations: ceil(n / 128) tiles of q or q + 1 rows (the sweep writes the tile count into
+// the workspace header, where the record fold reads it).  (Tiles balanced to whole rounds of the device's
+// block slots were measured and not kept, round 4, profiles/r04d: +4 % at config 3, no gain at config 2.)
 struct PairbTiling {
     int64_t tiles, q, rem;  // tiles; tile t holds q + (t < rem) rows starting at t q + min(t, rem)
 };
-#ifndef NNGP_PAIRB_BALANCE  // 1: balanced rounds (measured slower, above)
-#define NNGP_PAIRB_BALANCE 0
-#endif
 inline PairbTiling pairb_tiling(int64_t n_rows, int m, int kind) {
+    (void)m;
+    (void)kind;
     const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
     if (T == 0) return {0, 0, 0};
-    if (!NNGP_PAIRB_BALANCE) return {T, n_rows / T, n_rows % T};
-    const int64_t C = (int64_t)kDeviceCUs * pairb_waves_per_simd(m, kind);
-    const int64_t Tb = (T + C - 1) / C * C;
-    const int64_t t = (Tb > T && n_rows / Tb > 3 * 32) ? Tb : T;
-    return {t, n_rows / t, n_rows % t};
+    return {T, n_rows / T, n_rows % T};
 }
-// the most tiles any (m, kind) uses for n_rows (workspace sizing): T + C - 1 with C <= 3 x 256, and
-// balanced tilings keep more than 96 rows per tile
+// record slots a sweep of n_rows may use (workspace sizing; kept at the ABI-2 bound, which also covered the
+// balanced tilings, so workspace sizes do not change)
 inline int64_t pairb_tiles_bound(int64_t n_rows) {
     const int64_t T = (n_rows + kPairbTile - 1) / kPairbTile;
     const int64_t b = T + 3 * kDeviceCUs - 1 < n_rows / 97 ? T + 3 * kDeviceCUs - 1 : n_rows / 97;
@@ -286,8 +198,7 @@ __device__ __forceinline__ void pairb_tile_fold(double (*sh)[kPairbWaves][5], in
     lexp[tile] = (int32_t)le + __builtin_amdgcn_frexp_exp(lm);
 }
 
-// ---- the fixed-order fold of the tile records (the separate finalize kernel and the sweep's fused
-// last-block fold run this same code with kPairbThreads threads, so their bits agree).
+// ---- the fixed-order fold of the tile records (the finalize kernel, kPairbThreads threads).
 // rec[t] = (mantissa product m_t in [1/2, 1), sum r^2/F, bad-pivot row, bad-index row), lexp[t] =
 // exponent sum e_t.  sum log F = log(prod_t m_t) + (sum_t e_t) ln 2: the mantissas are multiplied
 // (renormalised by frexp after every product, exponents summed exactly as integers) and ONE log is
@@ -321,27 +232,6 @@ __device__ __forceinline__ void mant_norm(double& m, double& e) {
     m = __builtin_amdgcn_frexp_mant(m);
 }
 
-// COHERENT: the records were written by other blocks of the running kernel (the fused fold): read at
-// agent scope (past this XCD's non-coherent L2)
-template <bool COHERENT>
-__device__ __forceinline__ double4 pairb_rec_load(const double4* rec, int64_t k) {
-    if constexpr (COHERENT) {
-        const double* p = (const double*)(rec + k);
-        return make_double4(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                            __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                            __hip_atomic_load(p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                            __hip_atomic_load(p + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    } else {
-        return rec[k];
-    }
-}
-template <bool COHERENT>
-__device__ __forceinline__ int32_t pairb_lexp_load(const int32_t* lexp, int64_t k) {
-    if constexpr (COHERENT) return __hip_atomic_load(lexp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return lexp[k];
-}
-
-template <bool COHERENT = false>
 __device__ __forceinline__ void pairb_fold_records(const double4* __restrict__ rec, const int32_t* __restrict__ lexp,
                                                    int64_t n_tiles, double* __restrict__ partials,
                                                    double (*sh)[5]) {
@@ -356,8 +246,8 @@ __device__ __forceinline__ void pairb_fold_records(const double4* __restrict__ r
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int64_t k = k0 + (int64_t)u * NT;
-            r[u] = k < n_tiles ? pairb_rec_load<COHERENT>(rec, k) : make_double4(1.0, 0.0, INFINITY, INFINITY);
-            x[u] = k < n_tiles ? pairb_lexp_load<COHERENT>(lexp, k) : 0;
+            r[u] = k < n_tiles ? rec[k] : make_double4(1.0, 0.0, INFINITY, INFINITY);
+            x[u] = k < n_tiles ? lexp[k] : 0;
         }
         double pm = 1.0;
         int32_t pe = 0;
@@ -438,8 +328,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                                                 double* __restrict__ Fout, double* __restrict__ Rout,
                                                 double4* __restrict__ rec, int32_t* __restrict__ lexp, int dim,
                                                 const double* __restrict__ cblk, int64_t tq, int64_t trem,
-                                                int64_t* __restrict__ hdr, double* __restrict__ fused,
-                                                const PairPlanArgs pp) {
+                                                int64_t* __restrict__ hdr, const PairPlanArgs pp) {
     static_assert(M >= 1 && M <= 32, "pairb instantiated for 1 <= m <= 32");
     static_assert(D >= 0 && D <= 3, "0 (runtime dimension) <= D <= 3");
     constexpr bool CM = KIND == NNGP_KIND_BLOCKS;
@@ -456,12 +345,10 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     // head (slot 0: the exact zero), the wave's points at its end
     constexpr int PSL = PL ? plan_slice_bytes(M) : 16;
     __shared__ __attribute__((aligned(16))) double wsl[PL ? kPairbWaves * PSL / 8 : 1];
-    constexpr bool NOZ = LEFT || (NNGP_PAIRB_NOZ && (M != 19 || M > NNGP_PAIRB_TWO_WAVES_MAX));
-    constexpr bool SLDL = !LEFT && NNGP_PAIRB_SLDL && NOZ &&
-                          (M <= NNGP_PAIRB_SLDL_MAX || M > NNGP_PAIRB_TWO_WAVES_MAX);
-    constexpr int KL0 = pairb_left3_k(M, KIND)                 ? NNGP_PAIRB_LEFT_LDS_ROWS_3W
-                        : M >= NNGP_PAIRB_LEFT_ONE_WAVE_MIN ? NNGP_PAIRB_LEFT_LDS_ROWS_1W
-                                                              : NNGP_PAIRB_LEFT_LDS_ROWS;
+    // (no value column in the elimination: the residual is r = v_i - B v_N after the back-substitution, the
+    // oracle's own formula -- 5 % fewer VALU at m = 15 than forward-solving the values through it)
+    constexpr bool SLDL = !LEFT && M != kPairbSldlSkipM;
+    constexpr int KL0 = M >= kPairbLeftOneWaveMin ? kPairbLeftLdsRows1W : kPairbLeftLdsRows;
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
     // the left-looking kernel's LDS in one object: the exp table first (its reads fold the base into the
     // 16-bit offset field; the LDS lowering sorts separate objects by size, which put it above 64 KB), the
@@ -474,13 +361,10 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     double(*const lrow)[kPairbThreads] = (double(*)[kPairbThreads])(lbuf + NNGP_EXP_TAB_N);
     int32_t(*const lidx)[kPairbThreads] =
         (int32_t(*)[kPairbThreads])(lbuf + NNGP_EXP_TAB_N + KL * (KL + 1) * kPairbThreads);
-    constexpr bool ZLDS = NOZ && M >= NNGP_PAIRB_ZLDS_MIN;
-    __shared__ double zsh[ZLDS ? NP : 1][ZLDS ? kPairbThreads : 1];
     __shared__ double etab_own[MT || LEFT ? 1 : NNGP_EXP_TAB_N];
     double* const etab = LEFT ? lbuf : etab_own;
     extern __shared__ double4 pairb_mtab[];  // MT: the Matern table (dynamic LDS, NNGP_MT_BYTES(noct))
-    // (NNGP_MT_GLOBAL: the Matern table read in place from global memory -- no per-block copy)
-    const double* ctab = MT ? (NNGP_MT_GLOBAL ? cblk : (const double*)pairb_mtab) : etab;
+    const double* ctab = MT ? (const double*)pairb_mtab : etab;
     // table entries per thread (threads past the table's 256 entries of a 512-thread block fetch
     // entry j - 256 and do not store it)
     constexpr int kTabPer = kPairbThreads >= NNGP_EXP_TAB_N ? 1 : NNGP_EXP_TAB_N / kPairbThreads;
@@ -546,10 +430,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             }
             if constexpr (!LEFT) z[s] = *pv;  // (the left-looking kernel gathers the values late)
         }
-        if constexpr (ZLDS) {
-#pragma unroll
-            for (int s = 0; s < NP; ++s) zsh[s][threadIdx.x] = z[s];  // read back by this thread only
-        }
         const bool bad_index = (int64_t)jmax >= n_points || jmin < -1;
         if constexpr (LEFT) {  // the late state waits in LDS (read back by this thread only)
 #pragma unroll
@@ -561,7 +441,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 
         // the exp table entry was fetched before the gathers; storing it here lets its load and
         // the barrier overlap the gathers' latency instead of preceding it
-        if constexpr (MT && !NNGP_MT_GLOBAL) {
+        if constexpr (MT) {
             const int n4 = Pc.mt_noct * (NNGP_MT_K * NNGP_MT_NC / 4);
             const double4* g = (const double4*)cblk;
             for (int k = (int)threadIdx.x; k < n4; k += kPairbThreads) pairb_mtab[k] = g[k];
@@ -804,7 +684,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
 #pragma unroll
             for (int s0 = 0; s0 < NP; s0 += 2) {
                 const int s1 = s0 + 1;
-                if (M <= NNGP_PAIRB_DEDUP_MAX && s1 < NP) {
+                if (M <= kPairbDedupMax && s1 < NP) {
                     double a[DA], b[DA];
 #pragma unroll
                     for (int k = 0; k < DA; ++k) {
@@ -882,14 +762,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const double i11 = nngp_rsqrt(s11);
             R[t][t][0] = pr_sel(q1, i11, i00);
             R[t][t][1] = l10;
-            double wS = 0.0, wO = 0.0;
-            if constexpr (!NOZ) {
-                const double w0 = pr_from0(z[t]) * i00;
-                const double w1 = fma(-l10, w0, pr_from1(z[t])) * i11;
-                z[t] = pr_sel(q1, w1, w0);
-                wS = pr_sel(q1, w1, w0);
-                wO = pr_sel(q1, w0, w1);
-            }
             // panel map (L[a][2t], L[a][2t+1]) = (A[a][2t], A[a][2t+1]) U, U = [[i00, u01], [0, i11]],
             // written in own-parity-first coordinates: Y0 = X0 c00 + X1 c10, Y1 = X0 c01 + X1 c11
             const double u01 = -(l10 * i00) * i11;
@@ -904,7 +776,6 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 const double y1 = fma(x0, c01, x1 * c11);
                 R[s][t][0] = y0;
                 R[s][t][1] = y1;
-                if constexpr (!NOZ) z[s] = fma(-y0, wS, fma(-y1, wO, z[s]));
             }
             // trailing update: same-parity slots read this lane's panel, other-parity slots the swapped one
 #pragma unroll
@@ -940,15 +811,13 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const double i00 = nngp_rsqrt(a00);
             const double l10 = a10 * i00;
             Fu = fma(-l10, l10, a11);
-            if constexpr (!NOZ) res = fma(-l10, pr_from0(z[T]) * i00, pr_from1(z[T]));
             R[T][T][0] = i00;  // lane 0: 1 / L[M-1][M-1]
             R[T][T][1] = l10;  // L[M][M-1]
         } else {
             Fu = pr_from0(R[T][T][0]);
-            if constexpr (!NOZ) res = pr_from0(z[T]);
         }
         } else {
-            // ---- left-looking 2x2-blocked Cholesky (NNGP_PAIRB_LEFT_MIN): step u evaluates column
+            // ---- left-looking 2x2-blocked Cholesky (kPairbLeftMin): step u evaluates column
             // pair u's covariances for rows s >= u, subtracts the finished column pairs t < u (the
             // same 2x2 block products as the right-looking update, reordered), factors the diagonal
             // block and maps the panel.  Row pair u is then final; rows < KL move to LDS.
@@ -1055,7 +924,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             bidx = lidx[NP + 2][threadIdx.x] != 0;
         }
 
-        if (NOZ || Bout != nullptr) {
+        {
             // B = L_N^{-T} v, v = row M of L (lane M % 2, local row M / 2).  Lane q ends with
             // bown[s] = B_{2s+q}.
             constexpr int SM = M / 2;
@@ -1114,7 +983,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 bown[t] = pr_sel(q1, bx, b0);
             }
             NNGP_PHASE(residual);
-            if constexpr (NOZ) {
+            {
                 // r = v_i - B v_N (as the oracle states it): this lane's rows a = 2s + q < M, then the pair
                 double acc = 0.0;
 #pragma unroll
@@ -1122,9 +991,9 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                     if (2 * s >= M) continue;
                     double bs = bown[s];
                     if (2 * s + 1 >= M) bs = q1 ? 0.0 : bs;  // lane 1's row here is row M (or padding)
-                    acc = fma(bs, ZLDS ? zsh[s][threadIdx.x] : z[s], acc);
+                    acc = fma(bs, z[s], acc);
                 }
-                const double zm = ZLDS ? zsh[SM][threadIdx.x] : z[SM];
+                const double zm = z[SM];
                 const double vi = VQ1 ? pr_from1(zm) : pr_from0(zm);
                 res = vi - (acc + pr_swap(acc));
             }
@@ -1149,58 +1018,13 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                          lead ? res * res * pr_rcp(F) : 0.0, (lead && bad) ? (double)il : INFINITY,
                          (live && bidx) ? (double)il : INFINITY, sh, 0, rec, lexp, tile);
         __syncthreads();
-        if (fused == nullptr) {
-            if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
-            return;
-        }
-        // fused fold (small sweeps, NNGP_PAIRB_FUSED_FOLD_MAX_ROWS): the record goes out at agent scope,
-        // a ticket counts the finished tiles, and the last tile's block folds every record (the same
-        // pairb_fold_records as the separate finalize kernel) -- one launch per sweep instead of two.
-        // The ticket (the workspace header's second word) is zero before the first sweep and reset by
-        // the last block.
-        __shared__ int last;
-        if (threadIdx.x == 0) {
-            double lm = 1.0, le = 0.0, qq = 0.0, bp = INFINITY, bi = INFINITY;
-#pragma unroll
-            for (int k = 0; k < kPairbWaves; ++k) {
-                lm *= sh[0][k][0];
-                le += sh[0][k][1];
-                qq += sh[0][k][2];
-                bp = fmin(bp, sh[0][k][3]);
-                bi = fmin(bi, sh[0][k][4]);
-            }
-            double* rp = (double*)(rec + tile);
-            __hip_atomic_store(rp, __builtin_amdgcn_frexp_mant(lm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(rp + 1, qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(rp + 2, bp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(rp + 3, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(lexp + tile, (int32_t)le + __builtin_amdgcn_frexp_exp(lm), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            // release: the record's stores complete (vmcnt counts stores on gfx9) before the ticket
-            __builtin_amdgcn_s_waitcnt(0);
-            unsigned int* ticket = (unsigned int*)(hdr + 1);
-            const unsigned int old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = old == gridDim.x - 1;
-            if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        if (last) {
-            __shared__ double fsh[kPairbWaves][5];
-            pairb_fold_records<true>(rec, lexp, (int64_t)gridDim.x, fused, fsh);
-        }
+        if (threadIdx.x == 0) pairb_tile_fold(sh, 0, rec, lexp, tile);
     }
 }
 
-// Fused record fold (one launch per sweep) up to this many rows; 0: always the separate fold kernel.
-// Measured and not kept (round 4, profiles/r04d): the record at agent scope, the drain and the ticket
-// in every block cost more than the separate 4-us fold launch -- config 2 34.0 vs 29.2 us per sweep.
-#ifndef NNGP_PAIRB_FUSED_FOLD_MAX_ROWS
-#define NNGP_PAIRB_FUSED_FOLD_MAX_ROWS 0
-#endif
-
-// workspace: a 256-B header (int64 tile count, written by the sweep and read by the fold; uint32
-// ticket of the fused fold, zero between sweeps), the tile
-// records (32 B each) and the tile exponent sums (4 B each), sized for pairb_tiles_bound(n_rows)
+// workspace: a 256-B header (int64 tile count, written by the sweep and read by the fold; the second word,
+// once the ticket of a fused fold -- measured and not kept, round 4 -- stays zero), the tile records (32 B
+// each) and the tile exponent sums (4 B each), sized for pairb_tiles_bound(n_rows)
 inline size_t pairb_align(size_t b) { return (b + 255) & ~(size_t)255; }
 constexpr size_t kPairbHeader = 256;
 inline size_t bf_pairb_workspace_bytes(int64_t n_rows) {
@@ -1208,20 +1032,16 @@ inline size_t bf_pairb_workspace_bytes(int64_t n_rows) {
     return t > 0 ? kPairbHeader + pairb_align((size_t)t * 32) + pairb_align((size_t)t * 4) : 0;
 }
 inline int64_t* pairb_hdr(void* ws) { return (int64_t*)ws; }
-// the sweep folds its own records when the caller wants the partials now and the sweep is small
-inline bool pairb_fuse_fold(const BfArgs& a) {
-    return a.partials != nullptr && a.n_rows > 0 && a.n_rows <= (int64_t)NNGP_PAIRB_FUSED_FOLD_MAX_ROWS;
-}
 inline double4* pairb_rec(void* ws) { return (double4*)((char*)ws + kPairbHeader); }
 inline int32_t* pairb_lexp(void* ws, int64_t n_rows) {
     return (int32_t*)((char*)ws + kPairbHeader + pairb_align((size_t)pairb_tiles_bound(n_rows) * 32));
 }
 
 // a.tiles != null: sweep only the listed tiles (a planned sweep's direct regions, pair_plan.h), a.n_tiles
-// being the whole sweep's count; the records are then the caller's to fold (never fused)
+// being the whole sweep's count; the records are then the caller's to fold
 template <int M, int KIND, int D, bool PL = false>
 static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s, const PairPlanArgs* ppl = nullptr) {
-    const size_t lds = KIND == NNGP_KIND_MATERN && !NNGP_MT_GLOBAL ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
+    const size_t lds = KIND == NNGP_KIND_MATERN ? NNGP_MT_BYTES(Pc.mt_noct) : 0;
     const PairbTiling tl = pairb_tiling(a.n_rows, M, KIND);
     PairPlanArgs pp = ppl != nullptr ? *ppl : PairPlanArgs{};
     if (!PL && a.tiles != nullptr) {
@@ -1233,8 +1053,7 @@ static void launch_pairb_mkd(const BfArgs& a, const CovParams& Pc, hipStream_t s
     hipLaunchKernelGGL((bf_pairb<M, KIND, D, PL>), dim3((unsigned)nb), dim3(kPairbThreads), lds, s, a.coords,
                        a.n_points, a.nbr, a.order, a.n_rows, a.i0, Pc, KIND == NNGP_KIND_BLOCKS ? 1.0 : a.sigma2, a.values,
                        a.qcoords, a.qvalues, a.B, a.F, a.R, pairb_rec(a.bpart), pairb_lexp(a.bpart, a.n_rows), a.dim,
-                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart),
-                       pairb_fuse_fold(a) && pp.tiles == nullptr ? a.partials : nullptr, pp);
+                       a.cblk, tl.q, tl.rem, pairb_hdr(a.bpart), pp);
 }
 
 // the planned regions of a planned sweep (pair_plan.h; the direct ones go through bf_pairb_launch with

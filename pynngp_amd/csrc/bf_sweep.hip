@@ -193,8 +193,8 @@ __global__ __launch_bounds__(1024) void bf_finalize(const double* __restrict__ b
     }
 }
 
-// the separate fold of bf_pairb's tile records (pairb_fold_records, bf_pairb.h): one block of the same
-// kPairbThreads threads as the sweep's fused fold, so both give the same bits
+// the separate fold of bf_pairb's tile records (pairb_fold_records, bf_pairb.h): one block of kPairbThreads
+// threads, a fixed order
 // The tile count comes from the workspace header the sweep wrote; a count outside [0, bound] means the
 // workspace does not hold a pair-kernel sweep of n_rows rows (e.g. a deferred Matern sweep that ran on the
 // wavefront kernel, finalised as PAIRB): the fold then reads nothing and the partials are NaN (advice r04).
@@ -317,7 +317,7 @@ hipError_t bf_launch(const BfArgs& a, int algo, hipStream_t s) {
         ok = bf_pairb_launch(b, Pu, s);
         if (!ok) return hipErrorInvalidValue;
         hipError_t e = hipGetLastError();
-        if (e != hipSuccess || a.partials == nullptr || pairb_fuse_fold(a)) return e;
+        if (e != hipSuccess || a.partials == nullptr) return e;
         return bf_finalize_pairb_launch(a.bpart, a.n_rows, a.partials, s);
     } else if (algo == kAlgoQuad) {
         nb = bf_group_blocks(a.n_rows, 4);

@@ -338,7 +338,7 @@ int nngp_bf_sweep_blocks(const double* cov, const int32_t* nbr, const int32_t* o
     if (!(group ? nngp::bf_group_blocks_launch(args, s) : nngp::bf_pairb_blocks_launch(args, s)))
         return fail(NNGP_EUNSUP, "no covariance-block kernel for m=%d", m);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess && !(!group && nngp::pairb_fuse_fold(args)))
+    if (e == hipSuccess)
         e = group ? nngp::bf_finalize_launch((const double*)workspace, nngp::bf_group_blocks(n_rows, 4), partials, s)
                   : nngp::bf_finalize_pairb_launch(workspace, n_rows, partials, s);
     if (e != hipSuccess) return hip_fail(e, "bf_sweep_blocks launch");
@@ -537,6 +537,33 @@ int nngp_gibbs_w_sweep(const int32_t* member_rows, const int32_t* color_off_host
     hipError_t e = nngp::gibbs_w_sweep_launch(member_rows, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres,
                                               noise_w, w, r, rev_j, z, seed, sweep, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "gibbs_w_sweep launch");
+    return NNGP_OK;
+}
+
+int nngp_gibbs_w_sweep_tiles(const int32_t* tiles, const int32_t* phase_off_host, const int32_t* phase_lds_host,
+                             int32_t n_phases, const int32_t* tinfo, const int32_t* tstep, int32_t ecap,
+                             const int32_t* tfp, const int32_t* off, const int32_t* rev_loc, const void* prep,
+                             int64_t n, int32_t m, int64_t n_entries, double sigma2, double tau2, const double* yres,
+                             const double* noise_w, double* w, double* r, const double* z, void* stream) {
+    if (tiles == nullptr || phase_off_host == nullptr || phase_lds_host == nullptr || tinfo == nullptr ||
+        tstep == nullptr || tfp == nullptr || off == nullptr || prep == nullptr || yres == nullptr || w == nullptr ||
+        r == nullptr || z == nullptr || (n_entries > 0 && rev_loc == nullptr))
+        return fail(NNGP_EINVAL, "null pointer argument");
+    if (n_phases < 0 || n < 0 || m < 0 || m > NNGP_MAX_M || n_entries < 0 || n_entries > n * (int64_t)m)
+        return fail(NNGP_EINVAL, "bad n_phases, n, m or n_entries");
+    if (ecap < 0 || ecap > 2048) return fail(NNGP_EINVAL, "ecap=%d outside [0, 2048] (entries of one step)", ecap);
+    if (((uintptr_t)tinfo & 15) != 0) return fail(NNGP_EINVAL, "tinfo must be 16-byte aligned");
+    for (int p = 0; p < n_phases; ++p) {
+        if (phase_off_host[p + 1] < phase_off_host[p]) return fail(NNGP_EINVAL, "phase offsets must not decrease");
+        if (phase_lds_host[p] < 0 || phase_lds_host[p] > 160 * 1024)
+            return fail(NNGP_EINVAL, "phase %d needs %d B of LDS (> 160 KB)", p, phase_lds_host[p]);
+    }
+    if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
+        return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
+    hipError_t e = nngp::gibbs_tile_sweep_launch(tiles, phase_off_host, phase_lds_host, n_phases, tinfo, tstep, ecap,
+                                                 tfp, off, rev_loc, prep, n, m, n_entries, sigma2, tau2, yres, noise_w,
+                                                 w, r, z, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "gibbs_tile_sweep launch");
     return NNGP_OK;
 }
 

@@ -301,17 +301,13 @@ int64_t color_moral_graph_device(const int32_t* nbr, const int32_t* off, const i
 // fixed xor-butterfly sums their terms.  32 measured best for m = 15 (~15 children per
 // location): 8 lanes 1.30, 16 lanes 1.07, 32 lanes 1.05 ms per Gibbs iteration at
 // N = 1e6 -- the colour steps are latency bound.
-#ifndef NNGP_GIBBS_GROUP
 #define NNGP_GIBBS_GROUP 32
-#endif
 // ... each lane holding NNGP_GIBBS_PER children with their loads in flight together.  Fewer lanes
 // per member with more children each (fewer waves, no second round trip for the members with more
 // children than lanes) measured slower (round 3, profiles/r03s, ms per iteration at N = 1e6):
 // 32 x 1 0.799, 32 x 2 0.801, 16 x 2 0.859, 8 x 4 1.012 -- the steps want every gather in its own
 // lane (memory-level parallelism), not fewer waves.
-#ifndef NNGP_GIBBS_PER
 #define NNGP_GIBBS_PER 1
-#endif
 constexpr int kGroup = NNGP_GIBBS_GROUP;
 constexpr int kPer = NNGP_GIBBS_PER;
 constexpr int kSpan = kGroup * kPer;
@@ -323,10 +319,7 @@ constexpr int kSpan = kGroup * kPer;
 // (l ^ 15), instead of l ^ 4 (l ^ 8) -- the same two operands in the same order.  The quad steps and
 // the mirrors are DPP moves on the VALU; l ^ 16 is one ds_swizzle (bit mode) and l ^ 32 a
 // ds_bpermute: one LDS round trip instead of five.
-// (NNGP_GIBBS_DPP 0: the descending __shfl_xor butterfly, ds_bpermute per step -- the A/B baseline)
-#ifndef NNGP_GIBBS_DPP
-#define NNGP_GIBBS_DPP 1
-#endif
+// (the descending __shfl_xor butterfly, a ds_bpermute per step, was the A/B baseline)
 template <int CTRL>
 __device__ __forceinline__ double gdpp(double v) {
     const long long u = __double_as_longlong(v);
@@ -358,23 +351,11 @@ __device__ __forceinline__ double group_sum(double v) {
 //   rows:    kRowLanes lanes per location fold P_i over its contiguous reverse range
 //            (fixed order: lane-strided partial sums + a fixed xor-butterfly), 1 / Ft_i.
 // 0.183 ms per prepared phi at N = 1e6, m = 15 (tools/bench_prepare.py).  Measured and rejected
-// (round 3, profiles/r03k): one fused pass (NNGP_PREP_FUSED: L lanes per location, U entries per lane
+// (round 3, profiles/r03k): one fused pass (L lanes per location, U entries per lane
 // in flight, P_i folded without re-reading Brev / Grev) at L x U = 4 x 4 / 8 x 2 / 16 x 1 / 16 x 2:
 // 0.216 / 0.181 / 0.196 / 0.233 ms; the first version, kGroup lanes per location with one entry
 // each in flight, took 267 us.
-// NNGP_PREP_FUSED 0: the two streaming passes; 1: one pass, NNGP_PREP_LANES lanes per location with
-// NNGP_PREP_UNROLL entries each in flight
-#ifndef NNGP_PREP_FUSED
-#define NNGP_PREP_FUSED 0
-#endif
-#ifndef NNGP_PREP_LANES
-#define NNGP_PREP_LANES 4
-#endif
-#ifndef NNGP_PREP_UNROLL
-#define NNGP_PREP_UNROLL 4
-#endif
-constexpr int kRowLanes = NNGP_PREP_FUSED ? NNGP_PREP_LANES : 4;
-[[maybe_unused]] constexpr int kPrepUnroll = NNGP_PREP_UNROLL;
+constexpr int kRowLanes = 4;
 
 // Both passes cover the rows [row0, row1) -- the whole field, or the shard a rank of a sharded
 // chain owns (nngp_gibbs_prepare_range): the entries pass walks the contiguous reverse entries
@@ -418,55 +399,6 @@ __global__ __launch_bounds__(256) void gibbs_prepare_rows(const double* __restri
     }
 }
 
-#if NNGP_PREP_FUSED
-__global__ __launch_bounds__(256) void gibbs_prepare_fused(const double* __restrict__ B, const double* __restrict__ Ft,
-                                                           const int32_t* __restrict__ rev_j,
-                                                           const int32_t* __restrict__ rev_k,
-                                                           const int32_t* __restrict__ off, int64_t n, int m,
-                                                           double* __restrict__ Brev, double* __restrict__ Grev,
-                                                           double* __restrict__ P, double* __restrict__ invF) {
-    const int64_t t = xcd_logical_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    const int64_t i = t / kRowLanes;
-    const int l = (int)(t % kRowLanes);
-    const bool live = i < n;
-    const int64_t ic = live ? i : n - 1;
-    const int32_t e0 = off[ic], e1 = live ? off[ic + 1] : e0;
-    double acc = 0.0;
-    double bb[kPrepUnroll], gg[kPrepUnroll];
-#pragma unroll
-    for (int u = 0; u < kPrepUnroll; ++u) {  // the first kPrepUnroll entries of this lane, loads in flight together
-        const int32_t e = e0 + l + u * kRowLanes;
-        const bool has = e < e1;
-        const int64_t j = has ? (int64_t)rev_j[e] : 0;
-        const double b = has ? B[j * m + rev_k[e]] : 0.0;
-        bb[u] = b;
-        gg[u] = has ? b / Ft[j] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kPrepUnroll; ++u) {
-        const int32_t e = e0 + l + u * kRowLanes;
-        if (e < e1) {
-            Brev[e] = bb[u];
-            Grev[e] = gg[u];
-        }
-        acc = fma(bb[u], gg[u], acc);
-    }
-    for (int32_t e = e0 + l + kPrepUnroll * kRowLanes; e < e1; e += kRowLanes) {
-        const int64_t j = rev_j[e];
-        const double b = B[j * m + rev_k[e]];
-        const double g = b / Ft[j];
-        Brev[e] = b;
-        Grev[e] = g;
-        acc = fma(b, g, acc);
-    }
-#pragma unroll
-    for (int o = kRowLanes / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    if (live && l == 0) {
-        P[i] = acc;
-        invF[i] = 1.0 / Ft[i];
-    }
-}
-#endif
 
 struct GibbsPrep {
     double *Brev, *Grev, *P, *invF;
@@ -494,13 +426,6 @@ hipError_t gibbs_prepare_range_launch(const double* B, const double* Ft, const i
                                       hipStream_t s) {
     if (row1 <= row0) return hipSuccess;
     const GibbsPrep g = prep_layout(prep, n, m);
-#if NNGP_PREP_FUSED
-    if (row0 == 0 && row1 == n) {
-        hipLaunchKernelGGL(gibbs_prepare_fused, dim3((unsigned)((n * kRowLanes + 255) / 256)), dim3(256), 0, s, B, Ft,
-                           rev_j, rev_k, off, n, m, g.Brev, g.Grev, g.P, g.invF);
-        return hipGetLastError();
-    }
-#endif
     const int64_t rows = row1 - row0;
     // grid sized for m reverse entries per row (the average); the stride loop takes the rest
     const int64_t ne = rows * (int64_t)m;
@@ -553,6 +478,9 @@ hipError_t gibbs_member_rows_launch(const int32_t* members, int64_t n, const int
 // 7 waves per SIMD; without it 46 VGPRs, the 8-wave cap (round 4, profiles/r04l: 0.8022 -> 0.7885 ms per
 // Gibbs iteration at N = 1e6, median of 4 interleaved runs; the 8-wave cap binds, so asking the compiler
 // for more waves per SIMD changes nothing).
+// (Measured and not kept, round 6, profiles/r06e: the per-iteration streams of a colour step -- member rows,
+// the reverse entries, P, 1 / F, y - X beta, the normals -- read non-temporally, to keep r in the XCDs' L2s:
+// 0.829 against 0.792 ms per iteration, the colour kernel's L2 fetch unchanged at ~44 MB per launch.)
 template <bool INLINE_Z>
 __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ member_rows, int64_t n_members,
                                                      const double* __restrict__ Brev, const double* __restrict__ Grev,
@@ -616,12 +544,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color(const int4* __restrict__ me
         acc = c == 0 ? (has[0] ? gf[0] * rf[0] : 0.0) : (has[c] ? fma(gf[c], rf[c], acc) : acc);
     }
     for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(Grev[e], r[rev_j[e]], acc);
-#if NNGP_GIBBS_DPP
     acc = group_sum<kGroup>(acc);
-#else
-#pragma unroll
-    for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-#endif
     const double it2i = noise_w != nullptr ? it2 * hi : it2;  // 1 / (tau2 / h_i)
     const double prec = fma(iF + Pi, is2, it2i);
     const double lin = fma(yi, it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
@@ -672,6 +595,165 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
                        dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
                        (const int4*)member_rows, n_members, g.Brev, g.Grev, g.P, g.invF, 1.0 / tau2, 1.0 / sigma2, yres,
                        noise_w, w, r, rev_j, z, seed, sweep, w_out, var, n * (int64_t)m);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- tiled colour sweep (round 6)
+// pynngp_amd/gibbs_tiles.py builds the plan: spatial tiles whose footprints (each node and its children --
+// the r entries its update reads and writes) are disjoint within a launch.  One workgroup per tile holds
+// the footprint's r and the tile's new w in LDS, runs every colour of its nodes in order and writes r and
+// w back: the residuals cross HBM once per launch instead of once per colour.  The plan is contiguous
+// (SeqNNGP stores the nodes in its order): tile t's nodes are storage rows [n0, n1), colour-rank groups in
+// order, so the members of a step (<= 64 of one colour) and their reverse entries are contiguous ranges.
+// A step's operands -- per member 1 / F, P, y - X beta, the normal, w (and h), per reverse entry B, B / F
+// and the child's local index -- are loaded by the whole block (coalesced, one or two entries a thread)
+// two steps ahead into registers and written to one of two LDS step buffers after the current step: the
+// global latency is hidden behind two steps, and a member's children are read from LDS however many
+// there are.  A block barrier ends every step (the next buffer is ready; a colour's r updates are seen by
+// the next colour).  Per member the arithmetic is gibbs_w_color's (the same conditional; its 16-lane sum
+// of the children's terms is a fixed butterfly of its own order).
+constexpr int kTileThreads = 1024;
+constexpr int kTileLanes = 16;                         // lanes per member
+constexpr int kTileSlots = kTileThreads / kTileLanes;  // members per step (at most)
+constexpr int kTileEQ = 2;                             // staged entries per thread: a step holds <= 2048
+constexpr int kTileMem = 6;                            // staged values per member
+
+struct TileRegs {
+    double mv;
+    double g[kTileEQ], b[kTileEQ];
+    int32_t loc[kTileEQ];
+};
+
+__global__ __launch_bounds__(kTileThreads) void gibbs_tile_phase(
+    const int32_t* __restrict__ tiles, const int4* __restrict__ tinfo, const int32_t* __restrict__ tstep, int ecap,
+    int64_t n_entries, const int32_t* __restrict__ tfp, const int32_t* __restrict__ off,
+    const int32_t* __restrict__ rev_loc, const double* __restrict__ Brev, const double* __restrict__ Grev,
+    const double* __restrict__ P, const double* __restrict__ invF, const double* __restrict__ yres,
+    const double* __restrict__ noise_w, const double* __restrict__ z, double it2, double is2,
+    double* __restrict__ w, double* __restrict__ r) {
+    extern __shared__ double tile_lds[];
+    const int tile = tiles[blockIdx.x];
+    const int4 ta = tinfo[2 * tile], tb = tinfo[2 * tile + 1];  // rows [n0, n1), footprint, steps
+    const int n0 = ta.x, nn = ta.y - ta.x, nf = ta.w - ta.z, S = tb.y - tb.x;
+    const int bufd = kTileMem * kTileSlots + 2 * ecap;  // doubles per step buffer
+    double* const rl = tile_lds;                         // footprint r (its first nn: the tile's rows)
+    double* const wl = rl + nf;                          // the tile's new w
+    double* const bufs = wl + nn;                        // 2 step buffers: member values, B / F, B
+    int32_t* const locs = (int32_t*)(bufs + 2 * bufd);  // 2 x ecap local indices
+    int32_t* const eo = locs + 2 * ecap;                 // nn + 1 reverse-entry offsets off[n0 + k]
+    int32_t* const sk = eo + nn + 1;                     // S + 1 step starts (tile-local rows)
+    const int tid = (int)threadIdx.x;
+    for (int f = tid; f < nf; f += kTileThreads) rl[f] = r[tfp[ta.z + f]];
+    for (int k = tid; k <= nn; k += kTileThreads) eo[k] = off[n0 + k];
+    for (int q = tid; q <= S; q += kTileThreads) sk[q] = q < S ? tstep[tb.x + q] : nn;
+    __syncthreads();
+    // the member value this thread stages: field f of member j (threads >= 384 load a harmless copy)
+    const int mf = min(tid / kTileSlots, kTileMem - 1), mj = tid % kTileSlots;
+    const double* const msrc = mf == 0 ? invF : mf == 1 ? P : mf == 2 ? yres : mf == 3 ? z : mf == 4 ? w
+                             : (noise_w != nullptr ? noise_w : invF);
+    const int64_t ecl = n_entries > 0 ? n_entries - 1 : 0;
+    auto load = [&](int s, TileRegs& R) {  // every load unconditional (clamped): counted waits stay exact
+        if (s >= S) return;                // (block-uniform)
+        const int ka = sk[s], kb = sk[s + 1];
+        const int k = min(ka + mj, kb - 1);
+        R.mv = msrc[n0 + k];
+        if (n_entries == 0) return;
+        const int ea = eo[ka], ne = eo[kb] - ea;
+#pragma unroll
+        for (int q = 0; q < kTileEQ; ++q) {
+            const int x = tid + kTileThreads * q;
+            const int64_t e = min((int64_t)ea + min(x, max(ne - 1, 0)), ecl);
+            R.g[q] = Grev[e];
+            R.b[q] = Brev[e];
+            R.loc[q] = rev_loc[e];
+        }
+    };
+    auto store = [&](int s, const TileRegs& R) {  // into step buffer s & 1
+        if (s >= S) return;
+        double* const mem = bufs + (s & 1) * bufd;
+        double* const G = mem + kTileMem * kTileSlots;
+        double* const Bb = G + ecap;
+        int32_t* const L = locs + (s & 1) * ecap;
+        const int ka = sk[s], kb = sk[s + 1];
+        if (tid < kTileMem * kTileSlots && ka + mj < kb) mem[tid] = R.mv;
+        const int ne = eo[kb] - eo[ka];
+#pragma unroll
+        for (int q = 0; q < kTileEQ; ++q) {
+            const int x = tid + kTileThreads * q;
+            if (x < ne) {
+                G[x] = R.g[q];
+                Bb[x] = R.b[q];
+                L[x] = R.loc[q];
+            }
+        }
+    };
+    const int j = tid / kTileLanes, l = tid % kTileLanes;
+    auto compute = [&](int s) {
+        const double* const mem = bufs + (s & 1) * bufd;
+        const double* const G = mem + kTileMem * kTileSlots;
+        const double* const Bb = G + ecap;
+        const int32_t* const L = locs + (s & 1) * ecap;
+        const int ka = sk[s], kb = sk[s + 1];
+        const int k = ka + j;
+        if (k >= kb) {
+            (void)group_sum<kTileLanes>(0.0);  // (the butterfly is lane-collective: every lane joins)
+            return;
+        }
+        const int ea = eo[ka], e0 = eo[k] - ea, e1 = eo[k + 1] - ea;
+        double acc = 0.0;
+        for (int x = e0 + l; x < e1; x += kTileLanes) acc = fma(G[x], rl[L[x]], acc);
+        acc = group_sum<kTileLanes>(acc);
+        const double iF = mem[j], Pi = mem[kTileSlots + j], yi = mem[2 * kTileSlots + j];
+        const double zi = mem[3 * kTileSlots + j], wi = mem[4 * kTileSlots + j];
+        const double ri = rl[k];
+        const double it2i = noise_w != nullptr ? it2 * mem[5 * kTileSlots + j] : it2;
+        const double prec = fma(iF + Pi, is2, it2i);
+        const double lin = fma(yi, it2i, is2 * fma(wi - ri, iF, fma(wi, Pi, acc)));
+        const double sd = nngp_rsqrt(prec);
+        const double wn = fma(zi, sd, lin / prec);
+        const double dw = wn - wi;
+        if (l == 0) {
+            wl[k] = wn;
+            rl[k] = ri + dw;
+        }
+        for (int x = e0 + l; x < e1; x += kTileLanes) rl[L[x]] = fma(-Bb[x], dw, rl[L[x]]);
+    };
+    // two register sets: step s + 2 loads while step s computes; step s + 1 (loaded during step s - 1) is
+    // written to its buffer after step s, before the barrier that ends it
+    TileRegs Ra, Rb;
+    load(0, Ra);
+    load(1, Rb);
+    store(0, Ra);
+    __syncthreads();
+    for (int s = 0; s < S; s += 2) {
+        load(s + 2, Ra);
+        compute(s);
+        store(s + 1, Rb);
+        __syncthreads();
+        if (s + 1 >= S) break;
+        load(s + 3, Rb);
+        compute(s + 1);
+        store(s + 2, Ra);
+        __syncthreads();
+    }
+    for (int f = tid; f < nf; f += kTileThreads) r[tfp[ta.z + f]] = rl[f];
+    for (int k = tid; k < nn; k += kTileThreads) w[n0 + k] = wl[k];
+}
+
+hipError_t gibbs_tile_sweep_launch(const int32_t* tiles, const int32_t* phase_off_host, const int32_t* phase_lds_host,
+                                   int n_phases, const int32_t* tinfo, const int32_t* tstep, int ecap,
+                                   const int32_t* tfp, const int32_t* off, const int32_t* rev_loc, const void* prep,
+                                   int64_t n, int m, int64_t n_entries, double sigma2, double tau2,
+                                   const double* yres, const double* noise_w, double* w, double* r, const double* z,
+                                   hipStream_t s) {
+    const GibbsPrep g = prep_layout((void*)prep, n, m);
+    for (int p = 0; p < n_phases; ++p) {
+        const int nt = phase_off_host[p + 1] - phase_off_host[p];
+        if (nt <= 0) continue;
+        hipLaunchKernelGGL(gibbs_tile_phase, dim3((unsigned)nt), dim3(kTileThreads), (size_t)phase_lds_host[p], s,
+                           tiles + phase_off_host[p], (const int4*)tinfo, tstep, ecap, n_entries, tfp, off, rev_loc,
+                           g.Brev, g.Grev, g.P, g.invF, yres, noise_w, z, 1.0 / tau2, 1.0 / sigma2, w, r);
+    }
     return hipGetLastError();
 }
 
@@ -758,12 +840,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains(const int4* __restri
             acc = k == 0 ? (has[0] ? gf[c][0] * rf[c][0] : 0.0) : (has[k] ? fma(gf[c][k], rf[c][k], acc) : acc);
         }
         for (int32_t e = e0 + l + kSpan; e < e1; e += kGroup) acc = fma(cp.Grev[c][e], CR(c, rev_j[e]), acc);
-#if NNGP_GIBBS_DPP
         acc = group_sum<kGroup>(acc);
-#else
-#pragma unroll
-        for (int o = kGroup / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-#endif
         const double it2 = cp.it2[c], is2 = cp.is2[c];
         const double it2i = noise_w != nullptr ? it2 * hi : it2;
         const double prec = fma(iF[c] + Pi[c], is2, it2i);
@@ -890,12 +967,7 @@ __global__ __launch_bounds__(256) void gibbs_w_color_chains_il(const int4* __res
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         double a = acc[c];
-#if NNGP_GIBBS_DPP
         a = group_sum<kGroup>(a);
-#else
-#pragma unroll
-        for (int o = kGroup / 2; o > 0; o >>= 1) a += __shfl_xor(a, o);
-#endif
         const double it2 = cp.it2[c], is2 = cp.is2[c];
         const double it2i = noise_w != nullptr ? it2 * hi : it2;
         const double prec = fma(iF[c] + Pi[c], is2, it2i);

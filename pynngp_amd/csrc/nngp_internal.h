@@ -190,6 +190,12 @@ hipError_t gibbs_w_apply_launch(const int32_t* rows, int64_t n_rows, const doubl
                                 double* w, double* r, const int32_t* rev_j, const int32_t* rev_k, hipStream_t s);
 hipError_t gibbs_member_rows_launch(const int32_t* members, int64_t n, const int32_t* off, int32_t* rows,
                                     hipStream_t s);
+hipError_t gibbs_tile_sweep_launch(const int32_t* tiles, const int32_t* phase_off_host, const int32_t* phase_lds_host,
+                                   int n_phases, const int32_t* tinfo, const int32_t* tstep, int ecap,
+                                   const int32_t* tfp, const int32_t* off, const int32_t* rev_loc, const void* prep,
+                                   int64_t n, int m, int64_t n_entries, double sigma2, double tau2,
+                                   const double* yres, const double* noise_w, double* w, double* r, const double* z,
+                                   hipStream_t s);
 hipError_t gibbs_w_sweep_launch(const int32_t* member_rows, int n_colors, const int32_t* color_off_host,
                                 const void* prep, int64_t n, int m, double sigma2, double tau2,
                                 const double* yres, const double* noise_w, double* w, double* r,

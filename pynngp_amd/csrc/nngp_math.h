@@ -66,9 +66,7 @@ static __device__ const double kExp2Tab[256] = NNGP_EXP2_TAB;
                                  // "matern"; nu = 1/2, 3/2, 5/2 give the exponential / Matern-3/2 / -5/2 kinds)
 #define NNGP_N_KINDS 6
 #define NNGP_MATERN_NU_MAX 50.0
-#ifndef NNGP_MATERN_X_SWITCH
 #define NNGP_MATERN_X_SWITCH 1.5  // Temme below, the continued fraction above (the most accurate split, tests/test_matern.py)
-#endif
 // Runtime kind (the m = 25..32 kernels, one instantiation for kinds 0..4): every kind as
 // p(u) e, p(u) = 1 + c1 u + c2 u^2 + c3 u^3 with u = min(phi d, umax), e = 2^(nphi256 g / 256) with
 // g = d (g = d^2 for the gaussian kind; nphi256 = 0, i.e. e = 1, for the spherical kind).

@@ -109,12 +109,18 @@ class SeqNNGP:
     # the whole-field phi sweeps through a wave pair plan?  Off: slower than the unplanned kernel
     # (sweep.PLAN_DEFAULT, profiles/r06c); set True on an instance's class to opt in
     _use_plan = False
+    # nodes per level-0 tile of the tiled w sweep (sweep="tiled")
+    _tile_nodes = 2048
+    _tile_max_levels = 8
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
                  seed: int = 0, device=None, algo: str = "auto", w_init=None, eps=None, fix_tau2: bool = False,
                  ref=None, X_ref=None, nu: Optional[float] = None, cov=None, fix_phi: bool = False,
-                 fix_sigma2: bool = False):
+                 fix_sigma2: bool = False, sweep: str = "colour"):
+        if sweep not in ("colour", "tiled"):
+            raise ValueError(f"sweep must be 'colour' or 'tiled' (got {sweep!r})")
+        self.sweep_mode = sweep
         self.device = _default_device(device)
         dev = self.device
         # a covariance of the caller's own (the reference's plug-in cov(a, b), nngp.py:6,12): the latent
@@ -252,20 +258,8 @@ class SeqNNGP:
         # into Z-order STORAGE (slot p holds node perm[p]), so that a node's parents and
         # children sit near it in memory: the gathers and scatters of the sweeps share cache
         # lines.  The model is label-invariant (neighbour sets, colouring, conditionals); w is
-        # mapped back on output.
-        perm, _ = _lib.row_order(coords0)
-        self.perm = perm.long()
-        self.pos = torch.empty_like(self.perm)
-        self.pos[self.perm] = torch.arange(n, device=dev)
-        self.coords = coords0[self.perm].contiguous()
-        self.y = to(y_n)[self.perm].contiguous()
-        self.X = to(X_n)[self.perm].contiguous()
-        self._Xcols = self.X.t().contiguous()  # (p, n): y - X beta as p contiguous vector ops
-        self.noise_w = None if homoscedastic else to(h_n)[self.perm].contiguous()  # h_i, storage order
-        nb = nbr0[self.perm].long()
-        self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
-        self.off, self.rev_j, self.rev_k = _lib.reverse_neighbors(self.nbr)
-        # greedy colouring visits the nodes in MODEL order (S first, spatially scattered for
+        # mapped back on output (_relabel).
+        # The greedy colouring visits the nodes in MODEL order (S first, spatially scattered for
         # generation-order data: ~2x fewer colours than a scan in the spatial storage order);
         # the moral graph is label-invariant, so the colours carry over.  The leaves (data
         # locations outside S) are never parents, hence pairwise non-adjacent: they form one
@@ -274,12 +268,24 @@ class SeqNNGP:
         # on the device (round 5: the host greedy took ~10 s at N = 1e7; the same colours)
         colors0, self.n_colors, self.n_colors_ref = colour_dag(nbr0, off0, rev_j0, n_s)
         del off0, rev_j0
-        colors_d = colors0[self.perm]
-        self.colors = colors_d.cpu().numpy()
-        # members grouped by colour, storage (= Z) order inside a colour
-        self.members = torch.sort(colors_d, stable=True)[1].to(torch.int32)
-        self.color_off = np.concatenate([[0], np.cumsum(torch.bincount(colors_d, minlength=self.n_colors).cpu().numpy())
-                                         ]).astype(np.int32)
+        perm, _ = _lib.row_order(coords0)
+        self._relabel(perm.long(), coords0, y_n, X_n, None if homoscedastic else h_n, nbr0, colors0)
+        # the tiled w sweep (gibbs_tiles.py): one launch per phase of spatial tiles, r in LDS.  Its kernel
+        # wants each tile's nodes (colour-rank order) as one range of storage rows, so the storage order
+        # becomes the plan's node order, and the plan is rebuilt on the same tiles in that labelling
+        self._tiles = None
+        if sweep == "tiled":
+            from .gibbs_tiles import build_tile_plan
+
+            tp0 = build_tile_plan(self.coords, self.off, self.rev_j, self._colors_d, self.n_colors, self.n_colors_ref,
+                                  tile_nodes=self._tile_nodes, max_levels=self._tile_max_levels)
+            t0 = tp0.tnodes.long()
+            self._relabel(self.perm[t0], coords0, y_n, X_n, None if homoscedastic else h_n, nbr0, colors0)
+            self._tiles = build_tile_plan(self.coords, self.off, self.rev_j, self._colors_d, self.n_colors,
+                                          self.n_colors_ref, assign=(tp0.node_tile[t0], tp0.tile_level))
+            assert self._tiles.contiguous
+            del tp0, t0
+        del self._colors_d
         pos_h = self.pos.cpu().numpy()
         self._un_nodes = torch.from_numpy(pos_h[un_nodes].astype(np.int64)).to(dev)  # storage slots
         self._un_sd = to(un_sd)
@@ -351,6 +357,31 @@ class SeqNNGP:
         self.sum_logF, self.quad = float(ph[0]), float(ph[1])
 
     # ------------------------------------------------------------------ pieces
+    def _relabel(self, perm, coords0, y_n, X_n, h_n, nbr0, colors0):
+        """Storage order: slot p holds model node perm[p]; every per-node array, the neighbour sets (in
+        storage labels), their reverse lists and the colour groups follow it."""
+        dev = self.device
+        to = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+        n = coords0.shape[0]
+        self.perm = perm
+        self.pos = torch.empty_like(self.perm)
+        self.pos[self.perm] = torch.arange(n, device=dev)
+        self.coords = coords0[self.perm].contiguous()
+        self.y = to(y_n)[self.perm].contiguous()
+        self.X = to(X_n)[self.perm].contiguous()
+        self._Xcols = self.X.t().contiguous()  # (p, n): y - X beta as p contiguous vector ops
+        self.noise_w = None if h_n is None else to(h_n)[self.perm].contiguous()  # h_i, storage order
+        nb = nbr0[self.perm].long()
+        self.nbr = torch.where(nb >= 0, self.pos[nb.clamp(min=0)], -1).to(torch.int32).contiguous()
+        self.off, self.rev_j, self.rev_k = _lib.reverse_neighbors(self.nbr)
+        colors_d = colors0[self.perm]
+        self._colors_d = colors_d
+        self.colors = colors_d.cpu().numpy()
+        # members grouped by colour, storage order inside a colour
+        self.members = torch.sort(colors_d, stable=True)[1].to(torch.int32)
+        self.color_off = np.concatenate([[0], np.cumsum(torch.bincount(colors_d, minlength=self.n_colors).cpu().numpy())
+                                         ]).astype(np.int32)
+
     def _residual_y(self, beta):
         """y - X beta as elementwise device ops on contiguous columns (p is small; a tall-skinny
         GEMV is slower, and the strided columns of the row-major X took 18.7 us per op against
@@ -496,9 +527,18 @@ class SeqNNGP:
         """One iteration: phi; sigma2; update_wt; update_ws; tau2; beta; update_y_unobserved."""
         self.update_phi()
         self._before_w()
-        self.update_wt()
-        self.update_ws()
+        if self._tiles is not None:
+            self._sweep_tiles()  # update_wt and update_ws, tile by tile (the plan's order)
+        else:
+            self.update_wt()
+            self.update_ws()
         self._after_w(self._stats())
+
+    def _sweep_tiles(self):
+        """One w sweep through the tile plan (nngp_gibbs_w_sweep_tiles): every node's full conditional, in the
+        plan's (level, phase, colour) order -- leaves (update_wt) before the reference colours inside a tile."""
+        _lib.gibbs_w_sweep_tiles(self._tiles, self._prep, self.m, self.sigma2, self.tau2, self.yres, self.w, self.r,
+                                 self.off, self._z, noise_w=self.noise_w)
 
     def _before_w(self):
         """sigma2 | w, phi (held fixed on request, and with a callable covariance: its own scale), then the

@@ -1,0 +1,119 @@
+"""The tiled Gibbs sweep's plan on the host (pynngp_amd/gibbs_tiles.py, CPU tensors, no GPU).
+
+The plan is a valid Gibbs scan when every node lies in one tile, the tiles of one launch have disjoint
+footprints (each node and its children), every reverse entry's local index names its child, and the
+sweep order (level, phase, colour rank) is a proper colouring of the moral graph."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import nngp_gibbs_oracle as G
+from tests.test_gibbs_host import _reverse
+
+
+def off_of(nbr):
+    return _reverse(nbr)[0]
+
+
+def _plan(c_oracle, n, m, tile_nodes, seed, storage_perm=True, **kw):
+    from pynngp_amd import _lib
+    from pynngp_amd.gibbs_tiles import build_tile_plan, check_tile_plan
+
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(size=(n, 2))
+    nbr0 = c_oracle.c_knn_prior(c, m)
+    if storage_perm:  # a spatial-ish relabelling, as SeqNNGP stores nodes (children may precede parents)
+        perm = np.lexsort((c[:, 1], np.floor(c[:, 0] * 8)))
+        pos = np.empty(n, np.int64)
+        pos[perm] = np.arange(n)
+        nbr = np.where(nbr0[perm] >= 0, pos[np.maximum(nbr0[perm], 0)], -1).astype(np.int32)
+        c = c[perm]
+    else:
+        nbr = nbr0
+    off, rev_j = _reverse(nbr)
+    colors, nc = _lib.color_moral_graph(nbr, off, rev_j)
+    rev_j = np.concatenate([rev_j, np.zeros(n * m - rev_j.size, np.int32)])  # allocated for n m, as on the device
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    tp = build_tile_plan(t(c), t(off.astype(np.int64)), t(rev_j.astype(np.int64)), t(colors.astype(np.int64)), nc, nc,
+                         tile_nodes=tile_nodes, **kw)
+    check_tile_plan(tp, t(off.astype(np.int64)), t(rev_j.astype(np.int64)))
+    return nbr, colors, nc, tp
+
+
+@pytest.mark.parametrize("n,m,tile_nodes", [(1, 3, 16), (50, 1, 8), (600, 5, 32), (3000, 15, 256), (3000, 10, 4096)])
+def test_tile_plan_invariants(c_oracle, n, m, tile_nodes):
+    nbr, colors, nc, tp = _plan(c_oracle, n, m, tile_nodes, n + m)
+    assert G.coloring_is_valid(nbr, tp.effective_colors)
+    assert tp.effective_colors.min() == 0
+    ti = tp.tinfo.numpy()
+    assert (ti[:, 1] >= ti[:, 0]).all() and (ti[:, 3] - ti[:, 2] >= ti[:, 1] - ti[:, 0]).all()
+    # each footprint starts with its tile's nodes, in tnodes order
+    for a in range(ti.shape[0]):
+        np.testing.assert_array_equal(tp.tfp[ti[a, 2]:ti[a, 2] + ti[a, 1] - ti[a, 0]].numpy(),
+                                      tp.tnodes[ti[a, 0]:ti[a, 1]].numpy())
+    # colour-rank offsets cover each tile's nodes, and the nodes of rank k sit in [tcoff[k], tcoff[k+1])
+    tc = tp.tcoff.numpy()
+    np.testing.assert_array_equal(tc[:, -1], ti[:, 1] - ti[:, 0])
+    for a in range(ti.shape[0]):
+        nodes = tp.tnodes[ti[a, 0]:ti[a, 1]].numpy()
+        for k in range(tp.n_ranks):
+            assert (colors[nodes[tc[a, k]:tc[a, k + 1]]] == k).all()
+    assert sum(int(p.numel()) for p in tp.phases) == ti.shape[0]
+    assert max(tp.phase_lds) <= 144 * 1024
+    # steps: each inside one colour run of its tile, <= 64 members, <= ecap entries, covering the tile
+    deg = np.diff(off_of(nbr))
+    st = tp.tstep.numpy()
+    for a in range(ti.shape[0]):
+        ks = list(st[ti[a, 4]:ti[a, 5]]) + [ti[a, 1] - ti[a, 0]]
+        assert ks[0] == 0 and all(x < y for x, y in zip(ks, ks[1:]))
+        nodes = tp.tnodes[ti[a, 0]:ti[a, 1]].numpy()
+        for x, y in zip(ks, ks[1:]):
+            assert y - x <= 64 and len(set(colors[nodes[x:y]])) == 1
+            assert deg[nodes[x:y]].sum() <= tp.ecap
+        # colour boundaries are step boundaries
+        for k in range(tp.n_ranks + 1):
+            assert tc[a, k] in ks
+
+
+def test_tile_plan_cuts_into_several_launches(c_oracle):
+    _, _, nc, tp = _plan(c_oracle, 3000, 15, 256, 1)
+    assert tp.tinfo.shape[0] >= 8
+    # far fewer launches than tiles x colours; the phases of level 0 cover most nodes
+    assert len(tp.phases) < 4 * 9
+    ti = tp.tinfo.numpy()
+    lev0 = sum(int(ti[t, 1] - ti[t, 0]) for p in tp.phases[:1] for t in p.tolist())
+    assert lev0 > 0
+
+
+def test_tile_plan_reference_leaves_first(c_oracle):
+    """S != T: the leaf colour (update_wt) runs first inside each tile, then the reference colours."""
+    from pynngp_amd.gibbs import colour_dag
+    from pynngp_amd.gibbs_tiles import build_tile_plan, check_tile_plan
+
+    rng = np.random.default_rng(5)
+    s_pts, t_pts = rng.uniform(size=(400, 2)), rng.uniform(size=(900, 2))
+    coords, nbr = G.reference_dag(s_pts, t_pts, 6)
+    off, rev_j = _reverse(nbr)
+    colors, nc, nc_ref = colour_dag(nbr, off, rev_j, 400)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    tp = build_tile_plan(t(np.asarray(coords, np.float64)), t(off.astype(np.int64)), t(rev_j.astype(np.int64)),
+                         t(np.asarray(colors, np.int64)), nc, nc_ref, tile_nodes=128)
+    check_tile_plan(tp, t(off.astype(np.int64)), t(rev_j.astype(np.int64)))
+    assert G.coloring_is_valid(nbr, tp.effective_colors)
+    ti, tc = tp.tinfo.numpy(), tp.tcoff.numpy()
+    for a in range(ti.shape[0]):
+        nodes = tp.tnodes[ti[a, 0]:ti[a, 1]].numpy()
+        assert (np.asarray(colors)[nodes[:tc[a, 1]]] == nc_ref).all()  # rank 0 = the leaves
+        assert (np.asarray(colors)[nodes[tc[a, 1]:]] < nc_ref).all()
+
+
+def test_tile_plan_splits_tiles_over_the_lds(c_oracle):
+    """A tile whose footprint exceeds the LDS budget is cut into chunks of its nodes; the plan stays valid."""
+    nbr, colors, nc, tp0 = _plan(c_oracle, 3000, 15, 4096, 9)
+    lim = 64 * 1024  # (the step buffers take a fixed ~40 KB, a 3000-node tile ~48 KB more)
+    assert max(tp0.phase_lds) > lim
+    _, _, _, tp = _plan(c_oracle, 3000, 15, 4096, 9, lds_bytes=lim)
+    assert max(tp.phase_lds) <= lim and tp.tinfo.shape[0] > tp0.tinfo.shape[0]
+    assert G.coloring_is_valid(nbr, tp.effective_colors)
+    with pytest.raises(ValueError, match="children alone"):
+        _plan(c_oracle, 3000, 15, 1024, 9, lds_bytes=64)

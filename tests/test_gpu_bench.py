@@ -42,6 +42,11 @@ def test_bench_headline_contract(dev):
     _check(d, 20, 5)
     assert d["unit"] == "locations/s" and d["config"]["m"] == 15 and d["config"]["kind"] == "exponential"
     assert d["bad_rows"] == [-1, -1] and d["cpu_baseline"]["parity_max_rel_dF"] < 1e-10
+    # the live kernel time at the driver's --steps 20: at least 5 event-bracketed samples, and the
+    # per-launch loop time beside it
+    rf = d["roofline"]
+    assert rf["kernel_ms_samples"] >= 5 and rf["kernel_ms"] > 0 and rf["kernel_ms_loop_samples"] == 20
+    assert rf["kernel_ms_loop"] > 0
 
 
 def test_bench_config2_contract(dev):

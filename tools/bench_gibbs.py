@@ -29,7 +29,15 @@ ap.add_argument("--single-chain", action="store_true")
 ap.add_argument("--force-group", action="store_true")
 ap.add_argument("--backend", default="nccl")
 ap.add_argument("--graphs", type=int, default=None, help="single chain: 1/0 forces the HIP-graph colour loop on/off")
+ap.add_argument("--sweep", default="colour", choices=["colour", "tiled"],
+                help="the w sweep: one launch per colour, or the tiled sweep (gibbs_tiles.py, one launch per phase)")
+ap.add_argument("--tile-nodes", type=int, default=None, help="--sweep tiled: nodes per level-0 tile")
+ap.add_argument("--tile-levels", type=int, default=None, help="--sweep tiled: at most this many tile levels")
 args = ap.parse_args()
+if args.tile_nodes:
+    SeqNNGP._tile_nodes = args.tile_nodes
+if args.tile_levels:
+    SeqNNGP._tile_max_levels = args.tile_levels
 # several GPUs (torchrun): independent chains, one per GPU ("replicas only")
 world = int(os.environ.get("WORLD_SIZE", "1"))
 rank = int(os.environ.get("RANK", "0"))
@@ -58,7 +66,7 @@ if args.single_chain:
     g = ShardedSeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1, device=dev,
                        graphs=None if args.graphs is None else bool(args.graphs))
 else:
-    g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev)
+    g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev, sweep=args.sweep)
 torch.cuda.synchronize()
 setup_s = time.perf_counter() - t0
 for _ in range(args.warmup):
@@ -77,12 +85,30 @@ if grouped:
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+# the w sweep alone (normals drawn once; the same work as inside step())
+w_sweep_ms = None
+if not args.single_chain:
+    w_sweep = g._sweep_tiles if g._tiles is not None else (lambda: (g.update_wt(), g.update_ws()))
+    for _ in range(10):
+        w_sweep()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(100):
+        w_sweep()
+    e1.record()
+    torch.cuda.synchronize()
+    w_sweep_ms = e0.elapsed_time(e1) / 100
 if rank == 0:
-    extra = {}
+    extra = {"sweep": args.sweep, "w_sweep_ms": w_sweep_ms}
+    if getattr(g, "_tiles", None) is not None:
+        tp = g._tiles
+        extra.update(tiles=int(tp.tinfo.shape[0]), tile_launches=len(tp.phases), tile_levels=tp.levels,
+                     tiles_per_launch=[int(p.numel()) for p in tp.phases], steps=int(tp.tstep.numel()), ecap=tp.ecap,
+                     halo_fraction=float(tp.tfp.numel()) / args.n - 1.0)
     if args.single_chain:
-        extra = {"halo_rows": int(g._n_h), "replayed_rows": int(g._apply_rows.shape[0]),
+        extra.update({"halo_rows": int(g._n_h), "replayed_rows": int(g._apply_rows.shape[0]),
                  "collectives_per_iter": g._xchg.n_collectives / max(1, g.iteration), "group": grouped,
-                 "backend": args.backend if grouped else None, "graphs": len(g._graphs)}
+                 "backend": args.backend if grouped else None, "graphs": len(g._graphs)})
     chains = 1 if args.single_chain else world
     what = "ONE chain sharded over the GPUs" if args.single_chain else "one chain per GPU"
     print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, {what}", **extra,
