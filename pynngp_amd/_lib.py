@@ -879,12 +879,14 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
 
 def gibbs_w_sweep_tiles(plan, prep: torch.Tensor, m: int, sigma2: float, tau2: float, yres: torch.Tensor,
                         w: torch.Tensor, r: torch.Tensor, off: torch.Tensor, z: torch.Tensor,
-                        noise_w: Optional[torch.Tensor] = None) -> None:
+                        noise_w: Optional[torch.Tensor] = None, rev_j: Optional[torch.Tensor] = None) -> None:
     """The tiled colour sweep (nngp_gibbs_w_sweep_tiles) over a :class:`pynngp_amd.gibbs_tiles.TilePlan`: one
     launch per phase, each tile's footprint of r in LDS; in place on w and r; ``z`` the normals
     (:func:`gibbs_normals`).  The order is the plan's (level, phase, colour) -- its ``effective_colors`` as a
     colouring.  The plan must be contiguous (its node order is the storage order: ``plan.contiguous``;
-    :func:`pynngp_amd.gibbs_tiles.contiguous_plan` / SeqNNGP(sweep="tiled") arrange it)."""
+    :func:`pynngp_amd.gibbs_tiles.contiguous_plan` / SeqNNGP(sweep="tiled") arrange it).  A plan built with
+    coarse="colour" sweeps its coarse nodes after the tiles, one launch per colour (:func:`gibbs_w_sweep`,
+    which needs ``rev_j``)."""
     dev = _require_gpu(prep, yres, w, r, off, z, noise_w, plan.tinfo)
     _check_noise_w(noise_w, w.shape[0])
     if not plan.contiguous:
@@ -899,6 +901,13 @@ def gibbs_w_sweep_tiles(plan, prep: torch.Tensor, m: int, sigma2: float, tau2: f
                                            int(plan.rev_loc.numel()), float(sigma2), float(tau2), _ptr(yres),
                                            _ptr(noise_w), _ptr(w), _ptr(r), _ptr(z), _stream(dev)),
            "nngp_gibbs_w_sweep_tiles")
+    if plan.coarse_members is not None and plan.coarse_members.numel() > 0:
+        if rev_j is None:
+            raise ValueError("a tile plan with coarse nodes swept per colour needs rev_j")
+        if getattr(plan, "_coarse_rows", None) is None:
+            plan._coarse_rows = gibbs_member_rows(plan.coarse_members, off)
+        gibbs_w_sweep(plan.coarse_members, plan.coarse_color_off, prep, m, sigma2, tau2, yres, w, r, off, rev_j, 0, 0,
+                      z=z, noise_w=noise_w, member_rows=plan._coarse_rows)
 
 
 def gibbs_w_sweep_chains(member_rows: torch.Tensor, color_off_host, preps, m: int, sigma2s, tau2s, yres, w, r,

@@ -606,20 +606,25 @@ hipError_t gibbs_w_color_launch(const int32_t* member_rows, int64_t n_members, c
 // (SeqNNGP stores the nodes in its order): tile t's nodes are storage rows [n0, n1), colour-rank groups in
 // order, so the members of a step (<= 64 of one colour) and their reverse entries are contiguous ranges.
 // A step's operands -- per member 1 / F, P, y - X beta, the normal, w (and h), per reverse entry B, B / F
-// and the child's local index -- are loaded by the whole block (coalesced, one or two entries a thread)
-// two steps ahead into registers and written to one of two LDS step buffers after the current step: the
+// and the child's local index -- are loaded by the whole block (coalesced, a few entries a thread) two
+// steps ahead into registers and written to one of two LDS step buffers after the current step: the
 // global latency is hidden behind two steps, and a member's children are read from LDS however many
 // there are.  A block barrier ends every step (the next buffer is ready; a colour's r updates are seen by
 // the next colour).  Per member the arithmetic is gibbs_w_color's (the same conditional; its 16-lane sum
-// of the children's terms is a fixed butterfly of its own order).
+// of the children's terms is a fixed butterfly of its own order).  A step costs ~1.45 us even without its
+// global loads (a timing probe, tools/variants/tile_noload.patch, profiles/r06i): a tile's ~30-60 steps in
+// series outlast a colour launch's ~15 us per colour over the whole field, so this sweep is opt-in
+// (DESIGN.md 4.5).  (Measured and not kept: 4 lanes per member in 256-thread blocks, 2.2x slower per step --
+// a member's children then cost a chain of dependent LDS reads per lane, profiles/r06j.)
 constexpr int kTileThreads = 1024;
 constexpr int kTileLanes = 16;                         // lanes per member
 constexpr int kTileSlots = kTileThreads / kTileLanes;  // members per step (at most)
 constexpr int kTileEQ = 2;                             // staged entries per thread: a step holds <= 2048
 constexpr int kTileMem = 6;                            // staged values per member
+constexpr int kTileMQ = (kTileMem * kTileSlots + kTileThreads - 1) / kTileThreads;  // member values a thread
 
 struct TileRegs {
-    double mv;
+    double mv[kTileMQ];
     double g[kTileEQ], b[kTileEQ];
     int32_t loc[kTileEQ];
 };
@@ -635,29 +640,40 @@ __global__ __launch_bounds__(kTileThreads) void gibbs_tile_phase(
     const int tile = tiles[blockIdx.x];
     const int4 ta = tinfo[2 * tile], tb = tinfo[2 * tile + 1];  // rows [n0, n1), footprint, steps
     const int n0 = ta.x, nn = ta.y - ta.x, nf = ta.w - ta.z, S = tb.y - tb.x;
-    const int bufd = kTileMem * kTileSlots + 2 * ecap;  // doubles per step buffer
+    const int ecp = ecap + 1;                          // + a dummy slot (unconditional staging writes)
+    const int bufd = kTileMem * kTileSlots + 1 + 2 * ecp;  // doubles per step buffer
     double* const rl = tile_lds;                         // footprint r (its first nn: the tile's rows)
     double* const wl = rl + nf;                          // the tile's new w
     double* const bufs = wl + nn;                        // 2 step buffers: member values, B / F, B
-    int32_t* const locs = (int32_t*)(bufs + 2 * bufd);  // 2 x ecap local indices
-    int32_t* const eo = locs + 2 * ecap;                 // nn + 1 reverse-entry offsets off[n0 + k]
+    int32_t* const locs = (int32_t*)(bufs + 2 * bufd);  // 2 x (ecap + 1) local indices
+    int32_t* const eo = locs + 2 * ecp;                  // nn + 1 reverse-entry offsets off[n0 + k]
     int32_t* const sk = eo + nn + 1;                     // S + 1 step starts (tile-local rows)
     const int tid = (int)threadIdx.x;
     for (int f = tid; f < nf; f += kTileThreads) rl[f] = r[tfp[ta.z + f]];
     for (int k = tid; k <= nn; k += kTileThreads) eo[k] = off[n0 + k];
     for (int q = tid; q <= S; q += kTileThreads) sk[q] = q < S ? tstep[tb.x + q] : nn;
     __syncthreads();
-    // the member value this thread stages: field f of member j (threads >= 384 load a harmless copy)
-    const int mf = min(tid / kTileSlots, kTileMem - 1), mj = tid % kTileSlots;
-    const double* const msrc = mf == 0 ? invF : mf == 1 ? P : mf == 2 ? yres : mf == 3 ? z : mf == 4 ? w
-                             : (noise_w != nullptr ? noise_w : invF);
+    // the member values this thread stages: value v = tid + 256 q is field v / 64 of member v % 64 (past
+    // the 384 values: a harmless copy of the last field)
+    const double* msrc[kTileMQ];
+#pragma unroll
+    for (int q = 0; q < kTileMQ; ++q) {
+        const int mf = min((tid + kTileThreads * q) / kTileSlots, kTileMem - 1);
+        msrc[q] = mf == 0 ? invF : mf == 1 ? P : mf == 2 ? yres : mf == 3 ? z : mf == 4 ? w
+                : (noise_w != nullptr ? noise_w : invF);
+    }
+    const int mj = tid % kTileSlots;
     const int64_t ecl = n_entries > 0 ? n_entries - 1 : 0;
-    auto load = [&](int s, TileRegs& R) {  // every load unconditional (clamped): counted waits stay exact
-        if (s >= S) return;                // (block-uniform)
-        const int ka = sk[s], kb = sk[s + 1];
+    // Every load is unconditional (indices clamped into range; past the last step the last step reloads,
+    // unused): with no branch around them the compiler's counted waits stay exact -- a conditional load
+    // made it wait for every outstanding load (vmcnt(0)) before staging the previous step, serialising the
+    // pipeline (1.8 us per step, profiles/r06h).
+    auto load = [&](int s, TileRegs& R) {
+        const int sc = min(s, S - 1);
+        const int ka = sk[sc], kb = sk[sc + 1];
         const int k = min(ka + mj, kb - 1);
-        R.mv = msrc[n0 + k];
-        if (n_entries == 0) return;
+#pragma unroll
+        for (int q = 0; q < kTileMQ; ++q) R.mv[q] = msrc[q][n0 + k];
         const int ea = eo[ka], ne = eo[kb] - ea;
 #pragma unroll
         for (int q = 0; q < kTileEQ; ++q) {
@@ -668,31 +684,36 @@ __global__ __launch_bounds__(kTileThreads) void gibbs_tile_phase(
             R.loc[q] = rev_loc[e];
         }
     };
-    auto store = [&](int s, const TileRegs& R) {  // into step buffer s & 1
-        if (s >= S) return;
+    // into step buffer s & 1; unconditional too (what is not staged goes to the dummy slot), so that no
+    // branch leaves a staged register "maybe pending" for the compiler's waits
+    auto store = [&](int s, const TileRegs& R) {
+        const int sc = max(0, min(s, S - 1));  // (before the first / past the last step: a buffer not read)
         double* const mem = bufs + (s & 1) * bufd;
-        double* const G = mem + kTileMem * kTileSlots;
-        double* const Bb = G + ecap;
-        int32_t* const L = locs + (s & 1) * ecap;
-        const int ka = sk[s], kb = sk[s + 1];
-        if (tid < kTileMem * kTileSlots && ka + mj < kb) mem[tid] = R.mv;
+        double* const G = mem + kTileMem * kTileSlots + 1;
+        double* const Bb = G + ecp;
+        int32_t* const L = locs + (s & 1) * ecp;
+        const int ka = sk[sc], kb = sk[sc + 1];
+#pragma unroll
+        for (int q = 0; q < kTileMQ; ++q) {
+            const int v = tid + kTileThreads * q;
+            mem[v < kTileMem * kTileSlots && ka + mj < kb ? v : kTileMem * kTileSlots] = R.mv[q];
+        }
         const int ne = eo[kb] - eo[ka];
 #pragma unroll
         for (int q = 0; q < kTileEQ; ++q) {
             const int x = tid + kTileThreads * q;
-            if (x < ne) {
-                G[x] = R.g[q];
-                Bb[x] = R.b[q];
-                L[x] = R.loc[q];
-            }
+            const int xs = x < ne ? x : ecap;
+            G[xs] = R.g[q];
+            Bb[xs] = R.b[q];
+            L[xs] = R.loc[q];
         }
     };
     const int j = tid / kTileLanes, l = tid % kTileLanes;
     auto compute = [&](int s) {
         const double* const mem = bufs + (s & 1) * bufd;
-        const double* const G = mem + kTileMem * kTileSlots;
-        const double* const Bb = G + ecap;
-        const int32_t* const L = locs + (s & 1) * ecap;
+        const double* const G = mem + kTileMem * kTileSlots + 1;
+        const double* const Bb = G + ecp;
+        const int32_t* const L = locs + (s & 1) * ecp;
         const int ka = sk[s], kb = sk[s + 1];
         const int k = ka + j;
         if (k >= kb) {
@@ -719,20 +740,18 @@ __global__ __launch_bounds__(kTileThreads) void gibbs_tile_phase(
         for (int x = e0 + l; x < e1; x += kTileLanes) rl[L[x]] = fma(-Bb[x], dw, rl[L[x]]);
     };
     // two register sets: step s + 2 loads while step s computes; step s + 1 (loaded during step s - 1) is
-    // written to its buffer after step s, before the barrier that ends it
-    TileRegs Ra, Rb;
-    load(0, Ra);
-    load(1, Rb);
-    store(0, Ra);
-    __syncthreads();
-    for (int s = 0; s < S; s += 2) {
+    // written to its buffer after step s, before the barrier that ends it.  The loop starts two steps early
+    // (no compute) so that every load and staging write sits in the loop body: a separate prologue gave the
+    // loop head a merged "maybe pending" register state and early waits.
+    TileRegs Ra = {}, Rb = {};
+    for (int s = -2; s < S; s += 2) {
         load(s + 2, Ra);
-        compute(s);
+        if (s >= 0) compute(s);
         store(s + 1, Rb);
         __syncthreads();
         if (s + 1 >= S) break;
         load(s + 3, Rb);
-        compute(s + 1);
+        if (s + 1 >= 0) compute(s + 1);
         store(s + 2, Ra);
         __syncthreads();
     }
@@ -747,12 +766,17 @@ hipError_t gibbs_tile_sweep_launch(const int32_t* tiles, const int32_t* phase_of
                                    const double* yres, const double* noise_w, double* w, double* r, const double* z,
                                    hipStream_t s) {
     const GibbsPrep g = prep_layout((void*)prep, n, m);
+    // no reverse entries (m = 0, or no node has a child): the kernel's clamped entry loads read index 0 of
+    // arrays that exist (their values are never staged)
+    const double* Brev = n_entries > 0 ? g.Brev : g.P;
+    const double* Grev = n_entries > 0 ? g.Grev : g.P;
+    const int32_t* rloc = n_entries > 0 ? rev_loc : off;
     for (int p = 0; p < n_phases; ++p) {
         const int nt = phase_off_host[p + 1] - phase_off_host[p];
         if (nt <= 0) continue;
         hipLaunchKernelGGL(gibbs_tile_phase, dim3((unsigned)nt), dim3(kTileThreads), (size_t)phase_lds_host[p], s,
-                           tiles + phase_off_host[p], (const int4*)tinfo, tstep, ecap, n_entries, tfp, off, rev_loc,
-                           g.Brev, g.Grev, g.P, g.invF, yres, noise_w, z, 1.0 / tau2, 1.0 / sigma2, w, r);
+                           tiles + phase_off_host[p], (const int4*)tinfo, tstep, ecap, n_entries, tfp, off, rloc,
+                           Brev, Grev, g.P, g.invF, yres, noise_w, z, 1.0 / tau2, 1.0 / sigma2, w, r);
     }
     return hipGetLastError();
 }

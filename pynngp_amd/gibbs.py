@@ -110,8 +110,9 @@ class SeqNNGP:
     # (sweep.PLAN_DEFAULT, profiles/r06c); set True on an instance's class to opt in
     _use_plan = False
     # nodes per level-0 tile of the tiled w sweep (sweep="tiled")
-    _tile_nodes = 2048
+    _tile_nodes = 1024
     _tile_max_levels = 8
+    _tile_coarse = "colour"  # the nodes above level 0: "colour" (per-colour launches) or "tiles"
 
     def __init__(self, coords, y, X=None, m: int = 15, kind: str = "exponential", priors: Optional[Priors] = None,
                  sigma2: float = 1.0, tau2: float = 0.1, phi: Optional[float] = None, phi_tuning: float = 0.05,
@@ -270,6 +271,10 @@ class SeqNNGP:
         del off0, rev_j0
         perm, _ = _lib.row_order(coords0)
         self._relabel(perm.long(), coords0, y_n, X_n, None if homoscedastic else h_n, nbr0, colors0)
+        # (Measured and not kept, round 6, profiles/r06k: colour-major storage -- each colour's members one
+        # run of rows, so a colour step reads their operands contiguously: the colour kernel's L2 fetch halved,
+        # 44 -> 18 MB per launch, its time unchanged at 15.5 us (latency bound), and the
+        # prepare's gathers slowed: 0.797 vs 0.787 ms per iteration.)
         # the tiled w sweep (gibbs_tiles.py): one launch per phase of spatial tiles, r in LDS.  Its kernel
         # wants each tile's nodes (colour-rank order) as one range of storage rows, so the storage order
         # becomes the plan's node order, and the plan is rebuilt on the same tiles in that labelling
@@ -278,11 +283,12 @@ class SeqNNGP:
             from .gibbs_tiles import build_tile_plan
 
             tp0 = build_tile_plan(self.coords, self.off, self.rev_j, self._colors_d, self.n_colors, self.n_colors_ref,
-                                  tile_nodes=self._tile_nodes, max_levels=self._tile_max_levels)
+                                  tile_nodes=self._tile_nodes, max_levels=self._tile_max_levels,
+                                  coarse=self._tile_coarse)
             t0 = tp0.tnodes.long()
             self._relabel(self.perm[t0], coords0, y_n, X_n, None if homoscedastic else h_n, nbr0, colors0)
             self._tiles = build_tile_plan(self.coords, self.off, self.rev_j, self._colors_d, self.n_colors,
-                                          self.n_colors_ref, assign=(tp0.node_tile[t0], tp0.tile_level))
+                                          self.n_colors_ref, assign=(tp0.node_tile[t0], tp0.tile_level, tp0.coarse_tile))
             assert self._tiles.contiguous
             del tp0, t0
         del self._colors_d
@@ -538,7 +544,7 @@ class SeqNNGP:
         """One w sweep through the tile plan (nngp_gibbs_w_sweep_tiles): every node's full conditional, in the
         plan's (level, phase, colour) order -- leaves (update_wt) before the reference colours inside a tile."""
         _lib.gibbs_w_sweep_tiles(self._tiles, self._prep, self.m, self.sigma2, self.tau2, self.yres, self.w, self.r,
-                                 self.off, self._z, noise_w=self.noise_w)
+                                 self.off, self._z, noise_w=self.noise_w, rev_j=self.rev_j)
 
     def _before_w(self):
         """sigma2 | w, phi (held fixed on request, and with a callable covariance: its own scale), then the

@@ -38,7 +38,8 @@ def tile_lds_bytes(n_footprint, n_nodes, n_steps, ecap):
     """gibbs_tile_phase's LDS for one tile: the footprint's r and the rows' new w (8 B each), two step
     buffers (64 members x 6 doubles, ecap x (B, B / F, local index)), the tile's entry offsets (4 B per row
     + 1) and its step starts (4 B per step + 1), 16-B aligned"""
-    b = (8 * n_footprint + 8 * n_nodes + 2 * (8 * (6 * STEP_MEMBERS + 2 * ecap) + 4 * ecap) + 4 * (n_nodes + 1)
+    ecp = ecap + 1  # (+ a dummy slot)
+    b = (8 * n_footprint + 8 * n_nodes + 2 * (8 * (6 * STEP_MEMBERS + 1 + 2 * ecp) + 4 * ecp) + 4 * (n_nodes + 1)
          + 4 * (n_steps + 1))
     return (b + 15) // 16 * 16
 
@@ -58,6 +59,9 @@ class TilePlan:
     effective_colors: np.ndarray  # int64 (n,) storage order: the sweep's order as a colouring
     tstep: torch.Tensor = None       # int32: per tile its steps' first members (tile-local), in order
     ecap: int = 0                    # the most reverse entries of one step
+    coarse_tile: int = -1            # coarse="colour": the pseudo tile of the nodes above level 0 (not launched)
+    coarse_members: torch.Tensor = None  # ... its nodes by colour rank (int32), swept after the tiles
+    coarse_color_off: np.ndarray = None  # ... host int32 colour-rank offsets into coarse_members
     node_tile: torch.Tensor = None   # long (n,): each node's tile (storage order)
     tile_level: torch.Tensor = None  # long (n_tiles,)
     contiguous: bool = False  # tnodes is the identity: tile t's nodes are storage rows [n0, n1) (the kernel's
@@ -126,11 +130,14 @@ def _tiling(coords, dmax, tile_nodes, max_levels):
 
 def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor, colors: torch.Tensor,
                     n_colors: int, n_colors_ref: int, tile_nodes: int = 2048, max_levels: int = 8,
-                    lds_bytes: int = TILE_LDS_BYTES, assign=None) -> TilePlan:
+                    lds_bytes: int = TILE_LDS_BYTES, assign=None, coarse: str = "tiles") -> TilePlan:
     """Tiles, phases and local indices for the tiled colour sweep (storage-order arrays on the device).
 
     coords (n, d); off (n + 1,), rev_j: the reverse neighbour lists (children, the first off[n] entries);
-    colors (n,) long."""
+    colors (n,) long.  coarse="colour": the nodes above level 0 are not tiled but swept after the tiles, one
+    launch per colour (the per-colour kernel; their tiles' serial colour chains cost more than the launches)."""
+    if coarse not in ("tiles", "colour"):
+        raise ValueError(f"coarse must be 'tiles' or 'colour' (got {coarse!r})")
     dev = coords.device
     n, D = coords.shape
     off = off.long()
@@ -145,6 +152,7 @@ def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor
     rank = colour_rank(colors.long(), n_colors, n_colors_ref)
     n_ranks = int(max(n_colors, 1))
     ar = torch.arange(n, device=dev)
+    coarse_tile = -1
     maxdeg = int(counts.max()) if n else 0
     ecap_bound = STEP_ENTRIES + maxdeg
     if ecap_bound > MAX_ECAP:
@@ -153,11 +161,19 @@ def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor
         # the tiling of an earlier plan of the same field under another labelling (SeqNNGP relabels its
         # storage into the plan's node order, then rebuilds the plan there: tnodes = identity)
         tile_of, tile_level = assign[0].long(), assign[1].long()
+        coarse_tile = int(assign[2]) if len(assign) > 2 else -1
         n_tiles = int(tile_level.numel())
         levels = int(tile_level.max()) + 1 if n_tiles else 0
         fp_t, fp_x = _footprints(tile_of, owner, child, n)
     else:
         tile_of, level, levels = _tiling(coords, dmax, tile_nodes, max_levels)
+        cmask = level >= 1 if coarse == "colour" else torch.zeros(n, dtype=torch.bool, device=dev)
+        if bool(cmask.any()):  # every coarse node in one pseudo tile (level 1), swept per colour
+            tile_of = tile_of.clone()
+            tile_of[cmask] = int(tile_of[~cmask].max()) + 1 if bool((~cmask).any()) else 0
+            tile_of = torch.unique(tile_of, return_inverse=True)[1]
+            level = torch.where(cmask, torch.ones_like(level), level)
+            levels = 2
         # A tile whose footprint exceeds the LDS is cut into chunks of its nodes in storage order: the
         # early nodes of a generation-ordered field have ~m ln(n / i) children each, so a coarse cell of a
         # few hundred of them can reach 20k footprint entries (N = 1e6, m = 15).  Any node partition is a
@@ -168,6 +184,9 @@ def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor
             fp_t, fp_x = _footprints(tile_of, owner, child, n)
             nn_t = torch.bincount(tile_of, minlength=n_tiles)
             need = tile_lds_bytes(torch.bincount(fp_t, minlength=n_tiles), nn_t, nn_t + n_ranks, ecap_bound)
+            coarse_tile = int(tile_of[cmask][0]) if bool(cmask.any()) else -1
+            if coarse_tile >= 0:
+                need[coarse_tile] = 0  # (not run by the tile kernel)
             if n == 0 or int(need.max()) <= cap:
                 break
             parts = torch.clamp((need * 5 + 4 * cap - 1) // (4 * cap), min=1)  # ~80% full chunks
@@ -297,7 +316,15 @@ def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor
     phases, phase_lds = [], []
     tkey_h = launch_of_tile.cpu().numpy()
     n0_h, fsz_h, nn_h, nst_h = n0.cpu().numpy(), fsz.cpu().numpy(), nn.cpu().numpy(), nst.cpu().numpy()
+    coarse_members, coarse_off = None, None
+    if coarse_tile >= 0:
+        coarse_members = tnodes[int(n0[coarse_tile]):int(n1[coarse_tile])].to(torch.int32).contiguous()
+        coarse_off = tco[coarse_tile].cpu().numpy().astype(np.int32)
+        tkey_h = tkey_h.copy()
+        tkey_h[coarse_tile] = -1
     for lk in np.unique(tkey_h):
+        if lk < 0:
+            continue
         ts_ = np.nonzero(tkey_h == lk)[0]
         ts_ = ts_[np.argsort(n0_h[ts_])]
         phases.append(torch.from_numpy(ts_.astype(np.int32)).to(dev))
@@ -312,6 +339,7 @@ def build_tile_plan(coords: torch.Tensor, off: torch.Tensor, rev_j: torch.Tensor
                     tcoff=tco.to(torch.int32).contiguous(), rev_loc=rev_loc.to(torch.int32).contiguous(),
                     phases=phases, phase_lds=phase_lds, n_ranks=n_ranks, levels=levels,
                     effective_colors=eff.astype(np.int64), tstep=tstep.to(torch.int32).contiguous(), ecap=ecap,
+                    coarse_tile=coarse_tile, coarse_members=coarse_members, coarse_color_off=coarse_off,
                     node_tile=tile_of, tile_level=tile_level,
                     contiguous=bool(torch.equal(tnodes, ar)))
 
@@ -334,7 +362,7 @@ def contiguous_plan(coords: torch.Tensor, nbr: torch.Tensor, colors: torch.Tenso
     off2, rev_j2, rev_k2 = _lib.reverse_neighbors(nbr2)
     kw.pop("assign", None)
     tp = build_tile_plan(coords[perm].contiguous(), off2, rev_j2, colors[perm], n_colors, n_colors_ref,
-                         assign=(tp0.node_tile[perm], tp0.tile_level), **kw)
+                         assign=(tp0.node_tile[perm], tp0.tile_level, tp0.coarse_tile), **kw)
     assert tp.contiguous
     return perm, nbr2, off2, rev_j2, rev_k2, tp
 

@@ -117,3 +117,21 @@ def test_tile_plan_splits_tiles_over_the_lds(c_oracle):
     assert G.coloring_is_valid(nbr, tp.effective_colors)
     with pytest.raises(ValueError, match="children alone"):
         _plan(c_oracle, 3000, 15, 1024, 9, lds_bytes=64)
+
+
+def test_tile_plan_coarse_colour(c_oracle):
+    """coarse="colour": the nodes above level 0 leave the tiles for one pseudo tile swept per colour, last"""
+    nbr, colors, nc, tp = _plan(c_oracle, 3000, 15, 64, 11, coarse="colour")
+    assert tp.coarse_tile >= 0 and tp.coarse_members is not None
+    cm = tp.coarse_members.numpy()
+    co = tp.coarse_color_off
+    assert co[0] == 0 and co[-1] == cm.size and (np.diff(co) >= 0).all()
+    for k in range(len(co) - 1):
+        assert (colors[cm[co[k]:co[k + 1]]] == k).all()
+    launched = np.concatenate([p.numpy() for p in tp.phases])
+    assert tp.coarse_tile not in launched
+    assert G.coloring_is_valid(nbr, tp.effective_colors)
+    # the coarse nodes come last in the sweep order
+    eff = tp.effective_colors
+    rest = np.setdiff1d(np.arange(3000), cm)
+    assert eff[cm].min() > eff[rest].max()

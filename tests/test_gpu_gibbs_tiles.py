@@ -15,7 +15,7 @@ from oracle import nngp_gibbs_oracle as G
 pytestmark = pytest.mark.gpu
 
 
-def _setup(dev, n, m, phi=6.0, seed=0, tile_nodes=256):
+def _setup(dev, n, m, phi=6.0, seed=0, tile_nodes=256, coarse="tiles"):
     """A field stored in its tile plan's node order (gibbs_tiles.contiguous_plan), then B / F / r there"""
     from pynngp_amd import _lib
     from pynngp_amd.gibbs_tiles import check_tile_plan, contiguous_plan
@@ -26,7 +26,7 @@ def _setup(dev, n, m, phi=6.0, seed=0, tile_nodes=256):
     off0, rev_j0, _ = _lib.reverse_neighbors(nbr0)
     colors0, nc = _lib.color_moral_graph(nbr0.cpu().numpy(), off0.cpu().numpy(), rev_j0.cpu().numpy())
     perm, nbr, off, rev_j, rev_k, tp = contiguous_plan(c0, nbr0, torch.from_numpy(colors0.astype(np.int64)).to(dev),
-                                                       nc, nc, tile_nodes=tile_nodes)
+                                                       nc, nc, tile_nodes=tile_nodes, coarse=coarse)
     check_tile_plan(tp, off, rev_j)
     c = c0[perm].contiguous()
     colors = colors0[perm.cpu().numpy()]
@@ -42,17 +42,21 @@ def _residuals(nbr, B, w):
     return w - (B * wn).sum(1)
 
 
-@pytest.mark.parametrize("n,m,sigma2,tau2,weighted,tile_nodes", [(400, 5, 1.3, 0.2, False, 64),
-                                                                 (3000, 15, 2.0, 1.0, False, 256),
-                                                                 (3000, 10, 0.7, 0.05, True, 512),
-                                                                 (20000, 15, 1.0, 0.1, False, 2048)])
-def test_tiled_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted, tile_nodes):
-    """One tiled sweep with given normals equals the dense full-conditional sweep in the plan's order."""
+@pytest.mark.parametrize("n,m,sigma2,tau2,weighted,tile_nodes,coarse", [
+    (400, 5, 1.3, 0.2, False, 64, "tiles"), (3000, 15, 2.0, 1.0, False, 256, "tiles"),
+    (3000, 10, 0.7, 0.05, True, 512, "tiles"), (20000, 15, 1.0, 0.1, False, 2048, "tiles"),
+    (400, 5, 1.3, 0.2, False, 64, "colour"), (3000, 15, 2.0, 1.0, True, 256, "colour"),
+    (20000, 15, 1.0, 0.1, False, 2048, "colour")])
+def test_tiled_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted, tile_nodes, coarse):
+    """One tiled sweep with given normals equals the dense full-conditional sweep in the plan's order
+    (coarse="colour": the nodes above level 0 swept after the tiles, one launch per colour)."""
     from pynngp_amd import _lib
 
-    s = _setup(dev, n, m, seed=n + m, tile_nodes=tile_nodes)
+    s = _setup(dev, n, m, seed=n + m, tile_nodes=tile_nodes, coarse=coarse)
     tp = s["tp"]
     assert len(tp.phases) >= 2
+    if coarse == "colour":
+        assert tp.coarse_members is not None and tp.coarse_members.numel() > 0
     rng = s["rng"]
     yres = torch.from_numpy(rng.standard_normal(n) * 1.5).to(dev)
     z = torch.from_numpy(rng.standard_normal(n)).to(dev)
@@ -62,7 +66,7 @@ def test_tiled_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted, til
     w, r = s["w"].clone(), s["R"].clone()
     prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
     _lib.gibbs_w_sweep_tiles(tp, prep, m, sigma2, tau2, yres, w, r, s["off"], z,
-                             noise_w=torch.from_numpy(h).to(dev) if weighted else None)
+                             noise_w=torch.from_numpy(h).to(dev) if weighted else None, rev_j=s["rev_j"])
     wh = w.cpu().numpy()
     if n <= 5000:
         P = G.precision(nbr, B, F * sigma2) + np.diag(h / tau2)
@@ -182,7 +186,8 @@ def test_seqnngp_tiled_reference_set(dev):
     b = g.yres.cpu().numpy() * h / g.tau2
     w0 = g.w.cpu().numpy().copy()
     w_ref = G.color_sweep(P, b, w0, tp.effective_colors, z.cpu().numpy())
-    _lib.gibbs_w_sweep_tiles(tp, g._prep, g.m, g.sigma2, g.tau2, g.yres, g.w, g.r, g.off, z, noise_w=g.noise_w)
+    _lib.gibbs_w_sweep_tiles(tp, g._prep, g.m, g.sigma2, g.tau2, g.yres, g.w, g.r, g.off, z, noise_w=g.noise_w,
+                             rev_j=g.rev_j)
     np.testing.assert_allclose(g.w.cpu().numpy(), w_ref, rtol=1e-9, atol=1e-9 * np.abs(w_ref).max())
     assert bool(leaf.any())
     g.sample(50)
