@@ -66,7 +66,7 @@ constexpr int kPairbDedupMax = 17;
 // Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
 // Scalar-pivot LDL^T in the 2x2-blocked layout (reciprocals, unit factor) instead of the Cholesky factor
 // (inverse square roots) for the right-looking kernels: -44 VALU per wave at m = 15 (-1.7 %), -0.6 % time
-// (same-box A/B), every GPU parity test unchanged; except at m = 18 (the Matern-nu / blocks kinds there),
+// (same-box A/B), every GPU parity test unchanged; except at m = 18 (the blocks kind there),
 // where the two-wave register budget is tight (80 -> 216 B of scratch).
 constexpr int kPairbSldlSkipM = 18;
 // Left-looking elimination (m in [kPairbLeftMin, 32], the fused kinds): column pair by column pair, each
@@ -83,11 +83,21 @@ constexpr int kPairbLeftMin = 18;
 constexpr int kPairbLeftOneWaveMin = 23;
 constexpr int kPairbLeftLdsRows = 5;    // factor rows in LDS at two waves per SIMD (123 KB of 160 per CU)
 constexpr int kPairbLeftLdsRows1W = 7;  // ... and at one wave per SIMD (with the late state in LDS)
+// The general-nu Matern kind (its covariances from the launch's LDS table) is left-looking at m = 18 only, at
+// one wave per SIMD with 6 factor rows beside its <= 35 KB table: 0.694 vs 0.849 ms per 10^6 rows right-looking
+// (two waves, 736 B of scratch); from m = 19 its table evaluation's registers spill in the left-looking form
+// (224 - 1,344 B per lane at m = 20..24) and the right-looking one-wave kernel is faster: m = 19 0.699 vs 0.688,
+// m = 20 0.890 vs 0.780, m = 24 2.56 vs 1.31 (profiles/r06n, nu = 1.3).  (At two waves per SIMD the
+// left-looking Matern kernel spilled 1-2 KB per lane.)  The covariance-blocks kind stays right-looking: its
+// entries come from the caller's block array, whose per-column reads a left-looking form would put on the
+// column loop's critical path.
+constexpr int kPairbLeftMaternM = 18;
+constexpr int kPairbLeftLdsRowsMT = 6;
 constexpr bool pairb_left(int m) { return m >= kPairbLeftMin && m <= 32; }
-// the same for a kernel of covariance kind `kind` (the covariance-blocks and Matern-table kernels are
-// right-looking)
+// the same for a kernel of covariance kind `kind` (the covariance-blocks kernels are right-looking, the
+// Matern-table ones left-looking at m = kPairbLeftMaternM only)
 constexpr bool pairb_lk(int m, int kind) {
-    return pairb_left(m) && kind != NNGP_KIND_BLOCKS && kind != NNGP_KIND_MATERN;
+    return pairb_left(m) && kind != NNGP_KIND_BLOCKS && (kind != NNGP_KIND_MATERN || m == kPairbLeftMaternM);
 }
 // static per-phase budgets (tools/isa_phases.py): tools/variants/phases.h defines NNGP_PHASE to fence the
 // phases with named markers (hipcc -include tools/variants/phases.h); a product build leaves them empty
@@ -109,7 +119,7 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 }
 
 // Occupancy: up to m = kPairbTwoWavesMax the compiler is asked for two waves per SIMD (<= 256 VGPRs):
-// m = 16 / 17 fit without spills; m = 18 (the right-looking Matern-nu / blocks kinds) spills 20 dwords and
+// m = 16 / 17 fit without spills; m = 18 (the right-looking blocks kind) spills 20 dwords and
 // still runs ~30 % faster than at one wave per SIMD (0.314 vs 0.435 ms per 10^6 rows, profiles/r02ap).  From
 // m = 20 (342 VGPRs) the right-looking kernels' forced spills (91 dwords) cost more than the second wave gains
 // (+52 % at m = 20, 2-3x at m = 22 / 24).  Three waves per SIMD (<= 168 VGPRs) up to m = kPairbThreeWavesMax:
@@ -120,6 +130,7 @@ constexpr int kPairbThreeWavesMax = 13;
 // waves per SIMD the kernel for (m, kind) is built for: blocks per CU
 constexpr int pairb_waves_per_simd(int m, int kind) {
     return m <= kPairbThreeWavesMax ? 3
+           : (pairb_lk(m, kind) && kind == NNGP_KIND_MATERN) ? 1
            : (m <= kPairbTwoWavesMax || (pairb_lk(m, kind) && m < kPairbLeftOneWaveMin)) ? 2
                                                                                           : 1;
 }
@@ -348,7 +359,8 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     // (no value column in the elimination: the residual is r = v_i - B v_N after the back-substitution, the
     // oracle's own formula -- 5 % fewer VALU at m = 15 than forward-solving the values through it)
     constexpr bool SLDL = !LEFT && M != kPairbSldlSkipM;
-    constexpr int KL0 = M >= kPairbLeftOneWaveMin ? kPairbLeftLdsRows1W : kPairbLeftLdsRows;
+    constexpr int KL0 = MT ? kPairbLeftLdsRowsMT
+                           : (M >= kPairbLeftOneWaveMin ? kPairbLeftLdsRows1W : kPairbLeftLdsRows);
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
     // the left-looking kernel's LDS in one object: the exp table first (its reads fold the base into the
     // 16-bit offset field; the LDS lowering sorts separate objects by size, which put it above 64 KB), the
@@ -1111,7 +1123,7 @@ static bool launch_pairb_if(const BfArgs& a, const CovParams& Pc, hipStream_t s)
         case 2: launch_pairb_mkd<M, 2, D>(a, Pc, s); return true;
         case 3: launch_pairb_mkd<M, 3, D>(a, Pc, s); return true;
         case 4: launch_pairb_mkd<M, 4, D>(a, Pc, s); return true;
-        case NNGP_KIND_MATERN:  // right-looking (the table path); above m = 24 the four-lane kernel serves it
+        case NNGP_KIND_MATERN:  // the table path (left-looking at m = 18); above m = 24 the four-lane kernel
             if constexpr (M <= 24) {
                 launch_pairb_mkd<M, NNGP_KIND_MATERN, D>(a, Pc, s);
                 return true;

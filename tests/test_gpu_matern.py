@@ -69,6 +69,10 @@ def _check(dev, lib, O, coords, nbr, theta, nu, y, algo="auto"):
     (6.0, (1.0, 40.0, 0.1), 26, 1),
     (35.0, (1.0, 80.0, 0.1), 20, 2),
     (1.0, (1.0, 12.0, 0.1), 24, 3),
+    (1.3, (1.0, 10.0, 0.1), 18, 2),  # m = 18: the left-looking Matern kernel (round 6), every dimension
+    (0.7, (1.0, 8.0, 0.05), 18, 1),
+    (2.9, (1.0, 14.0, 0.05), 18, 3),
+    (0.3, (1.0, 20.0, 0.1), 19, 2),  # (m = 19: right-looking again)
 ])
 @pytest.mark.parametrize("algo", ["auto", "wave"])
 def test_matern_sweep_vs_oracle(lib, dev, c_oracle, nu, theta, m, dim, algo):
