@@ -66,9 +66,9 @@ constexpr int kPairbDedupMax = 17;
 // Matern-3/2, tau2 = 0, m = 8, beyond the 1e-10 bound.)
 // Scalar-pivot LDL^T in the 2x2-blocked layout (reciprocals, unit factor) instead of the Cholesky factor
 // (inverse square roots) for the right-looking kernels: -44 VALU per wave at m = 15 (-1.7 %), -0.6 % time
-// (same-box A/B), every GPU parity test unchanged; except at m = 18 (the blocks kind there),
-// where the two-wave register budget is tight (80 -> 216 B of scratch).
-constexpr int kPairbSldlSkipM = 18;
+// (same-box A/B), every GPU parity test unchanged.  (Until round 6 the right-looking Matern-nu / blocks kernels
+// at m = 18 kept the Cholesky form: the two-wave register budget was tight there, 80 -> 216 B of scratch;
+// every kind is left-looking at m = 18 now.)
 // Left-looking elimination (m in [kPairbLeftMin, 32], the fused kinds): column pair by column pair, each
 // column's covariances evaluated when it is reached and updated from the finished columns, so the trailing
 // block and every coordinate are never live at once; the finished factor rows 0..KL-1 wait in LDS for the
@@ -88,16 +88,18 @@ constexpr int kPairbLeftLdsRows1W = 7;  // ... and at one wave per SIMD (with th
 // (two waves, 736 B of scratch); from m = 19 its table evaluation's registers spill in the left-looking form
 // (224 - 1,344 B per lane at m = 20..24) and the right-looking one-wave kernel is faster: m = 19 0.699 vs 0.688,
 // m = 20 0.890 vs 0.780, m = 24 2.56 vs 1.31 (profiles/r06n, nu = 1.3).  (At two waves per SIMD the
-// left-looking Matern kernel spilled 1-2 KB per lane.)  The covariance-blocks kind stays right-looking: its
-// entries come from the caller's block array, whose per-column reads a left-looking form would put on the
-// column loop's critical path.
+// left-looking Matern kernel spilled 1-2 KB per lane.)  The covariance-blocks kind is left-looking at m = 18..24:
+// column pair u's entries are read from the caller's block array when the column is reached -- 0.50 / 0.53 /
+// 0.54 / 1.28 / 1.56 / 2.41 / 2.71 ms per 10^6 rows at m = 18..24 against 1.19 / 1.76 / 2.04 / 2.07 / 2.44 / 2.48 /
+// 2.83 right-looking (profiles/r06p; m = 18..20 at two waves without spills); the four-lane kernel keeps 25..32.
 constexpr int kPairbLeftMaternM = 18;
 constexpr int kPairbLeftLdsRowsMT = 6;
 constexpr bool pairb_left(int m) { return m >= kPairbLeftMin && m <= 32; }
-// the same for a kernel of covariance kind `kind` (the covariance-blocks kernels are right-looking, the
-// Matern-table ones left-looking at m = kPairbLeftMaternM only)
+// the same for a kernel of covariance kind `kind` (the Matern-table kernels left-looking at m =
+// kPairbLeftMaternM only, the covariance-blocks ones up to m = 24: the four-lane kernel serves them above)
 constexpr bool pairb_lk(int m, int kind) {
-    return pairb_left(m) && kind != NNGP_KIND_BLOCKS && (kind != NNGP_KIND_MATERN || m == kPairbLeftMaternM);
+    return pairb_left(m) && (kind != NNGP_KIND_MATERN || m == kPairbLeftMaternM) &&
+           (kind != NNGP_KIND_BLOCKS || m <= 24);
 }
 // static per-phase budgets (tools/isa_phases.py): tools/variants/phases.h defines NNGP_PHASE to fence the
 // phases with named markers (hipcc -include tools/variants/phases.h); a product build leaves them empty
@@ -119,7 +121,7 @@ __device__ __forceinline__ double pr_pick(uint32_t mask1, double v1, double v0) 
 }
 
 // Occupancy: up to m = kPairbTwoWavesMax the compiler is asked for two waves per SIMD (<= 256 VGPRs):
-// m = 16 / 17 fit without spills; m = 18 (the right-looking blocks kind) spills 20 dwords and
+// m = 16 / 17 fit without spills; m = 18 (the right-looking blocks kind, round 5) spilled 20 dwords and
 // still runs ~30 % faster than at one wave per SIMD (0.314 vs 0.435 ms per 10^6 rows, profiles/r02ap).  From
 // m = 20 (342 VGPRs) the right-looking kernels' forced spills (91 dwords) cost more than the second wave gains
 // (+52 % at m = 20, 2-3x at m = 22 / 24).  Three waves per SIMD (<= 168 VGPRs) up to m = kPairbThreeWavesMax:
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
     __shared__ __attribute__((aligned(16))) double wsl[PL ? kPairbWaves * PSL / 8 : 1];
     // (no value column in the elimination: the residual is r = v_i - B v_N after the back-substitution, the
     // oracle's own formula -- 5 % fewer VALU at m = 15 than forward-solving the values through it)
-    constexpr bool SLDL = !LEFT && M != kPairbSldlSkipM;
+    constexpr bool SLDL = !LEFT;
     constexpr int KL0 = MT ? kPairbLeftLdsRowsMT
                            : (M >= kPairbLeftOneWaveMin ? kPairbLeftLdsRows1W : kPairbLeftLdsRows);
     constexpr int KL = !LEFT ? 0 : (KL0 < M / 2 - 1 ? KL0 : M / 2 - 1);
@@ -635,11 +637,11 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             const int stale = h != ck ? 1 : 0;
             stale_plan = (stale | __builtin_amdgcn_mov_dpp(stale, 0xB1, 0xf, 0xf, true)) != 0;  // either lane of the pair
         }
+        // ---- covariances from the caller's blocks (CM), own-parity-first order.  vm: bit a set when
+        // joint row a holds a point (a valid neighbour slot, or a = M); this lane's rows, then the
+        // partner's by one swap
+        uint32_t vm = 0;
         if constexpr (CM) {
-            // ---- covariances from the caller's blocks, own-parity-first order.  vm: bit a set when
-            // joint row a holds a point (a valid neighbour slot, or a = M); this lane's rows, then the
-            // partner's by one swap
-            uint32_t vm = 0;
 #pragma unroll
             for (int s = 0; s < NP; ++s) {
                 const int a = 2 * s + q;
@@ -647,17 +649,19 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                 vm |= ok ? (1u << a) : 0u;
             }
             vm |= (uint32_t)__builtin_amdgcn_mov_dpp((int)vm, 0xB1, 0xf, 0xf, true);
-            const double* cb = cblk + rl;
-            // lane 0 reads entry (a0, b0), lane 1 (a1, b1) -- compile-time after unrolling, so each load
-            // costs two selects and an address multiply-add; 0 unless both rows hold points
-            auto ldc2 = [&](int a0, int b0, int a1, int b1) -> double {
-                const int e0 = (a0 * (a0 + 1) >> 1) + b0, e1 = (a1 * (a1 + 1) >> 1) + b1;
-                const uint32_t need = q1 ? ((1u << a1) | (1u << b1)) : ((1u << a0) | (1u << b0));
-                const bool ok = (vm & need) == need;
-                const int64_t e = ok ? (q1 ? e1 : e0) : 0;  // an in-range address either way (branch-free)
-                const double v = cb[e * n_rows];
-                return ok ? v : 0.0;
-            };
+        }
+        const double* cb = cblk + rl;
+        // lane 0 reads entry (a0, b0), lane 1 (a1, b1) -- compile-time after unrolling, so each load
+        // costs two selects and an address multiply-add; 0 unless both rows hold points
+        auto ldc2 = [&](int a0, int b0, int a1, int b1) -> double {
+            const int e0 = (a0 * (a0 + 1) >> 1) + b0, e1 = (a1 * (a1 + 1) >> 1) + b1;
+            const uint32_t need = q1 ? ((1u << a1) | (1u << b1)) : ((1u << a0) | (1u << b0));
+            const bool ok = (vm & need) == need;
+            const int64_t e = ok ? (q1 ? e1 : e0) : 0;  // an in-range address either way (branch-free)
+            const double v = cb[e * n_rows];
+            return ok ? v : 0.0;
+        };
+        if constexpr (CM && !LEFT) {
 #pragma unroll
             for (int s = 0; s < NP; ++s) {
                 const int a0 = 2 * s, a1 = 2 * s + 1;
@@ -837,6 +841,17 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
             double pnext[DA], wpnext = 0.0;  // pair u+1's partner coordinates / within-pair entry
 #pragma unroll
             for (int u = 0; u < NP; ++u) {
+                if constexpr (CM) {  // column pair u's entries from the caller's blocks
+#pragma unroll
+                    for (int s = u + 1; s < NP; ++s) {
+                        R[s][u][0] = ldc2(2 * s, 2 * u, 2 * s + 1, 2 * u + 1);      // (a, 2u + q)
+                        R[s][u][1] = ldc2(2 * s, 2 * u + 1, 2 * s + 1, 2 * u);      // (a, 2u + 1 - q)
+                    }
+                    const double dg = ldc2(2 * u, 2 * u, 2 * u + 1, 2 * u + 1);
+                    R[u][u][0] = ((vm >> (2 * u + q)) & 1u) ? dg : 1.0;  // a decoupled row: identity
+                    const double wv = ldc2(2 * u, 2 * u, 2 * u + 1, 2 * u);  // (2u+1, 2u), read from lane 1 only
+                    R[u][u][1] = q1 ? wv : 0.0;
+                } else {
                 double pu[DA];
 #pragma unroll
                 for (int k = 0; k < DA; ++k) pu[k] = (u % 2 == 1) ? pnext[k] : pr_swap(o[u][k]);
@@ -863,6 +878,7 @@ __global__ __launch_bounds__(kPairbThreads) NNGP_PAIRB_ATTR void bf_pairb(const 
                     R[u][u][1] = wpnext;
                 } else {
                     R[u][u][1] = nngp_cov_unit<KIND>(Pc, ctab, point_d2<DA>(o[u], pu));  // (2u+1, 2u): lane 1's
+                }
                 }
 #pragma unroll
                 for (int t = 0; t < u; ++t) {

@@ -70,7 +70,7 @@ def _check(B, F, p, Bo, Fo, po, n):
 
 
 @pytest.mark.parametrize("form", ["torch", "numpy", "loop"])
-@pytest.mark.parametrize("m", [1, 6, 15, 24, 25, 28, 32])
+@pytest.mark.parametrize("m", [1, 6, 15, 18, 19, 20, 21, 22, 23, 24, 25, 28, 32])  # 18..24: left-looking (round 6)
 def test_callable_sweep_vs_oracle(dev, form, m):
     from pynngp_amd import CallableCovariance, _lib
     from pynngp_amd.nngp import _sweep_any

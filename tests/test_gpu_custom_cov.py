@@ -42,7 +42,8 @@ def _sweep(lib, cov, c, nb, v=None, order=None):
 
 @pytest.mark.parametrize("kind,theta,m", [("exponential", (1.0, 20.0, 0.1), 15), ("matern32", (1.3, 12.0, 0.05), 10),
                                           ("gaussian", (0.9, 8.0, 0.2), 20), ("exponential", (1.0, 30.0, 0.0), 24),
-                                          ("spherical", (1.1, 6.0, 0.1), 5)])
+                                          ("spherical", (1.1, 6.0, 0.1), 5), ("matern32", (1.0, 15.0, 0.05), 18),
+                                          ("exponential", (1.2, 25.0, 0.1), 21), ("gaussian", (1.0, 6.0, 0.3), 23)])
 def test_custom_equals_builtin_kind(lib, dev, c_oracle, kind, theta, m):
     from pynngp_amd import Covariance, IsotropicCovariance
 
