@@ -46,7 +46,9 @@ def _residuals(nbr, B, w):
     (400, 5, 1.3, 0.2, False, 64, "tiles"), (3000, 15, 2.0, 1.0, False, 256, "tiles"),
     (3000, 10, 0.7, 0.05, True, 512, "tiles"), (20000, 15, 1.0, 0.1, False, 2048, "tiles"),
     (400, 5, 1.3, 0.2, False, 64, "colour"), (3000, 15, 2.0, 1.0, True, 256, "colour"),
-    (20000, 15, 1.0, 0.1, False, 2048, "colour")])
+    (20000, 15, 1.0, 0.1, False, 2048, "colour"),
+    (1, 3, 1.0, 0.5, False, 16, "tiles"), (2, 1, 0.8, 0.3, True, 16, "tiles"),  # no / one reverse entry
+    (37, 1, 1.1, 0.2, False, 4, "colour")])
 def test_tiled_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted, tile_nodes, coarse):
     """One tiled sweep with given normals equals the dense full-conditional sweep in the plan's order
     (coarse="colour": the nodes above level 0 swept after the tiles, one launch per colour)."""
@@ -54,8 +56,8 @@ def test_tiled_sweep_matches_dense_oracle(dev, n, m, sigma2, tau2, weighted, til
 
     s = _setup(dev, n, m, seed=n + m, tile_nodes=tile_nodes, coarse=coarse)
     tp = s["tp"]
-    assert len(tp.phases) >= 2
-    if coarse == "colour":
+    assert len(tp.phases) >= (2 if n > 100 else 1)
+    if coarse == "colour" and n > 100:
         assert tp.coarse_members is not None and tp.coarse_members.numel() > 0
     rng = s["rng"]
     yres = torch.from_numpy(rng.standard_normal(n) * 1.5).to(dev)
