@@ -12,13 +12,18 @@ concurrently, each by one workgroup holding its footprint's r (and its nodes' w)
 every colour of its nodes in order with a block barrier between colours; a greedy colouring of the
 tiles' overlap graph gives the phases (one launch each).  Nodes whose children are far (the first
 points of a generation-ordered field, whose prior neighbour sets are sparse) would make the footprints
-overlap widely: they go to coarser levels (cells 4x wider each level) swept after the finer ones.
+overlap widely: they go to coarser levels (cells 4x wider each level) swept after the finer ones, or
+(coarse="colour", SeqNNGP's default) one launch per colour after the tiles.
+
+Measured (profiles/r06i-r06r): the tiled sweep moves a third of the colour sweep's L2 bytes
+and takes the same time -- both are chains of dependent steps (a tile's ~30 steps in series, ~1.45 us each
+with their loads removed; a colour launch ~15 us), not byte-bound -- so SeqNNGP keeps the colour sweep by
+default and this one is opt-in (``SeqNNGP(sweep="tiled")``).
 
 Any order in which every node is drawn once from its full conditional given the current values, with
 no two dependent nodes drawn concurrently, is a valid Gibbs scan: here the order is (level, phase,
 colour), and the dense oracle reproduces it as a colouring (``TilePlan.effective_colors``).
 """
-import math
 from dataclasses import dataclass
 from typing import List
 
