@@ -623,15 +623,25 @@ class SeqNNGP:
                 "priors": {k: list(v) for k, v in dataclasses.asdict(self.priors).items()},
                 "n_t": self.n_t, "n_obs": self.n_obs, "n_colors": int(self.n_colors)}
 
-    def _fingerprint(self) -> str:
+    def _fingerprint(self, node_order: bool = True) -> str:
         """sha256 over the sampler's data (coordinates, responses, covariates, noise weights,
-        neighbour sets, all in storage order) and settings: a checkpoint resumes only into a
-        sampler built on the same inputs."""
+        neighbour sets) and settings: a checkpoint resumes only into a sampler built on the same
+        inputs.  node_order: the arrays in the model's node order with node labels (round 6), so a
+        checkpoint moves between storage orders (the colour sweep's Z-order, the tiled sweep's plan
+        order); False: the storage-order arrays, as checkpoints before round 6 recorded them."""
         import hashlib
         import json
 
         h = hashlib.sha256()
-        for t in (self.coords, self.y, self.X, self.nbr, self.noise_w, getattr(self, "_cblocks", None)):
+        arrays = (self.coords, self.y, self.X, self.nbr, self.noise_w, getattr(self, "_cblocks", None))
+        if node_order:
+            pos, perm = self.pos, self.perm
+            nb = self.nbr[pos].long()
+            nbr_nodes = torch.where(nb >= 0, perm[nb.clamp(min=0)], -1).to(torch.int32)
+            cb = getattr(self, "_cblocks", None)
+            arrays = (self.coords[pos], self.y[pos], self.X[pos], nbr_nodes,
+                      None if self.noise_w is None else self.noise_w[pos], None if cb is None else cb[:, pos])
+        for t in arrays:
             h.update(b"none" if t is None else t.contiguous().cpu().numpy().tobytes())
         h.update(json.dumps(self._settings(), sort_keys=True).encode())
         return h.hexdigest()
@@ -647,7 +657,7 @@ class SeqNNGP:
                 "iteration": self.iteration, "n_accept": self.n_accept, "n_notpd_reject": self.n_notpd_reject,
                 "sigma2": self.sigma2, "tau2": self.tau2, "phi": self.phi, "sum_logF": self.sum_logF,
                 "quad": self.quad, "rng": self.rng.bit_generator.state, "settings": self._settings(),
-                "fingerprint": self._fingerprint()}
+                "fingerprint_nodes": self._fingerprint()}
         np.savez(path, w=self.w[self.pos].cpu().numpy(), r=self.r[self.pos].cpu().numpy(), beta=np.asarray(self.beta),
                  y_unobserved=self.y_unobserved.cpu().numpy(), meta=np.array(json.dumps(meta)))
 
@@ -668,12 +678,17 @@ class SeqNNGP:
             for k, v in meta.get("settings", {}).items():
                 if mine.get(k) != v:
                     raise ValueError(f"checkpoint setting {k}={v!r} does not match this sampler's {mine.get(k)!r}")
-            if "fingerprint" not in meta:
+            if "fingerprint_nodes" in meta:
+                same = meta["fingerprint_nodes"] == self._fingerprint()
+            elif "fingerprint" in meta:  # (pynngp_amd 0.2 - 0.3: storage order)
+                same = meta["fingerprint"] == self._fingerprint(node_order=False)
+            else:
                 import warnings
 
                 warnings.warn("checkpoint predates the data fingerprint (pynngp_amd < 0.2): only sizes, kind, seed "
                               "and settings were compared -- make sure it was written on the same data", stacklevel=2)
-            elif meta["fingerprint"] != self._fingerprint():
+                same = True
+            if not same:
                 raise ValueError("checkpoint was written by a sampler built on different data (coordinates, "
                                  "responses, covariates, noise weights or neighbour sets) or settings")
             to = lambda a: torch.as_tensor(a).to(self.device)  # noqa: E731

@@ -206,12 +206,27 @@ def test_checkpoint_resume_bit_identical(dev, tmp_path, with_ref):
     with np.load(tmp_path / "ck.npz", allow_pickle=False) as z:
         arrs = {k: z[k] for k in z.files}
     meta = json.loads(str(arrs["meta"]))
-    del meta["fingerprint"]
+    del meta["fingerprint_nodes"]
     arrs["meta"] = np.array(json.dumps(meta))
     np.savez(tmp_path / "ck_old.npz", **arrs)
     with pytest.warns(UserWarning, match="predates the data fingerprint"):
         c = SeqNNGP(t, y, **kw).restore(tmp_path / "ck_old.npz")
     assert c.iteration == 6
+    # a 0.2 - 0.3 checkpoint (storage-order fingerprint) restores into the same storage order
+    meta["fingerprint"] = a._fingerprint(node_order=False)
+    arrs["meta"] = np.array(json.dumps(meta))
+    np.savez(tmp_path / "ck_03.npz", **arrs)
+    assert SeqNNGP(t, y, **kw).restore(tmp_path / "ck_03.npz").iteration == 6
+    # the node-order fingerprint lets a checkpoint move between storage orders: into the tiled sweep's
+    # sampler (its rows in the tile plan's order), the same state in node order
+    d = SeqNNGP(t, y, **kw, sweep="tiled").restore(tmp_path / "ck.npz")
+    assert d.iteration == 6 and not torch.equal(d.perm, a.perm)
+    e = SeqNNGP(t, y, **kw).restore(tmp_path / "ck.npz")
+    np.testing.assert_array_equal(d.w[d.pos].cpu().numpy(), e.w[e.pos].cpu().numpy())
+    np.testing.assert_array_equal(d.r[d.pos].cpu().numpy(), e.r[e.pos].cpu().numpy())
+    for _ in range(3):
+        d.step()
+    assert np.all(np.isfinite(d.w.cpu().numpy()))
 
 
 def test_reference_set_rejects_repeated_points(dev):
