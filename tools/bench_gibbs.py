@@ -31,6 +31,8 @@ ap.add_argument("--backend", default="nccl")
 ap.add_argument("--graphs", type=int, default=None, help="single chain: 1/0 forces the HIP-graph colour loop on/off")
 ap.add_argument("--sweep", default="colour", choices=["colour", "tiled"],
                 help="the w sweep: one launch per colour, or the tiled sweep (gibbs_tiles.py, one launch per phase)")
+ap.add_argument("--sweep-only", action="store_true", help="time only the w sweep (no iterations: timing probes "
+                                                             "whose values are wrong)")
 ap.add_argument("--tile-nodes", type=int, default=None, help="--sweep tiled: nodes per level-0 tile")
 ap.add_argument("--tile-levels", type=int, default=None, help="--sweep tiled: at most this many tile levels")
 args = ap.parse_args()
@@ -69,13 +71,13 @@ else:
     g = SeqNNGP(coords, y, m=args.m, sigma2=1.0, tau2=0.1, phi=30.0, seed=1 + rank, device=dev, sweep=args.sweep)
 torch.cuda.synchronize()
 setup_s = time.perf_counter() - t0
-for _ in range(args.warmup):
+for _ in range(0 if args.sweep_only else args.warmup):
     g.step()
 torch.cuda.synchronize()
 if grouped:
     dist.barrier()
 t0 = time.perf_counter()
-for _ in range(args.iters):
+for _ in range(0 if args.sweep_only else args.iters):
     g.step()
 torch.cuda.synchronize()
 if grouped:
@@ -112,8 +114,8 @@ if rank == 0:
     chains = 1 if args.single_chain else world
     what = "ONE chain sharded over the GPUs" if args.single_chain else "one chain per GPU"
     print(json.dumps({"workload": f"SeqNNGP Gibbs, N={args.n}, m={args.m}, exponential, {what}", **extra,
-                      "chains": chains, "chain_iters_per_s": chains * args.iters / el, "iters": args.iters, "ms_per_iter": 1e3 * el / args.iters, "iters_per_s": args.iters / el,
-                  "locations_per_s": args.n * args.iters / el, "setup_s": setup_s, "n_colors": int(g.n_colors),
+                      "chains": chains, "chain_iters_per_s": chains * args.iters / max(el, 1e-9), "iters": args.iters, "ms_per_iter": 1e3 * el / max(args.iters, 1), "iters_per_s": args.iters / max(el, 1e-9),
+                  "locations_per_s": args.n * args.iters / max(el, 1e-9), "setup_s": setup_s, "n_colors": int(g.n_colors),
                   "phi": g.phi, "sigma2": g.sigma2, "tau2": g.tau2, "accept": g.n_accept / max(1, g.iteration)}))
 if grouped:
     dist.destroy_process_group()
