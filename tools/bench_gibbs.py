@@ -31,6 +31,8 @@ ap.add_argument("--backend", default="nccl")
 ap.add_argument("--graphs", type=int, default=None, help="single chain: 1/0 forces the HIP-graph colour loop on/off")
 ap.add_argument("--sweep", default="colour", choices=["colour", "tiled"],
                 help="the w sweep: one launch per colour, or the tiled sweep (gibbs_tiles.py, one launch per phase)")
+ap.add_argument("--graph-probe", action="store_true", help="also time the w sweep replayed from a captured HIP "
+                "graph (timing probe: sigma2 / tau2 frozen at capture)")
 ap.add_argument("--sweep-only", action="store_true", help="time only the w sweep (no iterations: timing probes "
                                                              "whose values are wrong)")
 ap.add_argument("--tile-nodes", type=int, default=None, help="--sweep tiled: nodes per level-0 tile")
@@ -100,8 +102,27 @@ if not args.single_chain:
     e1.record()
     torch.cuda.synchronize()
     w_sweep_ms = e0.elapsed_time(e1) / 100
+    if args.graph_probe:
+        gr = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            w_sweep()
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(gr):
+            w_sweep()
+        for _ in range(10):
+            gr.replay()
+        e0.record()
+        for _ in range(100):
+            gr.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        w_sweep_graph_ms = e0.elapsed_time(e1) / 100
 if rank == 0:
     extra = {"sweep": args.sweep, "w_sweep_ms": w_sweep_ms}
+    if args.graph_probe:
+        extra["w_sweep_graph_ms"] = w_sweep_graph_ms
     if getattr(g, "_tiles", None) is not None:
         tp = g._tiles
         extra.update(tiles=int(tp.tinfo.shape[0]), tile_launches=len(tp.phases), tile_levels=tp.levels,
