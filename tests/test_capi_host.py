@@ -266,3 +266,30 @@ def test_gibbs_chains_entry_points_reject(lib):
     assert lib.nngp_gibbs_w_sweep_chains_il(*args(C, P(1032), P(2048))) == -1
     assert "16-byte" in lib.nngp_last_error().decode()
     assert lib.nngp_gibbs_w_sweep_chains(*args(0, arr, arr)) == -1
+
+
+def test_gibbs_tiles_entry_point_rejects(lib):
+    """nngp_gibbs_w_sweep_tiles validates before any device call: nulls, sizes, the step-entry cap, tinfo
+    alignment, phase offsets and LDS, the variances."""
+    P = ctypes.c_void_p
+    I32 = ctypes.c_int32
+    poff = (I32 * 3)(0, 2, 3)
+    plds = (I32 * 2)(4096, 8192)
+
+    def call(tiles=P(256), po=poff, pl=plds, n_phases=2, tinfo=P(256), ecap=768, n=10, m=3, n_entries=20,
+             sigma2=1.0, tau2=0.5, rev_loc=P(256), w=P(256)):
+        return lib.nngp_gibbs_w_sweep_tiles(tiles, po, pl, n_phases, tinfo, P(256), ecap, P(256), P(256), rev_loc,
+                                            P(256), n, m, n_entries, sigma2, tau2, P(256), None, w, P(256), P(256),
+                                            None)
+
+    assert call(tiles=None) == -1 and "null" in lib.nngp_last_error().decode()
+    assert call(w=None) == -1
+    assert call(rev_loc=None) == -1  # entries need their local slots
+    assert call(n_entries=31) == -1 and "n_entries" in lib.nngp_last_error().decode()  # > n * m
+    assert call(m=64) == -1
+    assert call(ecap=2049) == -1 and "ecap" in lib.nngp_last_error().decode()
+    assert call(tinfo=P(264)) == -1 and "16-byte" in lib.nngp_last_error().decode()
+    assert call(po=(I32 * 3)(0, 2, 1)) == -1 and "decrease" in lib.nngp_last_error().decode()
+    assert call(pl=(I32 * 2)(4096, 160 * 1024 + 16)) == -1 and "LDS" in lib.nngp_last_error().decode()
+    assert call(tau2=0.0) == -1 and "tau2" in lib.nngp_last_error().decode()
+    assert call(sigma2=float("inf")) == -1
