@@ -31,6 +31,9 @@
 #define MOV32(x) asm volatile("v_mov_b32 %0, %1" : "=v"(x) : "v"(x));
 #define MOV64(x) asm volatile("v_mov_b64 %0, %1" : "=v"(x) : "v"(x));
 #define MIN64(x) asm volatile("v_min_f64 %0, %0, %1" : "+v"(x) : "v"(b));
+#define RSQ32(f) asm volatile("v_rsq_f32 %0, %0" : "+v"(f));
+#define CVTF(x, f) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(f) : "v"(x));
+#define CVTD(x, f) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(x) : "v"(f));
 
 // 16-instruction bodies
 #define BODY_fma64 D8(FMA64) D8(FMA64)
@@ -56,6 +59,12 @@
     FMA64(d6) FMA64(d7) FMA64(d0) DPP32(f2) FMA64(d1) FMA64(d2) FMA64(d3) DPP32(f3)
 #define BODY_rsq64_fma64x7 RSQ64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d4) FMA64(d5) FMA64(d6) FMA64(d7) \
     RSQ64(d1) FMA64(d0) FMA64(d2) FMA64(d3) FMA64(d4) FMA64(d5) FMA64(d6) FMA64(d7)
+// round 6: an fp64 reciprocal square root seeded through fp32 (cvt, v_rsq_f32, cvt) against v_rsq_f64
+#define BODY_rsq32 F8(RSQ32) F8(RSQ32)
+#define BODY_cvt_pair CVTF(d0, f0) CVTF(d1, f1) CVTF(d2, f2) CVTF(d3, f3) CVTF(d4, f4) CVTF(d5, f5) CVTF(d6, f6) \
+    CVTF(d7, f7) CVTD(d0, f0) CVTD(d1, f1) CVTD(d2, f2) CVTD(d3, f3) CVTD(d4, f4) CVTD(d5, f5) CVTD(d6, f6) CVTD(d7, f7)
+#define BODY_rsq32seq_fma64x5 CVTF(d0, f0) FMA64(d1) FMA64(d2) RSQ32(f0) FMA64(d3) FMA64(d4) CVTD(d0, f0) FMA64(d5) \
+    CVTF(d6, f1) FMA64(d1) FMA64(d2) RSQ32(f1) FMA64(d3) FMA64(d4) CVTD(d6, f1) FMA64(d5)
 // dependent pairs: 4 chains of fma64 (ILP 4) and 2 chains (ILP 2)
 #define BODY_fma64_ilp4 FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) \
     FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3) FMA64(d0) FMA64(d1) FMA64(d2) FMA64(d3)
@@ -90,7 +99,8 @@
 KERNEL(fma64) KERNEL(mul64) KERNEL(rsq64) KERNEL(rcp64) KERNEL(dpp32) KERNEL(and32) KERNEL(lshladd32)
 KERNEL(bfi32) KERNEL(fma32) KERNEL(cnd32) KERNEL(fma64_dpp32) KERNEL(fma64_and32) KERNEL(fma64_bfi32)
 KERNEL(fma64x3_dpp32) KERNEL(rsq64_fma64x7) KERNEL(fma64_ilp4) KERNEL(fma64_ilp2) KERNEL(fma64_ilp1)
-KERNEL(cnds) KERNEL(mov32) KERNEL(mov64) KERNEL(min64) KERNEL(fma64_cnds)
+KERNEL(cnds) KERNEL(mov32) KERNEL(mov64) KERNEL(min64) KERNEL(fma64_cnds) KERNEL(rsq32) KERNEL(cvt_pair)
+KERNEL(rsq32seq_fma64x5)
 
 int main() {
     struct K { const char* n; void (*f)(long long*, double*, int); } ks[] = {
@@ -101,7 +111,8 @@ int main() {
         {"fma64x3+dpp32 (3:1)", k_fma64x3_dpp32}, {"rsq64+fma64x7 (1:7)", k_rsq64_fma64x7},
         {"fma64 ILP4", k_fma64_ilp4}, {"fma64 ILP2", k_fma64_ilp2}, {"fma64 ILP1", k_fma64_ilp1},
         {"cndmask_e64 (sgpr mask)", k_cnds}, {"mov32", k_mov32}, {"mov64", k_mov64}, {"min64", k_min64},
-        {"fma64+cndmask_e64 (1:1)", k_fma64_cnds}};
+        {"fma64+cndmask_e64 (1:1)", k_fma64_cnds}, {"rsq32", k_rsq32}, {"cvt f64>f32>f64", k_cvt_pair},
+        {"(cvt,rsq32,cvt)x2+fma64x10", k_rsq32seq_fma64x5}};
     const int cus = 256, iters = 2048;
     const size_t lds = 96 * 1024;
     long long* cyc;
