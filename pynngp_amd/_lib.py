@@ -894,6 +894,12 @@ def gibbs_w_sweep_tiles(plan, prep: torch.Tensor, m: int, sigma2: float, tau2: f
                          "store the field in plan.tnodes order and rebuild the plan there")
     if plan.tnodes.numel() != w.shape[0]:
         raise ValueError(f"the tile plan covers {plan.tnodes.numel()} nodes, the field has {w.shape[0]}")
+    key = (w.shape[0], off.data_ptr())
+    if getattr(plan, "_bounds_ok", None) != key:  # what the kernel indexes unchecked, once per plan and field
+        from .gibbs_tiles import validate_launch_bounds
+
+        validate_launch_bounds(plan, off, w.shape[0])
+        plan._bounds_ok = key
     tiles, poff, plds = plan.launch_arrays()
     _check(load().nngp_gibbs_w_sweep_tiles(_ptr(tiles), poff.ctypes.data, plds.ctypes.data, len(plds),
                                            _ptr(plan.tinfo), _ptr(plan.tstep), int(plan.ecap), _ptr(plan.tfp),

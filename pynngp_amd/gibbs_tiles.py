@@ -372,6 +372,70 @@ def contiguous_plan(coords: torch.Tensor, nbr: torch.Tensor, colors: torch.Tenso
     return perm, nbr2, off2, rev_j2, rev_k2, tp
 
 
+def validate_launch_bounds(tp: TilePlan, off: torch.Tensor, n: int) -> None:
+    """What gibbs_tile_phase indexes without a check of its own, verified once per plan and field (the C ABI
+    checks only sizes; :func:`pynngp_amd._lib.gibbs_w_sweep_tiles` calls this): the launched tiles' row,
+    footprint and step ranges inside their arrays, footprint node ids in [0, n) with each footprint starting
+    with its tile's rows, step starts increasing from 0 with <= STEP_MEMBERS members and <= ecap reverse
+    entries each, every entry's local index inside its tile's footprint, and each launch's LDS bytes covering
+    its tiles.  Raises ValueError."""
+    def bad(msg):
+        raise ValueError(f"tile plan does not fit the tiled sweep kernel: {msg}")
+
+    if tp.tinfo.dtype != torch.int32 or tp.tinfo.dim() != 2 or tp.tinfo.shape[1] != 8:
+        bad("tinfo must be int32 (n_tiles, 8)")
+    if not 0 <= int(tp.ecap) <= MAX_ECAP:
+        bad(f"ecap={tp.ecap} outside [0, {MAX_ECAP}]")
+    tiles, poff, plds = tp.launch_arrays()
+    if tiles.numel() == 0:
+        return
+    dev = tp.tinfo.device
+    ar = lambda k: torch.arange(k, device=dev)  # noqa: E731
+    tl = tiles.long().to(dev)
+    if int(tl.min()) < 0 or int(tl.max()) >= tp.tinfo.shape[0]:
+        bad("tile ids outside the plan")
+    n0, n1, f0, f1, s0, s1 = tp.tinfo.long()[tl].unbind(1)[:6]
+    nn, nf, S = n1 - n0, f1 - f0, s1 - s0
+    if bool(((n0 < 0) | (nn < 0) | (n1 > n)).any()):
+        bad("tile rows outside [0, n)")
+    if bool(((f0 < 0) | (nf < nn) | (f1 > tp.tfp.numel())).any()):
+        bad("footprint ranges")
+    if bool(((s0 < 0) | (S < (nn > 0).long()) | (s1 > tp.tstep.numel())).any()):
+        bad("step ranges")
+    offl = off.long().to(dev)
+    if offl.numel() != n + 1 or tp.rev_loc.numel() < int(offl[-1]):
+        bad("off / rev_loc do not cover the field's reverse entries")
+    fpv = tp.tfp.long()
+    if fpv.numel() and bool(((fpv < 0) | (fpv >= n)).any()):
+        bad("footprint node ids outside [0, n)")
+    seg = lambda cnt: torch.repeat_interleave(ar(cnt.numel()), cnt)  # noqa: E731
+    within = lambda cnt: ar(int(cnt.sum())) - torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt)  # noqa: E731
+    rt, k = seg(nn), within(nn)  # the launched rows: tile, tile-local index
+    rows = n0[rt] + k
+    if not torch.equal(fpv[f0[rt] + k], rows):
+        bad("a footprint must start with its tile's rows")
+    qt = seg(S)
+    qi = s0[qt] + within(S)
+    st = tp.tstep.long()
+    a = st[qi]
+    b = torch.where(qi == s1[qt] - 1, nn[qt], st[(qi + 1).clamp(max=max(st.numel() - 1, 0))])
+    if bool(((a < 0) | (b <= a) | (b > nn[qt]) | ((qi == s0[qt]) & (a != 0))).any()):
+        bad("step starts must increase from 0 inside their tile")
+    if bool(((b - a) > STEP_MEMBERS).any()):
+        bad(f"a step of more than {STEP_MEMBERS} members")
+    if bool(((offl[n0[qt] + b] - offl[n0[qt] + a]) > int(tp.ecap)).any()):
+        bad(f"a step of more than ecap={tp.ecap} reverse entries")
+    cnt = offl[rows + 1] - offl[rows]
+    et = torch.repeat_interleave(rt, cnt)
+    loc = tp.rev_loc.long()[torch.repeat_interleave(offl[rows], cnt) + within(cnt)]
+    if bool(((loc < 0) | (loc >= nf[et])).any()):
+        bad("a reverse entry's local index outside its tile's footprint")
+    phase = torch.repeat_interleave(ar(len(plds)), torch.as_tensor(np.diff(poff), device=dev).long())
+    need = tile_lds_bytes(nf, nn, S, int(tp.ecap))
+    if bool((torch.as_tensor(plds, device=dev).long()[phase] < need).any()) or int(plds.max()) > 160 * 1024:
+        bad("a launch's LDS bytes do not cover its tiles (or exceed 160 KB)")
+
+
 def check_tile_plan(tp: TilePlan, off: torch.Tensor, rev_j: torch.Tensor) -> None:
     """The plan's invariants (setup check): every node in exactly one tile; within a launch the tiles'
     footprints are disjoint; each reverse entry's local index names its child in its parent's footprint."""

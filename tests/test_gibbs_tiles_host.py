@@ -135,3 +135,80 @@ def test_tile_plan_coarse_colour(c_oracle):
     eff = tp.effective_colors
     rest = np.setdiff1d(np.arange(3000), cm)
     assert eff[cm].min() > eff[rest].max()
+
+
+def _contiguous(c_oracle, n, m, tile_nodes, seed, **kw):
+    """A plan rebuilt in its own node order (what the kernel wants: tile t's nodes are rows [n0, n1))."""
+    from pynngp_amd.gibbs_tiles import build_tile_plan
+
+    nbr0, colors0, nc, tp0 = _plan(c_oracle, n, m, tile_nodes, seed, storage_perm=False, **kw)
+    c0 = np.random.default_rng(seed).uniform(size=(n, 2))
+    perm = tp0.tnodes.numpy().astype(np.int64)
+    pos = np.empty(n, np.int64)
+    pos[perm] = np.arange(n)
+    nbr = np.where(nbr0[perm] >= 0, pos[np.maximum(nbr0[perm], 0)], -1).astype(np.int32)
+    off, rev_j = _reverse(nbr)
+    rev_j = np.concatenate([rev_j, np.zeros(n * m - rev_j.size, np.int32)])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    tp = build_tile_plan(t(c0[perm]), t(off.astype(np.int64)), t(rev_j.astype(np.int64)),
+                         t(np.asarray(colors0)[perm].astype(np.int64)), nc, nc,
+                         assign=(tp0.node_tile[t(perm)], tp0.tile_level, tp0.coarse_tile), **kw)
+    assert tp.contiguous
+    return t(off.astype(np.int64)), tp
+
+
+@pytest.mark.parametrize("coarse", ["tiles", "colour"])
+def test_launch_bounds_accepts_built_plans_and_rejects_corrupt_ones(c_oracle, coarse):
+    """validate_launch_bounds (run by gibbs_w_sweep_tiles once per plan) passes what build_tile_plan makes and
+    refuses plans the kernel would index out of range."""
+    import copy
+
+    from pynngp_amd.gibbs_tiles import validate_launch_bounds
+
+    n = 3000
+    off, tp = _contiguous(c_oracle, n, 15, 256, 3, coarse=coarse)
+    validate_launch_bounds(tp, off, n)
+    with pytest.raises(ValueError, match="rows outside|do not cover"):
+        validate_launch_bounds(tp, off, n - 1)
+
+    def corrupt(fn, match):
+        bad = copy.copy(tp)
+        bad._launch = None
+        fn(bad)
+        with pytest.raises(ValueError, match=match):
+            validate_launch_bounds(bad, off, n)
+
+    t0 = int(tp.phases[0][0])
+
+    def tfp_out(p):
+        p.tfp = p.tfp.clone()
+        p.tfp[int(p.tinfo[t0, 3]) - 1] = n
+
+    corrupt(tfp_out, "footprint node ids")
+
+    def loc_out(p):
+        p.rev_loc = p.rev_loc.clone()
+        r = int(p.tinfo[t0, 0])
+        while int(off[r + 1]) == int(off[r]):
+            r += 1
+        p.rev_loc[int(off[r])] = int(p.tinfo[t0, 3] - p.tinfo[t0, 2])
+
+    corrupt(loc_out, "local index")
+
+    def ecap_small(p):
+        p.ecap = 1
+
+    corrupt(ecap_small, "ecap")
+
+    def step_big(p):  # merge every step of the first tile into one
+        p.tstep = p.tstep.clone()
+        p.tinfo = p.tinfo.clone()
+        s0 = int(p.tinfo[t0, 4])
+        p.tinfo[t0, 5] = s0 + 1
+
+    corrupt(step_big, "members|entries")
+
+    def lds_small(p):
+        p.phase_lds = [x // 2 for x in p.phase_lds]
+
+    corrupt(lds_small, "LDS")
