@@ -838,6 +838,23 @@ def _check_noise_w(noise_w: Optional[torch.Tensor], n: int) -> None:
         raise ValueError(f"noise_w must be a contiguous float64 ({n},) tensor")
 
 
+def _check_member_rows(rows: torch.Tensor, co, n: int, n_entries: int) -> None:
+    """The colour kernels index w / r / the prep with each member row's location and reverse range unchecked:
+    verify them once per rows tensor (0 <= location < n, 0 <= first <= end <= n_entries), and the colour
+    offsets against the row count on every call."""
+    if co.size and int(co[-1]) > rows.shape[0]:  # (negative offsets: refused by the C ABI)
+        raise ValueError(f"colour offsets reach past the {rows.shape[0]} member rows")
+    key = (n, n_entries, rows.data_ptr())
+    if getattr(rows, "_nngp_bounds", None) == key:
+        return
+    if rows.shape[0]:
+        i, e0, e1 = rows[:, 0], rows[:, 1], rows[:, 2]
+        if bool(((i < 0) | (i >= n) | (e0 < 0) | (e1 < e0) | (e1 > n_entries)).any()):
+            raise ValueError("member_rows hold a location outside [0, n) or a reverse range outside the entries: "
+                             "build them with gibbs_member_rows(members, off) for this field")
+    rows._nngp_bounds = key
+
+
 def gibbs_member_rows(members: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
     """int32 (n, 4) rows (location, first / end reverse entry, 0) of the colour-ordered
     ``members`` (nngp_gibbs_member_rows): build once per colouring, pass to :func:`gibbs_w_sweep`."""
@@ -870,6 +887,7 @@ def gibbs_w_sweep(members: torch.Tensor, color_off_host, prep: torch.Tensor, m: 
         raise ValueError("member_rows must be a contiguous int32 (n, 4) tensor from gibbs_member_rows")
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
     n = w.shape[0]
+    _check_member_rows(member_rows, co, n, 0 if rev_j is None else rev_j.numel())
     _check(load().nngp_gibbs_w_sweep(_ptr(member_rows), co.ctypes.data, len(co) - 1, _ptr(prep), n, int(m),
                                      float(sigma2), float(tau2), _ptr(yres), _ptr(noise_w), _ptr(w), _ptr(r),
                                      _ptr(rev_j),
@@ -948,6 +966,7 @@ def gibbs_w_sweep_chains(member_rows: torch.Tensor, color_off_host, preps, m: in
     dev = _require_gpu(member_rows, rev_j, noise_w, *preps, *vecs, *((w, r) if il else ()))
     _check_noise_w(noise_w, n)
     co = np.ascontiguousarray(color_off_host, dtype=np.int32)
+    _check_member_rows(member_rows, co, n, 0 if rev_j is None else rev_j.numel())
     P = ctypes.c_void_p * C
     D = ctypes.c_double * C
     head = (_ptr(member_rows), co.ctypes.data, len(co) - 1, C, P(*[_ptr(t) for t in preps]), n, int(m),

@@ -532,6 +532,8 @@ int nngp_gibbs_w_sweep(const int32_t* member_rows, const int32_t* color_off_host
     if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
     if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
+    for (int c = 0; c <= n_colors; ++c)
+        if (color_off_host[c] < 0) return fail(NNGP_EINVAL, "negative colour offset");
     if (!(sigma2 > 0.0) || !(tau2 > 0.0) || !isfinite(sigma2) || !isfinite(tau2))
         return fail(NNGP_EINVAL, "need sigma2 > 0 and tau2 > 0 (finite)");
     hipError_t e = nngp::gibbs_w_sweep_launch(member_rows, n_colors, color_off_host, prep, n, m, sigma2, tau2, yres,
@@ -579,6 +581,8 @@ int nngp_gibbs_w_sweep_chains(const int32_t* member_rows, const int32_t* color_o
     if (((uintptr_t)member_rows & 15) != 0) return fail(NNGP_EINVAL, "member_rows must be 16-byte aligned");
     if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
+    for (int c = 0; c <= n_colors; ++c)
+        if (color_off_host[c] < 0) return fail(NNGP_EINVAL, "negative colour offset");
     for (int c = 0; c < chains; ++c) {
         if (prep[c] == nullptr || yres[c] == nullptr || w[c] == nullptr || r[c] == nullptr || z[c] == nullptr)
             return fail(NNGP_EINVAL, "null pointer for chain %d", c);
@@ -606,6 +610,8 @@ int nngp_gibbs_w_sweep_chains_il(const int32_t* member_rows, const int32_t* colo
         return fail(NNGP_EINVAL, "w_il / r_il must be 16-byte aligned");
     if (n_colors < 0 || n < 0 || m < 0 || m > NNGP_MAX_M) return fail(NNGP_EINVAL, "bad n_colors, n or m");
     if (n_colors > 0 && color_off_host[n_colors] > n) return fail(NNGP_EINVAL, "colour offsets exceed n");
+    for (int c = 0; c <= n_colors; ++c)
+        if (color_off_host[c] < 0) return fail(NNGP_EINVAL, "negative colour offset");
     for (int c = 0; c < chains; ++c) {
         if (prep[c] == nullptr || yres[c] == nullptr || z[c] == nullptr)
             return fail(NNGP_EINVAL, "null pointer for chain %d", c);

@@ -293,3 +293,12 @@ def test_gibbs_tiles_entry_point_rejects(lib):
     assert call(pl=(I32 * 2)(4096, 160 * 1024 + 16)) == -1 and "LDS" in lib.nngp_last_error().decode()
     assert call(tau2=0.0) == -1 and "tau2" in lib.nngp_last_error().decode()
     assert call(sigma2=float("inf")) == -1
+
+
+def test_gibbs_sweep_rejects_negative_colour_offsets(lib):
+    """A negative colour offset would index before the member rows: refused before any device call."""
+    P = ctypes.c_void_p
+    co = (ctypes.c_int32 * 3)(-4, 2, 10)
+    assert lib.nngp_gibbs_w_sweep(P(256), co, 2, P(256), 10, 3, 1.0, 0.5, P(256), None, P(256), P(256), P(256),
+                                  P(256), 0, 0, None) == -1
+    assert "negative colour offset" in lib.nngp_last_error().decode()

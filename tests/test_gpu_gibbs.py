@@ -362,3 +362,29 @@ def test_device_colouring_equals_host_greedy(dev, n, m, layout):
     np.testing.assert_array_equal(col_d.cpu().numpy(), col_h)
     if n <= 5000:
         assert G.coloring_is_valid(nbr.cpu().numpy(), col_h)
+
+
+def test_member_rows_bounds_checked(dev):
+    """member_rows from another field (a location past n, a reverse range past the entries) are refused before
+    a colour launch; good rows are checked once per tensor."""
+    from pynngp_amd import _lib
+
+    s = _setup(dev, 2000, 10, seed=3)
+    n = 2000
+    prep = _lib.gibbs_prepare(s["B"], s["F"], s["off"], s["rev_j"], s["rev_k"])
+    rows = _lib.gibbs_member_rows(s["members"], s["off"])
+    z = torch.zeros(n, dtype=torch.float64, device=dev)
+    yres = torch.zeros(n, dtype=torch.float64, device=dev)
+    args = lambda mr, co: (s["members"], co, prep, 10, 1.0, 0.5, yres, s["w"].clone(), s["R"].clone(),  # noqa: E731
+                           s["off"], s["rev_j"], 0, 0)
+    _lib.gibbs_w_sweep(*args(rows, s["color_off"]), z=z, member_rows=rows)
+    assert getattr(rows, "_nngp_bounds", None) is not None
+    for col, val in ((0, n), (2, int(s["rev_j"].numel()) + 1), (1, -1)):
+        bad = rows.clone()
+        bad[7, col] = val
+        with pytest.raises(ValueError, match="member_rows"):
+            _lib.gibbs_w_sweep(*args(bad, s["color_off"]), z=z, member_rows=bad)
+    co = s["color_off"].copy()
+    co[-1] = n + 1
+    with pytest.raises(ValueError, match="past the"):
+        _lib.gibbs_w_sweep(*args(rows, co), z=z, member_rows=rows)
